@@ -1,0 +1,254 @@
+"""CPU ORACLE — test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / the timed CPU baseline.  The product
+path (mamba-tts-project_amd/) never imports it.
+
+This is a plain-PyTorch (CPU) restatement of the arithmetic on the decoder hot
+path of whcorkran/mamba-TTS-project.  The hot-path arithmetic lives in the
+third-party ``mamba_ssm`` package, which the reference imports at
+``mamba_decoder.py:4`` and constructs with defaults at ``mamba_decoder.py:29``.
+It is NOT vendored and NOT pinned (absent from ``environment.yml:1-150``;
+``README.md:29`` names it without a version), so this file restates its
+published algorithm (mamba-ssm 1.x/2.x ``selective_scan_ref``,
+``causal_conv1d_ref``, ``Mamba.step``), and parity is pinned against golden
+vectors produced in the build container from
+  * transformers' torch-only Mamba v1 (an independent implementation of the
+    same math, ``transformers/models/mamba/modeling_mamba.py`` = ``HF``), and
+  * the reference ``mamba_decoder.py`` / ``style_cross_attention.py`` imported
+    with a ``mamba_ssm`` shim that wraps HF's mixer and honours the documented
+    ``out, state = mamba(x[, state])`` contract (``mamba_decoder.py:10-15``).
+See tests/golden/make_golden.py.
+
+Layouts follow upstream mamba-ssm: u/delta/z are (B, D, L), B/C are (B, N, L).
+Everything runs in the dtype of the inputs (tests use float64 for grads).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+# --------------------------------------------------------------------------
+# Op-level restatements
+# --------------------------------------------------------------------------
+
+def softplus(x: torch.Tensor) -> torch.Tensor:
+    """softplus with threshold 20, as torch.nn.functional.softplus and the
+    upstream CUDA kernel (``delta <= 20 ? log1p(exp(delta)) : delta``)."""
+    return torch.where(x <= 20.0, torch.log1p(torch.exp(torch.clamp(x, max=20.0))), x)
+
+
+def selective_scan_ref(u, delta, A, B, C, D=None, z=None, delta_bias=None,
+                       delta_softplus=False, h0=None, return_last_state=False):
+    """Restates [upstream] mamba_ssm/ops/selective_scan_interface.py::selective_scan_ref
+    (same math as HF:174-279, recurrent branch HF:248-268).
+
+    u, delta, z : (B, D, L)      A : (D, N)      B, C : (B, N, L)
+    D, delta_bias : (D,)         h0 : optional (B, D, N) initial state
+      delta   <- softplus(delta + delta_bias)
+      h_t      = exp(delta_t * A) * h_{t-1} + delta_t * B_t * u_t
+      y_t      = <h_t, C_t> + D * u_t ;  y_t *= silu(z_t)
+    Returns out (B, D, L) [, last_state (B, D, N)].
+    """
+    dt = delta
+    if delta_bias is not None:
+        dt = dt + delta_bias[None, :, None]
+    if delta_softplus:
+        dt = softplus(dt)
+    Bsz, Dm, L = u.shape
+    h = torch.zeros(Bsz, Dm, A.shape[1], dtype=u.dtype) if h0 is None else h0.to(u.dtype)
+    ys = []
+    for t in range(L):
+        dA = torch.exp(dt[:, :, t, None] * A[None])                      # (B, D, N)
+        dBu = dt[:, :, t, None] * B[:, None, :, t] * u[:, :, t, None]    # (B, D, N)
+        h = dA * h + dBu
+        ys.append((h * C[:, None, :, t]).sum(-1))
+    y = torch.stack(ys, dim=-1) if L > 0 else torch.zeros_like(u)
+    if D is not None:
+        y = y + u * D[None, :, None]
+    if z is not None:
+        y = y * F.silu(z)
+    return (y, h) if return_last_state else y
+
+
+def causal_conv1d_ref(x, weight, bias=None, activation=None, conv_state=None):
+    """Restates [upstream] causal_conv1d_ref (fallback HF:81-101): depthwise
+    causal conv of width K over L with left context ``conv_state`` (B, D, K)
+    (the last K pre-conv inputs; zeros when None), + bias, optional SiLU.
+
+    x : (B, D, L), weight : (D, K).  Returns (out (B, D, L), new_conv_state
+    (B, D, K)) where new_conv_state holds the last K inputs of [state ‖ x]
+    (mamba-ssm ``Mamba.forward`` prefill: ``F.pad(x, (d_conv - L, 0))``).
+    """
+    Bsz, Dm, L = x.shape
+    K = weight.shape[1]
+    prev = torch.zeros(Bsz, Dm, K, dtype=x.dtype) if conv_state is None else conv_state.to(x.dtype)
+    full = torch.cat([prev, x], dim=-1)                                  # (B, D, K+L)
+    out = torch.zeros_like(x)
+    for k in range(K):
+        # out[t] += w[k] * full[t + 1 + k]   (full index K+t is x_t)
+        out = out + weight[None, :, k, None] * full[:, :, 1 + k: 1 + k + L]
+    if bias is not None:
+        out = out + bias[None, :, None]
+    if activation in ("silu", "swish"):
+        out = F.silu(out)
+    return out, full[:, :, -K:].clone()
+
+
+def causal_conv1d_update_ref(x, conv_state, weight, bias=None, activation=None):
+    """Restates [upstream] causal_conv1d_update / Mamba.step conv part
+    (HF:61-78): roll the window, insert x (B, D), dot with weight, +b, SiLU.
+    Returns (out (B, D), new_conv_state)."""
+    st = torch.cat([conv_state[:, :, 1:], x[:, :, None]], dim=-1)
+    out = (st * weight[None]).sum(-1)
+    if bias is not None:
+        out = out + bias[None]
+    if activation in ("silu", "swish"):
+        out = F.silu(out)
+    return out, st
+
+
+def selective_state_update_ref(state, x, dt, A, B, C, D=None, z=None, dt_bias=None, dt_softplus=False):
+    """Restates [upstream] ops/triton/selective_state_update.py::selective_state_update_ref
+    (HF:128-171).  state (B, D, N), x/dt/z (B, D), B/C (B, N).
+    Returns (out (B, D), new_state)."""
+    if dt_bias is not None:
+        dt = dt + dt_bias[None]
+    if dt_softplus:
+        dt = softplus(dt)
+    dA = torch.exp(dt[..., None] * A[None])
+    dBx = dt[..., None] * B[:, None, :] * x[..., None]
+    new_state = state * dA + dBx
+    out = (new_state * C[:, None, :]).sum(-1)
+    if D is not None:
+        out = out + x * D[None]
+    if z is not None:
+        out = out * F.silu(z)
+    return out, new_state
+
+
+def layer_norm_ref(x, w, b, eps=1e-5):
+    mu = x.mean(-1, keepdim=True)
+    var = ((x - mu) ** 2).mean(-1, keepdim=True)
+    return (x - mu) / torch.sqrt(var + eps) * w + b
+
+
+def mha_ref(q_in, kv_in, in_w, in_b, out_w, out_b, n_heads, key_padding_mask=None):
+    """Restates torch nn.MultiheadAttention(batch_first=True, dropout=0) as
+    used at mamba_decoder.py:32-36,72-77 (query != key path).
+    key_padding_mask: (B, S) bool, True = ignore.  Fully masked rows -> NaN
+    (PyTorch semantics, reproduced on purpose)."""
+    Bsz, T, d = q_in.shape
+    S = kv_in.shape[1]
+    hd = d // n_heads
+    q = q_in @ in_w[:d].T + in_b[:d]
+    k = kv_in @ in_w[d:2 * d].T + in_b[d:2 * d]
+    v = kv_in @ in_w[2 * d:].T + in_b[2 * d:]
+    q = q.view(Bsz, T, n_heads, hd).transpose(1, 2)
+    k = k.view(Bsz, S, n_heads, hd).transpose(1, 2)
+    v = v.view(Bsz, S, n_heads, hd).transpose(1, 2)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
+    if key_padding_mask is not None:
+        s = s.masked_fill(key_padding_mask[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    o = (p @ v).transpose(1, 2).reshape(Bsz, T, d)
+    return o @ out_w.T + out_b
+
+
+# --------------------------------------------------------------------------
+# Module-level restatements (state_dict keys identical to the reference)
+# --------------------------------------------------------------------------
+
+def mamba_forward_ref(p: dict, prefix: str, x, state=None, d_state=16, d_conv=4):
+    """[upstream] mamba_simple.Mamba.forward / step under the contract of
+    mamba_decoder.py:10-15: returns (out (B, L, d), (conv_state (B, di, K),
+    ssm_state (B, di, N))).  p: flat dict of tensors keyed like the
+    reference state_dict."""
+    W_in = p[prefix + "in_proj.weight"]
+    di = W_in.shape[0] // 2
+    conv_w = p[prefix + "conv1d.weight"].reshape(di, -1)
+    conv_b = p[prefix + "conv1d.bias"]
+    W_x = p[prefix + "x_proj.weight"]
+    W_dt = p[prefix + "dt_proj.weight"]
+    b_dt = p[prefix + "dt_proj.bias"]
+    A = -torch.exp(p[prefix + "A_log"])
+    Dp = p[prefix + "D"]
+    W_out = p[prefix + "out_proj.weight"]
+    r = W_dt.shape[1]
+    N = A.shape[1]
+
+    xz = (x @ W_in.T).transpose(1, 2)                      # (B, 2di, L)
+    xs, z = xz[:, :di], xz[:, di:]
+    conv_state = None if state is None else state[0]
+    h0 = None if state is None else state[1]
+    u, new_conv = causal_conv1d_ref(xs, conv_w, conv_b, "silu", conv_state)
+    x_dbl = u.transpose(1, 2) @ W_x.T                      # (B, L, r+2N)
+    dt, Bm, Cm = torch.split(x_dbl, [r, N, N], dim=-1)
+    delta = (dt @ W_dt.T).transpose(1, 2)                  # (B, di, L)
+    y, last = selective_scan_ref(u, delta, A, Bm.transpose(1, 2), Cm.transpose(1, 2), Dp, z,
+                                 b_dt, True, h0=h0, return_last_state=True)
+    out = y.transpose(1, 2) @ W_out.T
+    return out, (new_conv, last)
+
+
+def decoder_layer_ref(p, prefix, x, text_hidden, z_style, text_mask, mamba_state, n_heads):
+    """Restates MambaTTSDecoderLayer.forward (mamba_decoder.py:50-91)."""
+    h = layer_norm_ref(x, p[prefix + "norm_mamba.weight"], p[prefix + "norm_mamba.bias"])
+    hm, new_state = mamba_forward_ref(p, prefix + "mamba.", h, mamba_state)
+    x = x + hm
+    h = layer_norm_ref(x, p[prefix + "norm_cross.weight"], p[prefix + "norm_cross.bias"])
+    kpm = None if text_mask is None else ~text_mask                     # :68-70 (inverted!)
+    attn = mha_ref(h, text_hidden, p[prefix + "cross_attn.in_proj_weight"],
+                   p[prefix + "cross_attn.in_proj_bias"], p[prefix + "cross_attn.out_proj.weight"],
+                   p[prefix + "cross_attn.out_proj.bias"], n_heads, kpm)
+    x = x + attn
+    h = layer_norm_ref(x, p[prefix + "norm_ff.weight"], p[prefix + "norm_ff.bias"])
+    gb = torch.tanh(z_style @ p[prefix + "style_mlp.0.weight"].T + p[prefix + "style_mlp.0.bias"])
+    gamma, beta = torch.chunk(gb, 2, dim=-1)
+    h = gamma[:, None] * h + beta[:, None]
+    f = F.gelu(h @ p[prefix + "ff.0.weight"].T + p[prefix + "ff.0.bias"])
+    x = x + (f @ p[prefix + "ff.2.weight"].T + p[prefix + "ff.2.bias"])
+    return x, new_state
+
+
+def _concat_ref(text_hidden, text_mask, ref_hidden, ref_mask):
+    """mamba_decoder.py:148-165 / 226-241."""
+    if ref_hidden is None:
+        return text_hidden, text_mask
+    B = ref_hidden.shape[0]
+    if ref_mask is None:
+        ref_mask = torch.ones(B, ref_hidden.shape[1], dtype=torch.bool)
+    text_hidden = torch.cat([ref_hidden, text_hidden], dim=1)
+    text_mask = ref_mask if text_mask is None else torch.cat([ref_mask, text_mask], dim=1)
+    return text_hidden, text_mask
+
+
+def decoder_forward_ref(p, n_layers, n_heads, audio_tokens, text_hidden, z_style,
+                        text_mask=None, ref_hidden=None, ref_mask=None):
+    """Restates MambaTTSDecoder.forward (mamba_decoder.py:120-186), 2D tokens."""
+    B, T = audio_tokens.shape
+    text_hidden, text_mask = _concat_ref(text_hidden, text_mask, ref_hidden, ref_mask)
+    x = (p["token_embed.weight"][audio_tokens] + p["pos_embed.weight"][:T][None]
+         + p["quant_embed.weight"][torch.zeros_like(audio_tokens)])
+    for i in range(n_layers):
+        x, _ = decoder_layer_ref(p, f"layers.{i}.", x, text_hidden, z_style, text_mask, None, n_heads)
+    x = layer_norm_ref(x, p["norm_out.weight"], p["norm_out.bias"])
+    return x @ p["head.weight"].T + p["head.bias"]
+
+
+def decode_step_ref(p, n_layers, n_heads, last_token, text_hidden, z_style, states, step_index,
+                    text_mask=None, ref_hidden=None, ref_mask=None):
+    """Restates MambaTTSDecoder.decode_step (mamba_decoder.py:188-256): no
+    quant_embed (quirk :217-221), pos = step_index."""
+    text_hidden, text_mask = _concat_ref(text_hidden, text_mask, ref_hidden, ref_mask)
+    x = p["token_embed.weight"][last_token] + p["pos_embed.weight"][step_index][None, None]
+    new_states = []
+    for i in range(n_layers):
+        st = None if states is None else states[i]
+        x, s = decoder_layer_ref(p, f"layers.{i}.", x, text_hidden, z_style, text_mask, st, n_heads)
+        new_states.append(s)
+    x = layer_norm_ref(x, p["norm_out.weight"], p["norm_out.bias"])
+    return x @ p["head.weight"].T + p["head.bias"], new_states
