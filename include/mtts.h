@@ -1,0 +1,240 @@
+/*
+ * mtts.h — C ABI of libmtts.so, the MI355X (gfx950) kernels behind the
+ * MambaTTSDecoder hot path of whcorkran/mamba-TTS-project.
+ *
+ * Boundary: the reference decoder calls `mamba_ssm.Mamba` (mamba_decoder.py:4,
+ * :29, :61, :63), whose CUDA extension entry points are what these functions
+ * replace.  The [upstream] mamba-ssm / causal-conv1d packages are neither
+ * vendored nor pinned by the reference (environment.yml:1-150, README.md:29),
+ * so the "reference interface" column below names the upstream pybind
+ * function each entry point stands in for, plus the reference call site.
+ *
+ * Conventions
+ *  - Plain C: pointers, sizes, element strides.  No torch types.
+ *  - Every tensor is caller-allocated device memory; the library never
+ *    allocates, frees or synchronises (safe inside hipGraph capture).
+ *  - Work is enqueued on `stream` (a hipStream_t; NULL = legacy default).
+ *  - Return 0 on success, a negative MTTS_E* code on failure; the message is
+ *    in mtts_last_error() (thread-local).
+ *  - Activations are CHANNEL-LAST: element (b, t, c) of a (B, L, C) tensor is
+ *    at  ptr[b*bstride + t*lstride + c]  (channel stride 1).  This is the
+ *    layout the projections produce; mamba-ssm's (B, D, L) layout is a
+ *    permutation of it (the math is identical).
+ *  - dtype codes: MTTS_F32 / MTTS_BF16 for activations; states, A, D,
+ *    biases, reductions and all accumulation are fp32.
+ */
+#ifndef MTTS_H
+#define MTTS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTTS_ABI_VERSION 1
+
+enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
+enum {
+  MTTS_OK = 0,
+  MTTS_EINVAL = -22,       /* bad shape / stride / dtype / null pointer   */
+  MTTS_EUNSUPPORTED = -95, /* valid but not on a built fast path          */
+  MTTS_ELAUNCH = -5        /* hipGetLastError after the launch             */
+};
+
+int mtts_abi_version(void);
+const char* mtts_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Selective scan.  Replaces [upstream] selective_scan_cuda.fwd / .bwd
+ * (mamba_ssm/ops/selective_scan_interface.py: SelectiveScanFn), reached from
+ * the reference at mamba_decoder.py:61 (full sequence) / :63 (with state).
+ *
+ *   delta <- softplus(delta + delta_bias)          (if delta_softplus)
+ *   h_t    = exp(delta_t * A) h_{t-1} + delta_t B_t u_t ,  h_{-1} = h0 or 0
+ *   y_t    = <h_t, C_t> + D u_t ;   out_t = y_t * silu(z_t)  (if z)
+ * u, delta, z, out : (B, L, D) channel-last, dtype `dtype_io`
+ * Bm, Cm           : (B, L, N) with N stride 1, dtype `dtype_bc`
+ * A                : (D, N) fp32, D/delta_bias : (D) fp32, h0/last_state :
+ * (B, D, N) fp32.  dstate N must be 16 (mamba-ssm default d_state).
+ * ckpt (optional)  : (B, ceil(L/ckpt_chunk), D, N) fp32 — h at the START of
+ *                    every chunk of `ckpt_chunk` steps (the backward's
+ *                    restart points; upstream saves `x` chunk states too).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int batch, dim, seqlen, dstate;
+  int dtype_io, dtype_bc;
+  int delta_softplus;
+  int ckpt_chunk;                 /* >0 iff ckpt != NULL; multiple of 16 */
+  int64_t u_bs, u_ls;             /* element strides (batch, time)       */
+  int64_t delta_bs, delta_ls;
+  int64_t z_bs, z_ls;
+  int64_t out_bs, out_ls;
+  int64_t B_bs, B_ls;
+  int64_t C_bs, C_ls;
+  const void* u;
+  const void* delta;
+  const float* A;
+  const void* Bm;
+  const void* Cm;
+  const float* D;          /* optional */
+  const void* z;           /* optional */
+  const float* delta_bias; /* optional */
+  const float* h0;         /* optional */
+  void* out;
+  float* last_state;       /* optional */
+  float* ckpt;             /* optional */
+} MttsScanFwdArgs;
+
+int mtts_selective_scan_fwd(const MttsScanFwdArgs* a, void* stream);
+
+/* Backward of the forward above (requires the forward's ckpt).
+ * dout : (B, L, D) dtype_io.  Outputs (caller-allocated):
+ *   du, ddelta, dz : (B, L, D) dtype_io (dz only if z; ddelta is w.r.t. the
+ *                    RAW delta, i.e. through softplus and delta_bias)
+ *   dB, dC         : (B, L, N) fp32 with strides dB_bs/dB_ls (N stride 1)
+ *   dA             : (D, N) fp32   dD, ddelta_bias : (D) fp32  (overwritten)
+ *   dh0            : optional (B, D, N) fp32 gradient w.r.t. h0
+ *   workspace      : mtts_selective_scan_bwd_workspace() bytes            */
+typedef struct {
+  MttsScanFwdArgs f;      /* same tensors / shapes as the forward call */
+  const void* dout;
+  int64_t dout_bs, dout_ls;
+  void* du;      int64_t du_bs, du_ls;
+  void* ddelta;  int64_t ddelta_bs, ddelta_ls;
+  void* dz;      int64_t dz_bs, dz_ls;
+  float* dB;     int64_t dB_bs, dB_ls;
+  float* dC;     int64_t dC_bs, dC_ls;
+  float* dA;
+  float* dD;
+  float* ddelta_bias;
+  float* dh0;
+  void* workspace;
+} MttsScanBwdArgs;
+
+int64_t mtts_selective_scan_bwd_workspace(int batch, int dim, int seqlen, int dstate);
+int mtts_selective_scan_bwd(const MttsScanBwdArgs* a, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Causal depthwise conv1d (width K <= 4) + bias + optional SiLU.
+ * Replaces [upstream] causal_conv1d_cuda.causal_conv1d_fwd / _bwd
+ * (causal-conv1d package; torch fallback HF:81-101), reached through
+ * Mamba.forward from mamba_decoder.py:61/:63.
+ *   out[b,t,c] = act( sum_k w[c,k] * xx[b, t-(K-1)+k, c] + bias[c] )
+ * where xx is x preceded by the K pre-conv inputs in conv_state_in
+ * (B, D, K) (zeros when NULL).  conv_state_out (B, D, K), optional, receives
+ * the last K inputs of [conv_state_in ‖ x] (mamba-ssm prefill semantics).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int batch, dim, seqlen, width;
+  int dtype;                      /* x / out / dx / dout */
+  int silu;
+  int64_t x_bs, x_ls, out_bs, out_ls;
+  const void* x;
+  const float* w;                 /* (D, K) */
+  const float* bias;              /* optional (D) */
+  const float* conv_state_in;     /* optional (B, D, K) */
+  void* out;
+  float* conv_state_out;          /* optional (B, D, K) */
+} MttsConvFwdArgs;
+
+int mtts_causal_conv1d_fwd(const MttsConvFwdArgs* a, void* stream);
+
+typedef struct {
+  MttsConvFwdArgs f;
+  const void* dout; int64_t dout_bs, dout_ls;
+  void* dx;         int64_t dx_bs, dx_ls;
+  float* dw;        /* (D, K)  overwritten */
+  float* dbias;     /* (D)     overwritten, optional */
+  void* workspace;  /* mtts_causal_conv1d_bwd_workspace() bytes */
+} MttsConvBwdArgs;
+
+int64_t mtts_causal_conv1d_bwd_workspace(int batch, int dim, int seqlen, int width);
+int mtts_causal_conv1d_bwd(const MttsConvBwdArgs* a, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Decode step (L = 1).  Replaces [upstream] causal_conv1d_update and
+ * selective_state_update (Mamba.step; HF:61-78, HF:128-171), reached from
+ * mamba_decoder.py:63 via decode_step (:188-256).  Both update the state
+ * tensors IN PLACE (as upstream does) — safe for hipGraph replay.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int batch, dim, width, dtype, silu;
+  int64_t x_bs, out_bs;
+  const void* x;       /* (B, D) */
+  float* conv_state;   /* (B, D, K) in/out */
+  const float* w;      /* (D, K) */
+  const float* bias;   /* optional */
+  void* out;           /* (B, D) */
+} MttsConvUpdateArgs;
+
+int mtts_causal_conv1d_update(const MttsConvUpdateArgs* a, void* stream);
+
+typedef struct {
+  int batch, dim, dstate, dtype_io, dtype_bc, dt_softplus;
+  int64_t x_bs, dt_bs, z_bs, out_bs, B_bs, C_bs;
+  float* state;              /* (B, D, N) in/out */
+  const void* x;             /* (B, D) */
+  const void* dt;            /* (B, D) raw delta */
+  const float* A;            /* (D, N) */
+  const void* Bm;            /* (B, N) */
+  const void* Cm;            /* (B, N) */
+  const float* D;            /* optional */
+  const void* z;             /* optional */
+  const float* dt_bias;      /* optional */
+  void* out;                 /* (B, D) */
+} MttsStateUpdateArgs;
+
+int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* stream);
+
+/* ------------------------------------------------------------------------
+ * LayerNorm (eps) with optional fused FiLM, optional fused residual add.
+ * Replaces torch nn.LayerNorm at mamba_decoder.py:59,67,81,184 and the FiLM
+ * modulation h = gamma*h + beta of mamba_decoder.py:82-86.
+ *   if res:   xs = x + res   (xs written to x_sum when x_sum != NULL)
+ *   y = LN(xs) * w + b ;  if gamma: y = gamma[row / rows_per_group] * y
+ *                                     + beta[row / rows_per_group]
+ * x/res/x_sum/y: (M, N) rows with row strides; gamma/beta: (G, N) with row
+ * stride gb_stride (fp32 or dtype).  mean/rstd: (M) fp32, saved for bwd.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int rows, cols, dtype, rows_per_group;
+  float eps;
+  int64_t x_rs, res_rs, xsum_rs, y_rs, gb_rs;
+  const void* x;
+  const void* res;         /* optional */
+  void* x_sum;             /* optional, written when res != NULL */
+  const float* w;
+  const float* b;
+  const void* gamma;       /* optional */
+  const void* beta;        /* optional (required iff gamma) */
+  int gb_dtype;
+  void* y;
+  float* mean;
+  float* rstd;
+} MttsLNArgs;
+
+int mtts_layernorm_fwd(const MttsLNArgs* a, void* stream);
+
+/* Backward: dy (M, N) -> dx (M, N) [+= dx_acc if given: dx = dx_acc + LN'],
+ * dw, db (N) fp32, dgamma/dbeta (G, N) fp32 (when gamma).  Uses the saved
+ * mean/rstd and the normalised input (x, or x_sum when res was fused). */
+typedef struct {
+  MttsLNArgs f;
+  const void* dy;   int64_t dy_rs;
+  const void* dx_acc; int64_t dxacc_rs;   /* optional residual-stream grad */
+  void* dx;         int64_t dx_rs;
+  float* dw;
+  float* db;
+  float* dgamma;
+  float* dbeta;
+  void* workspace;  /* mtts_layernorm_bwd_workspace() bytes */
+} MttsLNBwdArgs;
+
+int64_t mtts_layernorm_bwd_workspace(int rows, int cols, int rows_per_group);
+int mtts_layernorm_bwd(const MttsLNBwdArgs* a, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTTS_H */

@@ -1,0 +1,222 @@
+# mamba_decoder.py — MI355X-native drop-in for whcorkran/mamba-TTS-project's
+# mamba_decoder.py.  Same classes, constructor/forward/decode_step signatures
+# and state_dict keys (mamba_decoder.py:25-256 of the reference); the
+# arithmetic runs on libmtts HIP kernels (mtts/) instead of mamba-ssm CUDA.
+"""Mamba-based TTS decoder (drop-in).
+
+- `MambaTTSDecoderLayer(d_model, n_heads, d_ff, d_style)`:
+  LN -> Mamba -> +res -> LN -> cross-attn(text) -> +res -> LN -> FiLM -> FFN -> +res
+  (reference mamba_decoder.py:50-91).  The two "+res then LN" pairs run as
+  one fused HIP kernel (residual add + LayerNorm [+ FiLM]).
+- `MambaTTSDecoder(...)`: embeddings, layer stack, `forward` (teacher forced)
+  and `decode_step` (one AR step with per-layer states kept in HBM).
+
+Reference quirks reproduced on purpose:
+  * key_padding_mask = ~text_mask (True in text_mask = attend);
+  * decode_step adds no quant_embed;
+  * FiLM is gamma*h + beta with tanh-bounded gamma; GELU is exact (erf);
+  * 3D tokens with Q > 1 raise (size mismatch), as in the reference.
+
+Precision: set `model.compute_dtype = torch.bfloat16` to run activations and
+GEMMs in bf16 (params stay fp32 masters; scan/LN math is fp32 internally).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mtts.mamba import Mamba
+from mtts.attention import CrossAttention
+from mtts import ops
+
+
+class MambaTTSDecoderLayer(nn.Module):
+    def __init__(self, d_model, n_heads, d_ff, d_style):
+        super().__init__()
+        self.norm_mamba = nn.LayerNorm(d_model)
+        self.mamba = Mamba(d_model)
+
+        self.norm_cross = nn.LayerNorm(d_model)
+        self.cross_attn = CrossAttention(embed_dim=d_model, num_heads=n_heads, batch_first=True)
+
+        self.norm_ff = nn.LayerNorm(d_model)
+        self.ff = nn.Sequential(
+            nn.Linear(d_model, d_ff),
+            nn.GELU(),
+            nn.Linear(d_ff, d_model),
+        )
+
+        self.style_mlp = nn.Sequential(
+            nn.Linear(d_style, 2 * d_model),
+            nn.Tanh(),
+        )
+
+    def forward(self, x, text_hidden, z_style, text_mask=None, mamba_state=None):
+        cd = x.dtype
+        B, T, _ = x.shape
+        # 1) Mamba (mamba_decoder.py:59-64)
+        h, _ = ops.layer_norm(x, self.norm_mamba.weight, self.norm_mamba.bias, self.norm_mamba.eps)
+        h_mamba, new_state = self.mamba(h, mamba_state)
+
+        # 2) x = x + h_mamba ; h = norm_cross(x)   (fused, :64-67)
+        h, x = ops.layer_norm(h_mamba, self.norm_cross.weight, self.norm_cross.bias, self.norm_cross.eps, res=x)
+        key_padding_mask = None
+        if text_mask is not None:
+            key_padding_mask = ~text_mask                                   # :68-70 (sic)
+        attn_out, _ = self.cross_attn(query=h, key=text_hidden, value=text_hidden,
+                                      key_padding_mask=key_padding_mask)
+
+        # 3) x = x + attn ; h = gamma * norm_ff(x) + beta   (fused, :78-86)
+        gb = self.style_mlp(z_style.to(self.style_mlp[0].weight.dtype))
+        gamma, beta = torch.chunk(gb.to(cd), 2, dim=-1)
+        h, x = ops.layer_norm(attn_out, self.norm_ff.weight, self.norm_ff.bias, self.norm_ff.eps, res=x,
+                              gamma=gamma, beta=beta, rows_per_group=T)
+        f0, f2 = self.ff[0], self.ff[2]
+        ff_h = F.gelu(F.linear(h, f0.weight.to(cd), f0.bias.to(cd)))
+        ff_out = F.linear(ff_h, f2.weight.to(cd), f2.bias.to(cd))
+        x = x + ff_out                                                       # :88-89
+        return x, new_state
+
+
+class MambaTTSDecoder(nn.Module):
+    def __init__(
+        self,
+        vocab_size_audio,
+        d_model=512,
+        n_layers=8,
+        n_heads=8,
+        d_ff=2048,
+        d_style=256,
+        max_len=8192,  # allow flattened multi-quantizer codec sequences
+        num_quantizers=1,
+    ):
+        super().__init__()
+        self.vocab_size_audio = vocab_size_audio
+        self.token_embed = nn.Embedding(vocab_size_audio, d_model)
+        self.pos_embed = nn.Embedding(max_len, d_model)
+        self.quant_embed = nn.Embedding(num_quantizers, d_model)
+
+        self.layers = nn.ModuleList([
+            MambaTTSDecoderLayer(d_model, n_heads, d_ff, d_style)
+            for _ in range(n_layers)
+        ])
+
+        self.norm_out = nn.LayerNorm(d_model)
+        self.head = nn.Linear(d_model, vocab_size_audio)
+        self.compute_dtype = None  # e.g. torch.bfloat16
+
+    # -- helpers ----------------------------------------------------------
+    def _cd(self):
+        return self.compute_dtype if self.compute_dtype is not None else self.token_embed.weight.dtype
+
+    @staticmethod
+    def _concat_ref(text_hidden, text_mask, ref_hidden, ref_mask, B, device):
+        if ref_hidden is not None:
+            assert ref_hidden.dim() == 3 and ref_hidden.shape[0] == B, (
+                "ref_hidden must be (B, T_ref, d_model)"
+            )
+            if ref_mask is None:
+                ref_mask = torch.ones(B, ref_hidden.shape[1], dtype=torch.bool, device=device)
+            else:
+                assert ref_mask.dim() == 2 and ref_mask.shape[0] == B, (
+                    "ref_mask must be (B, T_ref) bool"
+                )
+            text_hidden = torch.cat([ref_hidden.to(text_hidden.dtype), text_hidden], dim=1)
+            if text_mask is None:
+                text_mask = ref_mask
+            else:
+                text_mask = torch.cat([ref_mask, text_mask], dim=1)
+        return text_hidden, text_mask
+
+    def _tail(self, x):
+        x, _ = ops.layer_norm(x, self.norm_out.weight, self.norm_out.bias, self.norm_out.eps)
+        cd = x.dtype
+        return F.linear(x, self.head.weight.to(cd), self.head.bias.to(cd))
+
+    # -- API --------------------------------------------------------------
+    def forward(self, audio_tokens, text_hidden, z_style, text_mask=None, ref_hidden=None, ref_mask=None):
+        """
+        audio_tokens: either
+            - (B, T_audio) int codec ids (single quantizer)
+            - (B, Q, T_audio) int codec ids (multi-quantizer; flattened internally)
+        text_hidden: (B, T_text, d_model) text encoder outputs
+        z_style: (B, d_style) style/timbre embedding
+        """
+        if audio_tokens.dim() == 3:
+            B, Q, T = audio_tokens.shape
+            audio_tokens = audio_tokens.reshape(B, Q * T)
+            quant_ids = torch.arange(Q, device=audio_tokens.device).repeat_interleave(T)
+            quant_ids = quant_ids.unsqueeze(0).expand(B, -1)
+        elif audio_tokens.dim() == 2:
+            B, T = audio_tokens.shape
+            quant_ids = torch.zeros_like(audio_tokens)
+        else:
+            raise ValueError("audio_tokens must be (B, T) or (B, Q, T)")
+        device = audio_tokens.device
+
+        if text_mask is not None:
+            assert text_mask.dim() == 2 and text_mask.shape[0] == B, (
+                "text_mask must be shape (B, T_text) with dtype=bool"
+            )
+        cd = self._cd()
+        text_hidden = text_hidden.to(cd)
+        text_hidden, text_mask = self._concat_ref(text_hidden, text_mask, ref_hidden, ref_mask, B, device)
+
+        tok = self.token_embed(audio_tokens)
+        qemb = self.quant_embed(quant_ids)
+        pos_ids = torch.arange(T, device=device)
+        pos = self.pos_embed(pos_ids)[None, :, :].expand(B, T, -1)
+        x = (tok + pos + qemb).to(cd)
+
+        for layer in self.layers:
+            x, _ = layer(x=x, text_hidden=text_hidden, z_style=z_style, text_mask=text_mask, mamba_state=None)
+        return self._tail(x)
+
+    def decode_step(
+        self,
+        last_token,
+        text_hidden,
+        z_style,
+        mamba_states,
+        step_index: int,
+        text_mask=None,
+        ref_hidden=None,
+        ref_mask=None,
+    ):
+        """Generate logits for a single autoregressive step.
+
+        Args:
+            last_token: (B, 1) int tensor containing the most recent audio token.
+            text_hidden: (B, T_text, d_model) encoder outputs.
+            z_style: (B, d_style) style embedding.
+            mamba_states: list of per-layer states (length == n_layers). Each
+                entry may be None for the first step.
+            step_index: int, absolute position index of this token (0-based).
+            text_mask: optional (B, T_text) boolean mask for text padding.
+
+        Returns:
+            logits: (B, 1, vocab_size_audio)
+            new_states: list of updated per-layer mamba states
+        """
+        B_local = last_token.shape[0]
+        device = last_token.device
+        cd = self._cd()
+
+        tok = self.token_embed(last_token)
+        pos_id = torch.tensor([step_index], device=device)
+        pos = self.pos_embed(pos_id)[None, :, :].expand(B_local, 1, -1)
+        x = (tok + pos).to(cd)                                               # no quant_embed (:217-221)
+
+        text_hidden = text_hidden.to(cd)
+        text_hidden, text_mask = self._concat_ref(text_hidden, text_mask, ref_hidden, ref_mask, B_local, device)
+
+        new_states = [None] * len(self.layers)
+        for i, layer in enumerate(self.layers):
+            x, new_state = layer(
+                x=x,
+                text_hidden=text_hidden,
+                z_style=z_style,
+                text_mask=text_mask,
+                mamba_state=mamba_states[i] if mamba_states is not None else None,
+            )
+            new_states[i] = new_state
+        return self._tail(x), new_states

@@ -1,0 +1,143 @@
+"""ctypes binding of libmtts.so (include/mtts.h).
+
+The library is the product: there is no CPU fallback.  Loading fails loudly
+when libmtts.so is missing, and every wrapper raises RuntimeError with
+mtts_last_error() on a non-zero return code.
+
+torch must be imported before the library is loaded so that the HIP runtime
+torch bundles (libamdhip64.so.7) is the one the library binds to.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the dlopen below)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
+ABI_VERSION = 1
+
+F32, BF16 = 0, 1
+i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
+
+
+class ScanFwdArgs(C.Structure):
+    _fields_ = [("batch", i32), ("dim", i32), ("seqlen", i32), ("dstate", i32),
+                ("dtype_io", i32), ("dtype_bc", i32), ("delta_softplus", i32), ("ckpt_chunk", i32),
+                ("u_bs", i64), ("u_ls", i64), ("delta_bs", i64), ("delta_ls", i64),
+                ("z_bs", i64), ("z_ls", i64), ("out_bs", i64), ("out_ls", i64),
+                ("B_bs", i64), ("B_ls", i64), ("C_bs", i64), ("C_ls", i64),
+                ("u", vp), ("delta", vp), ("A", vp), ("Bm", vp), ("Cm", vp), ("D", vp), ("z", vp),
+                ("delta_bias", vp), ("h0", vp), ("out", vp), ("last_state", vp), ("ckpt", vp)]
+
+
+class ScanBwdArgs(C.Structure):
+    _fields_ = [("f", ScanFwdArgs), ("dout", vp), ("dout_bs", i64), ("dout_ls", i64),
+                ("du", vp), ("du_bs", i64), ("du_ls", i64),
+                ("ddelta", vp), ("ddelta_bs", i64), ("ddelta_ls", i64),
+                ("dz", vp), ("dz_bs", i64), ("dz_ls", i64),
+                ("dB", vp), ("dB_bs", i64), ("dB_ls", i64),
+                ("dC", vp), ("dC_bs", i64), ("dC_ls", i64),
+                ("dA", vp), ("dD", vp), ("ddelta_bias", vp), ("dh0", vp), ("workspace", vp)]
+
+
+class ConvFwdArgs(C.Structure):
+    _fields_ = [("batch", i32), ("dim", i32), ("seqlen", i32), ("width", i32), ("dtype", i32), ("silu", i32),
+                ("x_bs", i64), ("x_ls", i64), ("out_bs", i64), ("out_ls", i64),
+                ("x", vp), ("w", vp), ("bias", vp), ("conv_state_in", vp), ("out", vp), ("conv_state_out", vp)]
+
+
+class ConvBwdArgs(C.Structure):
+    _fields_ = [("f", ConvFwdArgs), ("dout", vp), ("dout_bs", i64), ("dout_ls", i64),
+                ("dx", vp), ("dx_bs", i64), ("dx_ls", i64), ("dw", vp), ("dbias", vp), ("workspace", vp)]
+
+
+class ConvUpdateArgs(C.Structure):
+    _fields_ = [("batch", i32), ("dim", i32), ("width", i32), ("dtype", i32), ("silu", i32),
+                ("x_bs", i64), ("out_bs", i64), ("x", vp), ("conv_state", vp), ("w", vp), ("bias", vp),
+                ("out", vp)]
+
+
+class StateUpdateArgs(C.Structure):
+    _fields_ = [("batch", i32), ("dim", i32), ("dstate", i32), ("dtype_io", i32), ("dtype_bc", i32),
+                ("dt_softplus", i32),
+                ("x_bs", i64), ("dt_bs", i64), ("z_bs", i64), ("out_bs", i64), ("B_bs", i64), ("C_bs", i64),
+                ("state", vp), ("x", vp), ("dt", vp), ("A", vp), ("Bm", vp), ("Cm", vp), ("D", vp), ("z", vp),
+                ("dt_bias", vp), ("out", vp)]
+
+
+class LNArgs(C.Structure):
+    _fields_ = [("rows", i32), ("cols", i32), ("dtype", i32), ("rows_per_group", i32), ("eps", f32),
+                ("x_rs", i64), ("res_rs", i64), ("xsum_rs", i64), ("y_rs", i64), ("gb_rs", i64),
+                ("x", vp), ("res", vp), ("x_sum", vp), ("w", vp), ("b", vp), ("gamma", vp), ("beta", vp),
+                ("gb_dtype", i32), ("y", vp), ("mean", vp), ("rstd", vp)]
+
+
+class LNBwdArgs(C.Structure):
+    _fields_ = [("f", LNArgs), ("dy", vp), ("dy_rs", i64), ("dx_acc", vp), ("dxacc_rs", i64),
+                ("dx", vp), ("dx_rs", i64), ("dw", vp), ("db", vp), ("dgamma", vp), ("dbeta", vp),
+                ("workspace", vp)]
+
+
+_SIGS = {
+    "mtts_abi_version": ([], i32),
+    "mtts_last_error": ([], C.c_char_p),
+    "mtts_selective_scan_fwd": ([C.POINTER(ScanFwdArgs), vp], i32),
+    "mtts_selective_scan_bwd_workspace": ([i32, i32, i32, i32], i64),
+    "mtts_selective_scan_bwd": ([C.POINTER(ScanBwdArgs), vp], i32),
+    "mtts_causal_conv1d_fwd": ([C.POINTER(ConvFwdArgs), vp], i32),
+    "mtts_causal_conv1d_bwd_workspace": ([i32, i32, i32, i32], i64),
+    "mtts_causal_conv1d_bwd": ([C.POINTER(ConvBwdArgs), vp], i32),
+    "mtts_causal_conv1d_update": ([C.POINTER(ConvUpdateArgs), vp], i32),
+    "mtts_selective_state_update": ([C.POINTER(StateUpdateArgs), vp], i32),
+    "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
+    "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),
+    "mtts_layernorm_bwd": ([C.POINTER(LNBwdArgs), vp], i32),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libmtts.so once (raises if it is missing or ABI-incompatible)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libmtts.so not found at {LIB_PATH}; run __graft_entry__.build() "
+                               "(make -C mamba-tts-project_amd/mtts/csrc)")
+        L = C.CDLL(LIB_PATH)
+        for name, (argt, rest) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = rest
+        v = L.mtts_abi_version()
+        if v != ABI_VERSION:
+            raise RuntimeError(f"libmtts ABI {v} != expected {ABI_VERSION}")
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def call(name, args):
+    """Invoke ``name(&args, current_stream)``; raise on error."""
+    L = lib()
+    stream = torch.cuda.current_stream().cuda_stream
+    rc = getattr(L, name)(C.byref(args), C.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"{name} failed ({rc}): {L.mtts_last_error().decode()}")
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype} (libmtts takes float32 / bfloat16)")
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,115 @@
+// Shared device/host helpers for libmtts (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "mtts.h"
+
+namespace mtts {
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+
+#define MTTS_CHECK(cond, ...)                                                 \
+  do {                                                                        \
+    if (!(cond)) {                                                            \
+      ::mtts::set_error(__VA_ARGS__);                                         \
+      return MTTS_EINVAL;                                                     \
+    }                                                                         \
+  } while (0)
+
+#define MTTS_LAUNCH_CHECK(name)                                               \
+  do {                                                                        \
+    hipError_t e_ = hipGetLastError();                                        \
+    if (e_ != hipSuccess) {                                                   \
+      ::mtts::set_error("%s: launch failed: %s", name, hipGetErrorString(e_)); \
+      return MTTS_ELAUNCH;                                                    \
+    }                                                                         \
+  } while (0)
+
+// ---------------------------------------------------------------- dtypes
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return *reinterpret_cast<bf16_t*>(&h);
+}
+
+template <typename T> struct IO;
+template <> struct IO<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+};
+template <> struct IO<bf16_t> {
+  static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(bf16_t* p, float v) { *p = f2bf(v); }
+};
+template <typename T> __device__ __forceinline__ float ldf(const T* p) { return IO<T>::ld(p); }
+template <typename T> __device__ __forceinline__ void stf(T* p, float v) { IO<T>::st(p, v); }
+
+// ---------------------------------------------------------------- math
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * kLog2e); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// softplus with torch's threshold (x > 20 -> x); accurate for very negative x
+__device__ __forceinline__ float softplus_f(float x) {
+  float e = __builtin_amdgcn_exp2f(fminf(x, 20.f) * kLog2e);
+  float lg = __builtin_amdgcn_logf(1.f + e) * kLn2;  // v_log_f32 is log2
+  float sm = e * (1.f - 0.5f * e);                   // log1p(e) for tiny e
+  float r = e < 1e-3f ? sm : lg;
+  return x > 20.f ? x : r;
+}
+// d softplus / dx = sigmoid(x)  (1 for x > 20, matching torch's threshold)
+__device__ __forceinline__ float softplus_grad(float x) {
+  float s = fast_rcp(1.f + __builtin_amdgcn_exp2f(-x * kLog2e));
+  return x > 20.f ? 1.f : s;
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return fast_rcp(1.f + __builtin_amdgcn_exp2f(-x * kLog2e)); }
+__device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
+
+// ---------------------------------------------------------------- cross-lane
+// DPP quad_perm controls
+constexpr int kQuadXor1 = 0xB1;  // [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;  // [2,3,0,1]
+template <int L> constexpr int quad_bcast() { return L * 0x55; }
+constexpr int kRowRor4 = 0x124;
+constexpr int kRowRor8 = 0x128;
+constexpr int kRowRor12 = 0x12C;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float xor32(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]);
+}
+__device__ __forceinline__ float xor16(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]);
+}
+// lane ^ 4 within each 16-lane row
+__device__ __forceinline__ float xor4(float v, int lane) {
+  float a = dpp<kRowRor4>(v);   // from lane-4
+  float b = dpp<kRowRor12>(v);  // from lane+4
+  return (lane & 4) ? a : b;
+}
+__device__ __forceinline__ float xor8(float v) { return dpp<kRowRor8>(v); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp<kQuadXor1>(v);
+  v += dpp<kQuadXor2>(v);
+  v += xor4(v, threadIdx.x & 63);
+  v += xor8(v);
+  v += xor16(v);
+  v += xor32(v);
+  return v;
+}
+
+}  // namespace mtts

@@ -1,0 +1,366 @@
+// LayerNorm (+ fused residual add, + fused FiLM) forward / backward, gfx950.
+//
+// Replaces nn.LayerNorm at mamba_decoder.py:59,67,81,184 and the FiLM of
+// mamba_decoder.py:82-86 (h = gamma*LN(x) + beta, gamma/beta per batch row,
+// no "1+gamma").  One wave per row: the row stays in registers (16-byte
+// vector loads), statistics by DPP/permlane wave reductions; HBM-bound.
+// Parameter-gradient sums over rows go to per-block partials reduced by a
+// second deterministic kernel (no atomics).
+#include "common.h"
+
+namespace mtts {
+
+constexpr int kLnWaves = 4;
+constexpr int kMaxVec = 8;  // elements per 16-byte vector (bf16)
+
+template <typename T, int VEC>
+__device__ __forceinline__ void ld_vec(const T* p, float (&o)[VEC]) {
+  if constexpr (VEC * sizeof(T) == 16) {
+    uint4 v = *reinterpret_cast<const uint4*>(p);
+    if constexpr (sizeof(T) == 4) {
+      o[0] = __uint_as_float(v.x); o[1] = __uint_as_float(v.y); o[2] = __uint_as_float(v.z); o[3] = __uint_as_float(v.w);
+    } else {
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { o[2 * q] = __uint_as_float(w[q] << 16); o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) o[q] = ldf(p + q);
+  }
+}
+template <typename T, int VEC>
+__device__ __forceinline__ void st_vec(T* p, const float (&v)[VEC]) {
+  if constexpr (VEC * sizeof(T) == 16) {
+    uint4 w;
+    if constexpr (sizeof(T) == 4) {
+      w = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+    } else {
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+      w = make_uint4(q[0], q[1], q[2], q[3]);
+    }
+    *reinterpret_cast<uint4*>(p) = w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) stf(p + q, v[q]);
+  }
+}
+
+// NV = vectors per lane (cols = 64 * VEC * NV)
+template <typename T, typename TG, int VEC, int NV>
+__global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_kernel(const MttsLNArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kLnWaves + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int n = a.cols;
+  float v[NV][VEC];
+  const T* x = (const T*)a.x + (int64_t)row * a.x_rs;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) ld_vec<T, VEC>(x + (k * 64 + lane) * VEC, v[k]);
+  if (a.res) {
+    const T* r = (const T*)a.res + (int64_t)row * a.res_rs;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      float t[VEC];
+      ld_vec<T, VEC>(r + (k * 64 + lane) * VEC, t);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) v[k][q] += t[q];
+    }
+    if (a.x_sum) {
+      T* xs = (T*)a.x_sum + (int64_t)row * a.xsum_rs;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        // round to the storage dtype so fwd/bwd see the same stream value
+        st_vec<T, VEC>(xs + (k * 64 + lane) * VEC, v[k]);
+        ld_vec<T, VEC>(xs + (k * 64 + lane) * VEC, v[k]);
+      }
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) s += v[k][q];
+  const float mean = wave_sum(s) / n;
+  float s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) { const float d = v[k][q] - mean; s2 = fmaf(d, d, s2); }
+  const float var = wave_sum(s2) / n;
+  const float rstd = 1.f / sqrtf(var + a.eps);
+  if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
+  const int grp = a.gamma ? row / a.rows_per_group : 0;
+  T* y = (T*)a.y + (int64_t)row * a.y_rs;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c0 = (k * 64 + lane) * VEC;
+    float o[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) o[q] = fmaf((v[k][q] - mean) * rstd, a.w[c0 + q], a.b[c0 + q]);
+    if (a.gamma) {
+      float g[VEC], be[VEC];
+      ld_vec<TG, VEC>((const TG*)a.gamma + (int64_t)grp * a.gb_rs + c0, g);
+      ld_vec<TG, VEC>((const TG*)a.beta + (int64_t)grp * a.gb_rs + c0, be);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o[q] = fmaf(g[q], o[q], be[q]);
+    }
+    st_vec<T, VEC>(y + c0, o);
+  }
+}
+
+// Each block handles RB consecutive rows (all in one FiLM group); partials
+// per block: dw, db (cols each) and dgamma, dbeta (cols each).
+template <typename T, typename TG, int VEC, int NV>
+__global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const MttsLNBwdArgs a, int RB, float* __restrict__ part) {
+  const MttsLNArgs& f = a.f;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int n = f.cols;
+  const int row0 = blockIdx.x * RB;
+  const bool film = f.gamma != nullptr;
+  const int grp = film ? row0 / f.rows_per_group : 0;
+  float wv[NV][VEC], bv[NV][VEC], gv[NV][VEC];
+  float pdw[NV][VEC], pdb[NV][VEC], pdg[NV][VEC], pdbe[NV][VEC];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c0 = (k * 64 + lane) * VEC;
+    ld_vec<float, VEC>(f.w + c0, wv[k]);
+    ld_vec<float, VEC>(f.b + c0, bv[k]);
+    if (film) ld_vec<TG, VEC>((const TG*)f.gamma + (int64_t)grp * f.gb_rs + c0, gv[k]);
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      if (!film) gv[k][q] = 1.f;
+      pdw[k][q] = pdb[k][q] = pdg[k][q] = pdbe[k][q] = 0.f;
+    }
+  }
+  const T* xsrc = (const T*)((f.res && f.x_sum) ? f.x_sum : f.x);
+  const int64_t xrs = (f.res && f.x_sum) ? f.xsum_rs : f.x_rs;
+  for (int r = wave; r < RB; r += kLnWaves) {
+    const int row = row0 + r;
+    if (row >= f.rows) break;
+    const float mean = f.mean[row], rstd = f.rstd[row];
+    float xh[NV][VEC], dxh[NV][VEC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c0 = (k * 64 + lane) * VEC;
+      float xv[VEC], dy[VEC];
+      ld_vec<T, VEC>(xsrc + (int64_t)row * xrs + c0, xv);
+      ld_vec<T, VEC>((const T*)a.dy + (int64_t)row * a.dy_rs + c0, dy);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        const float h = (xv[q] - mean) * rstd;
+        xh[k][q] = h;
+        const float g = dy[q] * gv[k][q];
+        pdw[k][q] = fmaf(g, h, pdw[k][q]);
+        pdb[k][q] += g;
+        if (film) {
+          pdg[k][q] = fmaf(dy[q], fmaf(h, wv[k][q], bv[k][q]), pdg[k][q]);
+          pdbe[k][q] += dy[q];
+        }
+        const float d = g * wv[k][q];
+        dxh[k][q] = d;
+        s1 += d;
+        s2 = fmaf(d, h, s2);
+      }
+    }
+    const float m1 = wave_sum(s1) / n, m2 = wave_sum(s2) / n;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c0 = (k * 64 + lane) * VEC;
+      float o[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o[q] = rstd * (dxh[k][q] - m1 - xh[k][q] * m2);
+      if (a.dx_acc) {
+        float t[VEC];
+        ld_vec<T, VEC>((const T*)a.dx_acc + (int64_t)row * a.dxacc_rs + c0, t);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) o[q] += t[q];
+      }
+      st_vec<T, VEC>((T*)a.dx + (int64_t)row * a.dx_rs + c0, o);
+    }
+  }
+  // block partials: reduce the 4 waves through LDS, then one write per column
+  extern __shared__ float sm[];  // [kLnWaves][cols]
+  const int nk = film ? 4 : 2;
+  for (int which = 0; which < nk; ++which) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c0 = (k * 64 + lane) * VEC;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        const float val = which == 0 ? pdw[k][q] : which == 1 ? pdb[k][q] : which == 2 ? pdg[k][q] : pdbe[k][q];
+        sm[wave * n + c0 + q] = val;
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < n; c += 64 * kLnWaves) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < kLnWaves; ++w) s += sm[w * n + c];
+      part[((int64_t)which * gridDim.x + blockIdx.x) * n + c] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// dw/db: sum over all blocks; dgamma/dbeta: sum over the blocks of a group
+__global__ void ln_bwd_reduce(const float* __restrict__ part, int nblk, int cols, int blk_per_group, int ngroups,
+                              float* dw, float* db, float* dg, float* dbeta) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n1 = (int64_t)2 * cols;
+  if (idx < n1) {
+    const int which = idx / cols, c = idx % cols;
+    float s = 0.f;
+    for (int p = 0; p < nblk; ++p) s += part[((int64_t)which * nblk + p) * cols + c];
+    (which == 0 ? dw : db)[c] = s;
+    return;
+  }
+  if (!dg) return;
+  const int64_t j = idx - n1;
+  if (j >= (int64_t)2 * ngroups * cols) return;
+  const int which = 2 + j / ((int64_t)ngroups * cols);
+  const int g = (j / cols) % ngroups, c = j % cols;
+  float s = 0.f;
+  for (int p = g * blk_per_group; p < (g + 1) * blk_per_group && p < nblk; ++p)
+    s += part[((int64_t)which * nblk + p) * cols + c];
+  (which == 2 ? dg : dbeta)[(int64_t)g * cols + c] = s;
+}
+
+static int ln_rb(const MttsLNArgs* a) {
+  if (!a->gamma) return 64;
+  for (int rb = 64; rb > 1; rb >>= 1)
+    if (a->rows_per_group % rb == 0) return rb;
+  return 1;
+}
+
+template <typename T, typename TG, int VEC, int NV>
+static void launch_fwd(const MttsLNArgs* a, hipStream_t st) {
+  hipLaunchKernelGGL((ln_fwd_kernel<T, TG, VEC, NV>), dim3((a->rows + kLnWaves - 1) / kLnWaves), dim3(64 * kLnWaves), 0,
+                     st, *a);
+}
+template <typename T, typename TG, int VEC, int NV>
+static void launch_bwd(const MttsLNBwdArgs* a, int rb, float* part, hipStream_t st) {
+  const int nblk = (a->f.rows + rb - 1) / rb;
+  hipLaunchKernelGGL((ln_bwd_kernel<T, TG, VEC, NV>), dim3(nblk), dim3(64 * kLnWaves),
+                     kLnWaves * a->f.cols * sizeof(float), st, *a, rb, part);
+}
+
+// dispatch on (dtype, gamma dtype, cols)
+template <template <typename, typename, int, int> class F, typename... Args>
+static int dispatch_ln(const MttsLNArgs* a, Args... args) {
+  const int n = a->cols;
+  auto go = [&](auto tag_t, auto tag_g) -> int {
+    using T = typename decltype(tag_t)::type;
+    using TG = typename decltype(tag_g)::type;
+    constexpr int VEC = 16 / sizeof(T);
+    const bool vec_ok = n % (64 * VEC) == 0 && (a->x_rs * (int64_t)sizeof(T)) % 16 == 0 &&
+                        (a->y_rs * (int64_t)sizeof(T)) % 16 == 0 && (uintptr_t)a->x % 16 == 0 &&
+                        (uintptr_t)a->y % 16 == 0 &&
+                        (!a->res || ((uintptr_t)a->res % 16 == 0 && (a->res_rs * (int64_t)sizeof(T)) % 16 == 0)) &&
+                        (!a->gamma || ((uintptr_t)a->gamma % 16 == 0 && (a->gb_rs * (int64_t)sizeof(TG)) % 16 == 0 &&
+                                       (uintptr_t)a->beta % 16 == 0));
+    if (vec_ok) {
+      switch (n / (64 * VEC)) {
+        case 1: F<T, TG, VEC, 1>::run(a, args...); return MTTS_OK;
+        case 2: F<T, TG, VEC, 2>::run(a, args...); return MTTS_OK;
+        case 3: F<T, TG, VEC, 3>::run(a, args...); return MTTS_OK;
+        case 4: F<T, TG, VEC, 4>::run(a, args...); return MTTS_OK;
+        default: break;
+      }
+    }
+    if (n % 64 == 0) {
+      switch (n / 64) {
+        case 1: F<T, TG, 1, 1>::run(a, args...); return MTTS_OK;
+        case 2: F<T, TG, 1, 2>::run(a, args...); return MTTS_OK;
+        case 3: F<T, TG, 1, 3>::run(a, args...); return MTTS_OK;
+        case 4: F<T, TG, 1, 4>::run(a, args...); return MTTS_OK;
+        case 6: F<T, TG, 1, 6>::run(a, args...); return MTTS_OK;
+        case 8: F<T, TG, 1, 8>::run(a, args...); return MTTS_OK;
+        case 16: F<T, TG, 1, 16>::run(a, args...); return MTTS_OK;
+        default: break;
+      }
+    }
+    set_error("layernorm: cols=%d unsupported", n);
+    return MTTS_EUNSUPPORTED;
+  };
+  struct F32 { using type = float; };
+  struct BF { using type = bf16_t; };
+  const bool gf = !a->gamma || a->gb_dtype == MTTS_F32;
+  if (a->dtype == MTTS_F32) return gf ? go(F32{}, F32{}) : go(F32{}, BF{});
+  return gf ? go(BF{}, F32{}) : go(BF{}, BF{});
+}
+
+template <typename T, typename TG, int VEC, int NV>
+struct FwdRunner {
+  static void run(const MttsLNArgs* a, hipStream_t st) { launch_fwd<T, TG, VEC, NV>(a, st); }
+};
+template <typename T, typename TG, int VEC, int NV>
+struct BwdRunner {
+  static void run(const MttsLNArgs* a, const MttsLNBwdArgs* b, int rb, float* part, hipStream_t st) {
+    (void)a;
+    launch_bwd<T, TG, VEC, NV>(b, rb, part, st);
+  }
+};
+
+static int check_ln(const MttsLNArgs* a) {
+  MTTS_CHECK(a && a->x && a->w && a->b && a->y && a->mean && a->rstd, "layernorm: null tensor");
+  MTTS_CHECK(a->rows >= 0 && a->cols > 0, "layernorm: bad sizes");
+  MTTS_CHECK(a->dtype == MTTS_F32 || a->dtype == MTTS_BF16, "layernorm: bad dtype");
+  MTTS_CHECK(!a->gamma || (a->beta && a->rows_per_group > 0), "layernorm: FiLM needs beta and rows_per_group");
+  return MTTS_OK;
+}
+
+}  // namespace mtts
+
+using namespace mtts;
+
+extern "C" int mtts_layernorm_fwd(const MttsLNArgs* a, void* stream) {
+  int rc = check_ln(a);
+  if (rc) return rc;
+  if (a->rows == 0) return MTTS_OK;
+  rc = dispatch_ln<FwdRunner>(a, (hipStream_t)stream);
+  if (rc) return rc;
+  MTTS_LAUNCH_CHECK("layernorm_fwd");
+  return MTTS_OK;
+}
+
+extern "C" int64_t mtts_layernorm_bwd_workspace(int rows, int cols, int rows_per_group) {
+  MttsLNArgs t{};
+  t.gamma = rows_per_group > 0 ? (const void*)1 : nullptr;
+  t.rows_per_group = rows_per_group;
+  const int rb = ln_rb(&t);
+  const int64_t nblk = (rows + rb - 1) / rb;
+  return 4 * nblk * cols * 4 + 256;
+}
+
+extern "C" int mtts_layernorm_bwd(const MttsLNBwdArgs* a, void* stream) {
+  MTTS_CHECK(a, "layernorm_bwd: null args");
+  int rc = check_ln(&a->f);
+  if (rc) return rc;
+  MTTS_CHECK(a->dy && a->dx && a->dw && a->db && a->workspace, "layernorm_bwd: null tensor");
+  MTTS_CHECK(!a->f.gamma || (a->dgamma && a->dbeta), "layernorm_bwd: FiLM needs dgamma/dbeta");
+  const MttsLNArgs& f = a->f;
+  hipStream_t st = (hipStream_t)stream;
+  if (f.rows == 0) {
+    (void)hipMemsetAsync(a->dw, 0, f.cols * 4, st);
+    (void)hipMemsetAsync(a->db, 0, f.cols * 4, st);
+    return MTTS_OK;
+  }
+  const int rb = ln_rb(&f);
+  float* part = (float*)a->workspace;
+  rc = dispatch_ln<BwdRunner>(&f, a, rb, part, st);
+  if (rc) return rc;
+  MTTS_LAUNCH_CHECK("layernorm_bwd");
+  const int nblk = (f.rows + rb - 1) / rb;
+  const int ngroups = f.gamma ? (f.rows + f.rows_per_group - 1) / f.rows_per_group : 0;
+  const int bpg = f.gamma ? f.rows_per_group / rb : 0;
+  const int64_t tot = (int64_t)2 * f.cols + (int64_t)2 * ngroups * f.cols;
+  hipLaunchKernelGGL(ln_bwd_reduce, dim3((tot + 255) / 256), dim3(256), 0, st, part, nblk, f.cols, bpg, ngroups,
+                     a->dw, a->db, a->dgamma, a->dbeta);
+  MTTS_LAUNCH_CHECK("layernorm_bwd_reduce");
+  return MTTS_OK;
+}

@@ -1,0 +1,159 @@
+"""Mamba v1 mixer on libmtts (the build's replacement for `mamba_ssm.Mamba`).
+
+Reference contract: mamba_decoder.py:10-15 documents
+    out, new_state = mamba(x)          # full sequence, state from h = 0
+    out, new_state = mamba(x, state)   # incremental (decode) step
+with x (B, T, d_model) and an opaque per-layer state; the build's state is
+(conv_state (B, d_inner, d_conv) fp32, ssm_state (B, d_inner, d_state) fp32),
+the [upstream] mamba-ssm InferenceParams layout.  Parameters, names, shapes
+and initialisation follow [upstream] mamba_ssm/modules/mamba_simple.py
+(d_state=16, d_conv=4, expand=2, dt_rank=ceil(d/16), bias=False,
+conv_bias=True, dt in [1e-3, 1e-1], A_log = log(1..16), D = 1), so a
+reference state_dict loads unchanged.
+
+Hot path (all HIP through the C ABI, GEMMs through torch):
+  xz = in_proj(x)                         (B, L, 2*di)   channel-last
+  u  = silu(conv1d(xz[..., :di]))         HIP causal_conv1d (strided view)
+  x_dbl = x_proj(u) -> dt | B | C
+  delta = dt_proj.weight @ dt             (bias folded into the scan)
+  y  = selective_scan(u, delta, A, B, C, D, z = xz[..., di:])   HIP
+  out = out_proj(y)
+Backward (MambaInnerFn) runs the HIP scan/conv backward kernels and writes
+dz and dx straight into one d(xz) buffer (no concat).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+class MambaInnerFn(torch.autograd.Function):
+    """(xz, params[, state]) -> (y, conv_state, ssm_state); y is pre-out_proj."""
+
+    @staticmethod
+    def forward(ctx, xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, conv_state_in, h0):
+        di = xz.shape[-1] // 2
+        N = A_log.shape[1]
+        r = W_dt.shape[1]
+        x, z = xz[..., :di], xz[..., di:]
+        u, conv_state = ops.conv_fwd(x, conv_w, conv_b, True, state_in=conv_state_in, want_state=True)
+        x_dbl = F.linear(u, W_x)
+        dt, Bm, Cm = x_dbl[..., :r], x_dbl[..., r:r + N], x_dbl[..., r + N:]
+        delta = F.linear(dt, W_dt)
+        A = -torch.exp(A_log.float())
+        need = any(ctx.needs_input_grad)
+        y, last, ckpt = ops.scan_fwd(u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, want_last=True, want_ckpt=need)
+        if need:
+            ctx.save_for_backward(xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt)
+        ctx.mark_non_differentiable(conv_state, last)
+        return y, conv_state, last
+
+    @staticmethod
+    def backward(ctx, dy, _dconv, _dlast):
+        xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt = ctx.saved_tensors
+        di = xz.shape[-1] // 2
+        N = A_log.shape[1]
+        r = W_dt.shape[1]
+        Bsz, Ln, _ = xz.shape
+        x, z = xz[..., :di], xz[..., di:]
+        dt, Bm, Cm = x_dbl[..., :r], x_dbl[..., r:r + N], x_dbl[..., r + N:]
+        A = -torch.exp(A_log.float())
+        dxz = torch.empty_like(xz)
+        dx_dbl = torch.empty(Bsz, Ln, r + 2 * N, device=xz.device, dtype=torch.float32)
+        du, ddelta, _, _, _, dA, dD, dbias, _ = ops.scan_bwd(
+            u, delta, A, Bm, Cm, D, z, dt_bias, True, None, ckpt, dy,
+            dz=dxz[..., di:], dB=dx_dbl[..., r:r + N], dC=dx_dbl[..., r + N:])
+        cd = u.dtype
+        # dt_proj: delta = dt @ W_dt^T
+        dx_dbl[..., :r] = (ddelta @ W_dt).float()
+        dW_dt = ddelta.reshape(-1, di).t() @ dt.reshape(-1, r)
+        # x_proj: x_dbl = u @ W_x^T
+        gx = dx_dbl.to(cd)
+        du = du + gx @ W_x
+        dW_x = gx.reshape(-1, r + 2 * N).t() @ u.reshape(-1, di)
+        _, dw, db = ops.conv_bwd(x, conv_w, conv_b, du, True, dx=dxz[..., :di])
+        dA_log = (dA * A).to(A_log.dtype)
+        return (dxz, dw.reshape(conv_w.shape).to(conv_w.dtype), db.to(conv_b.dtype), dW_x.to(W_x.dtype),
+                dW_dt.to(W_dt.dtype), dA_log, dD.to(D.dtype), dbias.to(dt_bias.dtype), None, None)
+
+
+class Mamba(nn.Module):
+    def __init__(self, d_model, d_state=16, d_conv=4, expand=2, dt_rank="auto", dt_min=0.001, dt_max=0.1,
+                 dt_init="random", dt_scale=1.0, dt_init_floor=1e-4, conv_bias=True, bias=False,
+                 device=None, dtype=None):
+        super().__init__()
+        fk = {"device": device, "dtype": dtype}
+        self.d_model = d_model
+        self.d_state = d_state
+        self.d_conv = d_conv
+        self.expand = expand
+        self.d_inner = int(expand * d_model)
+        self.dt_rank = math.ceil(d_model / 16) if dt_rank == "auto" else dt_rank
+        di = self.d_inner
+        self.in_proj = nn.Linear(d_model, di * 2, bias=bias, **fk)
+        self.conv1d = nn.Conv1d(di, di, kernel_size=d_conv, groups=di, padding=d_conv - 1, bias=conv_bias, **fk)
+        self.x_proj = nn.Linear(di, self.dt_rank + d_state * 2, bias=False, **fk)
+        self.dt_proj = nn.Linear(self.dt_rank, di, bias=True, **fk)
+        dt_init_std = self.dt_rank ** -0.5 * dt_scale
+        with torch.no_grad():
+            if dt_init == "constant":
+                self.dt_proj.weight.fill_(dt_init_std)
+            else:
+                self.dt_proj.weight.uniform_(-dt_init_std, dt_init_std)
+            dt = torch.exp(torch.rand(di, **fk) * (math.log(dt_max) - math.log(dt_min)) + math.log(dt_min))
+            dt = dt.clamp(min=dt_init_floor)
+            self.dt_proj.bias.copy_(dt + torch.log(-torch.expm1(-dt)))
+        self.dt_proj.bias._no_reinit = True
+        A = torch.arange(1, d_state + 1, dtype=torch.float32, device=device).repeat(di, 1).contiguous()
+        self.A_log = nn.Parameter(torch.log(A))
+        self.A_log._no_weight_decay = True
+        self.D = nn.Parameter(torch.ones(di, device=device))
+        self.D._no_weight_decay = True
+        self.out_proj = nn.Linear(di, d_model, bias=bias, **fk)
+
+    def _w(self, lin, cd):
+        return lin.weight.to(cd)
+
+    def forward(self, x, state=None):
+        """x (B, L, d) -> (out (B, L, d), (conv_state, ssm_state))."""
+        if not x.is_cuda:
+            raise RuntimeError("mtts.Mamba runs on the HIP kernels only (no CPU path)")
+        cd = x.dtype
+        Bsz, Ln, _ = x.shape
+        if state is not None and Ln == 1:
+            return self.step(x, state)
+        xz = F.linear(x, self._w(self.in_proj, cd), None if self.in_proj.bias is None else self.in_proj.bias.to(cd))
+        conv_state_in = h0 = None
+        if state is not None:
+            conv_state_in, h0 = state
+        y, conv_state, ssm_state = MambaInnerFn.apply(
+            xz, self.conv1d.weight, self.conv1d.bias, self._w(self.x_proj, cd), self._w(self.dt_proj, cd),
+            self.A_log, self.D, self.dt_proj.bias, conv_state_in, h0)
+        out = F.linear(y, self._w(self.out_proj, cd),
+                       None if self.out_proj.bias is None else self.out_proj.bias.to(cd))
+        return out, (conv_state, ssm_state)
+
+    @torch.no_grad()
+    def step(self, x, state):
+        """One decode step; updates conv_state / ssm_state IN PLACE ([upstream]
+        Mamba.step semantics) and returns them."""
+        conv_state, ssm_state = state
+        cd = x.dtype
+        di, N, r = self.d_inner, self.d_state, self.dt_rank
+        xz = F.linear(x[:, 0], self._w(self.in_proj, cd))
+        xs, z = xz[:, :di], xz[:, di:]
+        u = ops.conv_update(xs, conv_state, self.conv1d.weight.detach().reshape(di, -1).float().contiguous(),
+                            None if self.conv1d.bias is None else self.conv1d.bias.detach().float(), True)
+        x_dbl = F.linear(u, self._w(self.x_proj, cd))
+        dt, Bm, Cm = x_dbl[:, :r], x_dbl[:, r:r + N], x_dbl[:, r + N:]
+        delta = F.linear(dt, self._w(self.dt_proj, cd))
+        A = -torch.exp(self.A_log.detach().float())
+        y = ops.state_update(ssm_state, u, delta, A, Bm.contiguous(), Cm.contiguous(), self.D.detach().float(),
+                             z, self.dt_proj.bias.detach().float(), True)
+        out = F.linear(y, self._w(self.out_proj, cd))
+        return out[:, None], (conv_state, ssm_state)

@@ -1,0 +1,416 @@
+"""Tensor-level wrappers and autograd Functions over libmtts.so.
+
+Every function here launches HIP kernels through the C ABI (mtts._lib); none
+falls back to PyTorch arithmetic.  Activations are channel-last (B, L, C).
+
+Public op API mirroring [upstream] mamba-ssm (layout (B, D, L)):
+    selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None,
+                      delta_softplus=False, return_last_state=False)
+    causal_conv1d_fn(x, weight, bias=None, activation=None)
+    causal_conv1d_update(x, conv_state, weight, bias=None, activation=None)
+    selective_state_update(state, x, dt, A, B, C, D=None, z=None,
+                           dt_bias=None, dt_softplus=False)
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+
+SCAN_CKPT = 16  # must equal kSub in scan.hip
+
+
+def _check_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("libmtts ops need CUDA (HIP) tensors; there is no CPU path")
+
+
+def _f32c(t):
+    return None if t is None else t.detach().to(torch.float32).contiguous()
+
+
+def _bc_ok(t):
+    """B/C views must have N-stride 1 and 16-byte aligned rows."""
+    es = t.element_size()
+    return (t.stride(-1) == 1 and t.data_ptr() % 16 == 0 and (t.stride(0) * es) % 16 == 0
+            and (t.stride(1) * es) % 16 == 0)
+
+
+def _bc(t):
+    return t if _bc_ok(t) else t.contiguous()
+
+
+# ---------------------------------------------------------------------------
+# selective scan (channel-last)
+# ---------------------------------------------------------------------------
+def _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, ckpt):
+    Bsz, Ln, Dm = u.shape
+    for t in (u, delta, out) + ((z,) if z is not None else ()):
+        if t.stride(-1) != 1:
+            raise ValueError("scan: channel stride must be 1")
+    a = L.ScanFwdArgs()
+    a.batch, a.seqlen, a.dim, a.dstate = Bsz, Ln, Dm, A.shape[1]
+    a.dtype_io, a.dtype_bc = L.dtype_code(u), L.dtype_code(Bm)
+    a.delta_softplus = int(bool(softplus))
+    a.ckpt_chunk = SCAN_CKPT if ckpt is not None else 0
+    a.u_bs, a.u_ls = u.stride(0), u.stride(1)
+    a.delta_bs, a.delta_ls = delta.stride(0), delta.stride(1)
+    if z is not None:
+        a.z_bs, a.z_ls = z.stride(0), z.stride(1)
+    a.out_bs, a.out_ls = out.stride(0), out.stride(1)
+    a.B_bs, a.B_ls = Bm.stride(0), Bm.stride(1)
+    a.C_bs, a.C_ls = Cm.stride(0), Cm.stride(1)
+    a.u, a.delta, a.A, a.Bm, a.Cm = u.data_ptr(), delta.data_ptr(), A.data_ptr(), Bm.data_ptr(), Cm.data_ptr()
+    a.D, a.z, a.delta_bias, a.h0 = L.ptr(D), L.ptr(z), L.ptr(delta_bias), L.ptr(h0)
+    a.out, a.last_state, a.ckpt = out.data_ptr(), L.ptr(last), L.ptr(ckpt)
+    return a
+
+
+def scan_fwd(u, delta, A, Bm, Cm, D=None, z=None, delta_bias=None, softplus=True, h0=None,
+             want_last=False, want_ckpt=False, out=None):
+    """u, delta, z: (B, L, D) channel-last; Bm, Cm: (B, L, N); A: (D, N) fp32.
+    Returns (out, last_state | None, ckpt | None)."""
+    _check_cuda(u, delta, A, Bm, Cm, D, z, delta_bias, h0)
+    Bsz, Ln, Dm = u.shape
+    N = A.shape[1]
+    if delta.dtype != u.dtype or (z is not None and z.dtype != u.dtype):
+        raise TypeError("scan: u/delta/z must share a dtype")
+    Bm, Cm = _bc(Bm), _bc(Cm)
+    if Cm.dtype != Bm.dtype:
+        Cm = Cm.to(Bm.dtype)
+    A, D, delta_bias, h0 = _f32c(A), _f32c(D), _f32c(delta_bias), _f32c(h0)
+    if out is None:
+        out = torch.empty(Bsz, Ln, Dm, device=u.device, dtype=u.dtype)
+    last = torch.empty(Bsz, Dm, N, device=u.device, dtype=torch.float32) if want_last else None
+    ckpt = (torch.empty(Bsz, (Ln + SCAN_CKPT - 1) // SCAN_CKPT, Dm, N, device=u.device, dtype=torch.float32)
+            if want_ckpt else None)
+    a = _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, ckpt)
+    L.call("mtts_selective_scan_fwd", a)
+    return out, last, ckpt
+
+
+def scan_bwd(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, ckpt, dout,
+             du=None, ddelta=None, dz=None, dB=None, dC=None, need_dh0=False):
+    """Backward of scan_fwd.  du/ddelta/dz may be preallocated (strided)
+    views to write into; dB/dC (B, L, N) fp32 views likewise.
+    Returns du, ddelta, dz, dB, dC, dA, dD, ddelta_bias, dh0."""
+    Bsz, Ln, Dm = u.shape
+    N = A.shape[1]
+    dev = u.device
+    Bm, Cm = _bc(Bm), _bc(Cm)
+    if Cm.dtype != Bm.dtype:
+        Cm = Cm.to(Bm.dtype)
+    A, D, delta_bias, h0 = _f32c(A), _f32c(D), _f32c(delta_bias), _f32c(h0)
+    dout = dout if dout.stride(-1) == 1 else dout.contiguous()
+    if dout.dtype != u.dtype:
+        dout = dout.to(u.dtype)
+    du = torch.empty(Bsz, Ln, Dm, device=dev, dtype=u.dtype) if du is None else du
+    ddelta = torch.empty(Bsz, Ln, Dm, device=dev, dtype=u.dtype) if ddelta is None else ddelta
+    if z is not None and dz is None:
+        dz = torch.empty(Bsz, Ln, Dm, device=dev, dtype=u.dtype)
+    dB = torch.empty(Bsz, Ln, N, device=dev, dtype=torch.float32) if dB is None else dB
+    dC = torch.empty(Bsz, Ln, N, device=dev, dtype=torch.float32) if dC is None else dC
+    dA = torch.empty(Dm, N, device=dev, dtype=torch.float32)
+    dD = torch.empty(Dm, device=dev, dtype=torch.float32)
+    dbias = torch.empty(Dm, device=dev, dtype=torch.float32)
+    dh0 = torch.empty(Bsz, Dm, N, device=dev, dtype=torch.float32) if need_dh0 else None
+    ws = torch.empty(L.lib().mtts_selective_scan_bwd_workspace(Bsz, Dm, Ln, N), device=dev, dtype=torch.uint8)
+    dummy_out = dout  # the forward's `out` is not read by the backward
+    b = L.ScanBwdArgs()
+    b.f = _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, dummy_out, None, ckpt)
+    b.dout, b.dout_bs, b.dout_ls = dout.data_ptr(), dout.stride(0), dout.stride(1)
+    b.du, b.du_bs, b.du_ls = du.data_ptr(), du.stride(0), du.stride(1)
+    b.ddelta, b.ddelta_bs, b.ddelta_ls = ddelta.data_ptr(), ddelta.stride(0), ddelta.stride(1)
+    if dz is not None:
+        b.dz, b.dz_bs, b.dz_ls = dz.data_ptr(), dz.stride(0), dz.stride(1)
+    b.dB, b.dB_bs, b.dB_ls = dB.data_ptr(), dB.stride(0), dB.stride(1)
+    b.dC, b.dC_bs, b.dC_ls = dC.data_ptr(), dC.stride(0), dC.stride(1)
+    b.dA, b.dD, b.ddelta_bias, b.dh0, b.workspace = dA.data_ptr(), dD.data_ptr(), dbias.data_ptr(), L.ptr(dh0), ws.data_ptr()
+    L.call("mtts_selective_scan_bwd", b)
+    return du, ddelta, dz, dB, dC, dA, dD, dbias, dh0
+
+
+class SelectiveScanFn(torch.autograd.Function):
+    """Channel-last selective scan with autograd (fwd + bwd in HIP)."""
+
+    @staticmethod
+    def forward(ctx, u, delta, A, Bm, Cm, D, z, delta_bias, softplus, return_last_state):
+        out, last, ckpt = scan_fwd(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, want_last=True, want_ckpt=True)
+        ctx.softplus = softplus
+        ctx.has = (D is not None, z is not None, delta_bias is not None)
+        ctx.bc_dtype = Bm.dtype
+        ctx.save_for_backward(u, delta, A, Bm, Cm, D, z, delta_bias, ckpt)
+        ctx.mark_non_differentiable(last)
+        return out, last
+
+    @staticmethod
+    def backward(ctx, dout, dlast):
+        u, delta, A, Bm, Cm, D, z, delta_bias, ckpt = ctx.saved_tensors
+        du, ddelta, dz, dB, dC, dA, dD, dbias, _ = scan_bwd(u, delta, A, Bm, Cm, D, z, delta_bias, ctx.softplus,
+                                                            None, ckpt, dout)
+        hasD, hasz, hasb = ctx.has
+        return (du, ddelta, dA.to(A.dtype), dB.to(Bm.dtype), dC.to(Cm.dtype), dD.to(D.dtype) if hasD else None,
+                dz if hasz else None, dbias.to(delta_bias.dtype) if hasb else None, None, None)
+
+
+def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
+                      return_last_state=False):
+    """mamba-ssm signature and (B, D, L) layout; see oracle selective_scan_ref."""
+    cl = lambda t: None if t is None else t.transpose(1, 2).contiguous()  # noqa: E731
+    out, last = SelectiveScanFn.apply(cl(u), cl(delta), A, cl(B), cl(C), D, cl(z), delta_bias, delta_softplus,
+                                      return_last_state)
+    out = out.transpose(1, 2)
+    return (out, last) if return_last_state else out
+
+
+# ---------------------------------------------------------------------------
+# causal conv1d (channel-last)
+# ---------------------------------------------------------------------------
+def _conv_args(x, w, bias, silu, state_in, out, state_out):
+    Bsz, Ln, Dm = x.shape
+    a = L.ConvFwdArgs()
+    a.batch, a.dim, a.seqlen, a.width, a.dtype, a.silu = Bsz, Dm, Ln, w.shape[-1], L.dtype_code(x), int(silu)
+    a.x_bs, a.x_ls = x.stride(0), x.stride(1)
+    a.out_bs, a.out_ls = out.stride(0), out.stride(1)
+    a.x, a.w, a.bias, a.conv_state_in = x.data_ptr(), w.data_ptr(), L.ptr(bias), L.ptr(state_in)
+    a.out, a.conv_state_out = out.data_ptr(), L.ptr(state_out)
+    return a
+
+
+def conv_fwd(x, w, bias=None, silu=True, state_in=None, want_state=False, out=None):
+    """x (B, L, D) channel-last (may be a strided view); w (D, K)."""
+    _check_cuda(x, w, bias, state_in)
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    Bsz, Ln, Dm = x.shape
+    w = _f32c(w.reshape(Dm, -1))
+    bias, state_in = _f32c(bias), _f32c(state_in)
+    out = torch.empty(Bsz, Ln, Dm, device=x.device, dtype=x.dtype) if out is None else out
+    st = torch.empty(Bsz, Dm, w.shape[1], device=x.device, dtype=torch.float32) if want_state else None
+    L.call("mtts_causal_conv1d_fwd", _conv_args(x, w, bias, silu, state_in, out, st))
+    return out, st
+
+
+def conv_bwd(x, w, bias, dout, silu=True, dx=None):
+    Bsz, Ln, Dm = x.shape
+    w = _f32c(w.reshape(Dm, -1))
+    bias = _f32c(bias)
+    dout = dout if dout.stride(-1) == 1 else dout.contiguous()
+    if dout.dtype != x.dtype:
+        dout = dout.to(x.dtype)
+    dx = torch.empty(Bsz, Ln, Dm, device=x.device, dtype=x.dtype) if dx is None else dx
+    dw = torch.empty(Dm, w.shape[1], device=x.device, dtype=torch.float32)
+    db = torch.empty(Dm, device=x.device, dtype=torch.float32)
+    ws = torch.empty(L.lib().mtts_causal_conv1d_bwd_workspace(Bsz, Dm, Ln, w.shape[1]), device=x.device,
+                     dtype=torch.uint8)
+    b = L.ConvBwdArgs()
+    b.f = _conv_args(x, w, bias, silu, None, dout, None)
+    b.dout, b.dout_bs, b.dout_ls = dout.data_ptr(), dout.stride(0), dout.stride(1)
+    b.dx, b.dx_bs, b.dx_ls = dx.data_ptr(), dx.stride(0), dx.stride(1)
+    b.dw, b.dbias, b.workspace = dw.data_ptr(), db.data_ptr(), ws.data_ptr()
+    L.call("mtts_causal_conv1d_bwd", b)
+    return dx, dw, db
+
+
+class CausalConv1dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, silu):
+        out, _ = conv_fwd(x, w, bias, silu)
+        ctx.silu = silu
+        ctx.save_for_backward(x, w, bias)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w, bias = ctx.saved_tensors
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        dx, dw, db = conv_bwd(x, w, bias, dout, ctx.silu)
+        return dx, dw.reshape(w.shape).to(w.dtype), (db.to(bias.dtype) if bias is not None else None), None
+
+
+def causal_conv1d_fn(x, weight, bias=None, activation=None):
+    """[upstream] causal_conv1d_fn signature, x (B, D, L)."""
+    silu = activation in ("silu", "swish")
+    out = CausalConv1dFn.apply(x.transpose(1, 2), weight, bias, silu)
+    return out.transpose(1, 2)
+
+
+# ---------------------------------------------------------------------------
+# decode step
+# ---------------------------------------------------------------------------
+def conv_update(x, conv_state, w, bias=None, silu=True, out=None):
+    """x (B, D); conv_state (B, D, K) fp32 updated IN PLACE.  Returns out (B, D)."""
+    _check_cuda(x, conv_state, w)
+    Bsz, Dm = x.shape
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    out = torch.empty(Bsz, Dm, device=x.device, dtype=x.dtype) if out is None else out
+    a = L.ConvUpdateArgs()
+    a.batch, a.dim, a.width, a.dtype, a.silu = Bsz, Dm, conv_state.shape[-1], L.dtype_code(x), int(silu)
+    a.x_bs, a.out_bs = x.stride(0), out.stride(0)
+    a.x, a.conv_state, a.w, a.bias, a.out = x.data_ptr(), conv_state.data_ptr(), w.data_ptr(), L.ptr(bias), out.data_ptr()
+    L.call("mtts_causal_conv1d_update", a)
+    return out
+
+
+def state_update(state, x, dt, A, Bm, Cm, D=None, z=None, dt_bias=None, softplus=True, out=None):
+    """state (B, D, N) fp32 updated IN PLACE; x/dt/z (B, D); Bm/Cm (B, N)."""
+    _check_cuda(state, x, dt, A, Bm, Cm)
+    Bsz, Dm = x.shape
+    out = torch.empty(Bsz, Dm, device=x.device, dtype=x.dtype) if out is None else out
+    a = L.StateUpdateArgs()
+    a.batch, a.dim, a.dstate = Bsz, Dm, state.shape[-1]
+    a.dtype_io, a.dtype_bc, a.dt_softplus = L.dtype_code(x), L.dtype_code(Bm), int(softplus)
+    a.x_bs, a.dt_bs, a.out_bs, a.B_bs, a.C_bs = x.stride(0), dt.stride(0), out.stride(0), Bm.stride(0), Cm.stride(0)
+    if z is not None:
+        a.z_bs = z.stride(0)
+    a.state, a.x, a.dt, a.A, a.Bm, a.Cm = state.data_ptr(), x.data_ptr(), dt.data_ptr(), A.data_ptr(), Bm.data_ptr(), Cm.data_ptr()
+    a.D, a.z, a.dt_bias, a.out = L.ptr(D), L.ptr(z), L.ptr(dt_bias), out.data_ptr()
+    L.call("mtts_selective_state_update", a)
+    return out
+
+
+def causal_conv1d_update(x, conv_state, weight, bias=None, activation=None):
+    """[upstream] signature: x (B, D), conv_state (B, D, K) fp32 (in place)."""
+    return conv_update(x, conv_state, _f32c(weight.reshape(x.shape[1], -1)), _f32c(bias),
+                       activation in ("silu", "swish"))
+
+
+def selective_state_update(state, x, dt, A, B, C, D=None, z=None, dt_bias=None, dt_softplus=False):
+    """[upstream] signature: state (B, D, N) fp32 (in place)."""
+    return state_update(state, x, dt, _f32c(A), B.contiguous(), C.contiguous(), _f32c(D), z, _f32c(dt_bias),
+                        dt_softplus)
+
+
+# ---------------------------------------------------------------------------
+# LayerNorm (+ residual, + FiLM)
+# ---------------------------------------------------------------------------
+def _rows(t):
+    """(..., N) with last stride 1 -> (rows, row_stride)."""
+    n = t.shape[-1]
+    if t.stride(-1) != 1:
+        raise ValueError("layernorm: last stride must be 1")
+    rows = t.numel() // n
+    if t.dim() == 1:
+        return rows, n
+    # require a uniform row stride over the flattened leading dims
+    st = t.stride(-2)
+    for d in range(t.dim() - 2):
+        if t.shape[d] > 1 and t.stride(d) != st * _prod(t.shape[d + 1:-1]):
+            raise ValueError("layernorm: leading dims must be collapsible")
+    return rows, st
+
+
+def _prod(s):
+    p = 1
+    for v in s:
+        p *= v
+    return p
+
+
+def _ln_args(x, w, b, eps, res, x_sum, gamma, beta, rows_per_group, y, mean, rstd):
+    rows, xrs = _rows(x)
+    a = L.LNArgs()
+    a.rows, a.cols, a.dtype, a.eps = rows, x.shape[-1], L.dtype_code(x), float(eps)
+    a.rows_per_group = int(rows_per_group) if gamma is not None else 0
+    a.x_rs, a.y_rs = xrs, _rows(y)[1]
+    a.x, a.w, a.b, a.y, a.mean, a.rstd = x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr()
+    if res is not None:
+        a.res, a.res_rs = res.data_ptr(), _rows(res)[1]
+        if x_sum is not None:
+            a.x_sum, a.xsum_rs = x_sum.data_ptr(), _rows(x_sum)[1]
+    if gamma is not None:
+        a.gamma, a.beta, a.gb_rs, a.gb_dtype = gamma.data_ptr(), beta.data_ptr(), gamma.stride(0), L.dtype_code(gamma)
+    return a
+
+
+def layernorm_fwd(x, w, b, eps=1e-5, res=None, gamma=None, beta=None, rows_per_group=1, want_sum=True):
+    """y = LN(x [+ res]) * w + b [then gamma*y + beta per row group].
+    Returns (y, mean, rstd, x_sum | None)."""
+    _check_cuda(x, w, b, res, gamma, beta)
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    if res is not None and (res.shape != x.shape):
+        raise ValueError("layernorm: res shape mismatch")
+    if res is not None and res.dtype != x.dtype:
+        res = res.to(x.dtype)
+    w, b = _f32c(w), _f32c(b)
+    if gamma is not None:
+        gamma = gamma if gamma.stride(-1) == 1 else gamma.contiguous()
+        beta = beta if beta.stride(-1) == 1 else beta.contiguous()
+        if beta.stride(0) != gamma.stride(0):
+            beta = beta.contiguous()
+            gamma = gamma.contiguous()
+    rows = x.numel() // x.shape[-1]
+    y = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    x_sum = torch.empty(x.shape, device=x.device, dtype=x.dtype) if (res is not None and want_sum) else None
+    L.call("mtts_layernorm_fwd", _ln_args(x, w, b, eps, res, x_sum, gamma, beta, rows_per_group, y, mean, rstd))
+    return y, mean, rstd, x_sum
+
+
+def layernorm_bwd(xn, w, b, eps, gamma, beta, rows_per_group, mean, rstd, dy, dx_acc=None):
+    """xn: the normalised input (x, or x + res).  Returns dx, dw, db, dgamma, dbeta."""
+    dy = dy if dy.stride(-1) == 1 else dy.contiguous()
+    if dy.dtype != xn.dtype:
+        dy = dy.to(xn.dtype)
+    w, b = _f32c(w), _f32c(b)
+    rows, cols = mean.numel(), xn.shape[-1]
+    dx = torch.empty(xn.shape, device=xn.device, dtype=xn.dtype)
+    dw = torch.empty(cols, device=xn.device, dtype=torch.float32)
+    db = torch.empty(cols, device=xn.device, dtype=torch.float32)
+    film = gamma is not None
+    G = rows // rows_per_group if film else 0
+    dg = torch.empty(G, cols, device=xn.device, dtype=torch.float32) if film else None
+    dbe = torch.empty(G, cols, device=xn.device, dtype=torch.float32) if film else None
+    ws = torch.empty(L.lib().mtts_layernorm_bwd_workspace(rows, cols, rows_per_group if film else 0),
+                     device=xn.device, dtype=torch.uint8)
+    bb = L.LNBwdArgs()
+    bb.f = _ln_args(xn, w, b, eps, None, None, gamma, beta, rows_per_group, xn, mean, rstd)
+    bb.dy, bb.dy_rs = dy.data_ptr(), _rows(dy)[1]
+    if dx_acc is not None:
+        dx_acc = dx_acc if dx_acc.stride(-1) == 1 else dx_acc.contiguous()
+        if dx_acc.dtype != xn.dtype:
+            dx_acc = dx_acc.to(xn.dtype)
+        bb.dx_acc, bb.dxacc_rs = dx_acc.data_ptr(), _rows(dx_acc)[1]
+    bb.dx, bb.dx_rs = dx.data_ptr(), _rows(dx)[1]
+    bb.dw, bb.db, bb.dgamma, bb.dbeta, bb.workspace = dw.data_ptr(), db.data_ptr(), L.ptr(dg), L.ptr(dbe), ws.data_ptr()
+    L.call("mtts_layernorm_bwd", bb)
+    return dx, dw, db, dg, dbe
+
+
+class LayerNormFn(torch.autograd.Function):
+    """y = FiLM(LN(x [+ res])); returns (y, x_sum) where x_sum = x + res (or x).
+    gamma/beta: (G, N) with G = rows / rows_per_group."""
+
+    @staticmethod
+    def forward(ctx, x, res, w, b, gamma, beta, eps, rows_per_group):
+        y, mean, rstd, x_sum = layernorm_fwd(x, w, b, eps, res, gamma, beta, rows_per_group)
+        xn = x_sum if res is not None else x
+        ctx.eps, ctx.rpg = eps, rows_per_group
+        ctx.has_res = res is not None
+        ctx.dtypes = (w.dtype, b.dtype, None if gamma is None else gamma.dtype)
+        ctx.save_for_backward(xn, w, b, gamma, beta, mean, rstd)
+        if res is None:
+            x_sum = x.new_empty(0)
+            ctx.mark_non_differentiable(x_sum)
+        return y, x_sum
+
+    @staticmethod
+    def backward(ctx, dy, dsum):
+        xn, w, b, gamma, beta, mean, rstd = ctx.saved_tensors
+        if dsum is not None and dsum.numel() == 0:
+            dsum = None
+        dx, dw, db, dg, dbe = layernorm_bwd(xn, w, b, ctx.eps, gamma, beta, ctx.rpg, mean, rstd, dy, dx_acc=dsum)
+        wd, bd, gd = ctx.dtypes
+        dres = dx if ctx.has_res else None
+        return (dx, dres, dw.to(wd), db.to(bd), None if dg is None else dg.to(gd),
+                None if dbe is None else dbe.to(gd), None, None)
+
+
+def layer_norm(x, w, b, eps=1e-5, res=None, gamma=None, beta=None, rows_per_group=1):
+    """Returns (y, x_sum) with x_sum = x + res (an empty tensor when res is None)."""
+    return LayerNormFn.apply(x, res, w, b, gamma, beta, eps, rows_per_group)

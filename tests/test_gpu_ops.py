@@ -1,0 +1,253 @@
+"""GPU parity of the libmtts kernels against the golden vectors (HF's
+independent Mamba v1, float64) and the CPU oracle.  Tolerance: the north
+star's 1e-3 relative (fp32), measured as max|err| <= 1e-3 * max|ref| per
+tensor; bf16 I/O runs use a looser, stated bound."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mamba_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RTOL = 1e-3
+
+
+def close(out, ref, rtol=RTOL, name=""):
+    out = torch.as_tensor(out).detach().double().cpu()
+    ref = torch.as_tensor(np.asarray(ref) if not torch.is_tensor(ref) else ref).double().cpu()
+    assert out.shape == ref.shape, f"{name}: shape {tuple(out.shape)} vs {tuple(ref.shape)}"
+    assert torch.isfinite(out).all(), f"{name}: non-finite"
+    err = (out - ref).abs().max().item()
+    scale = max(ref.abs().max().item(), 1e-6)
+    assert err <= rtol * scale, f"{name}: max|err|={err:.3e} > {rtol}*{scale:.3e}"
+
+
+def cl(a, dtype=torch.float32):
+    """(B, D, L) numpy -> channel-last (B, L, D) cuda tensor"""
+    return torch.from_numpy(np.ascontiguousarray(np.swapaxes(a, 1, 2))).to(DEV, dtype)
+
+
+def g32(a):
+    return torch.from_numpy(np.asarray(a)).to(DEV, torch.float32)
+
+
+@pytest.fixture(params=["1", "2", "4"])
+def scan_p(request):
+    old = os.environ.get("MTTS_SCAN_P")
+    os.environ["MTTS_SCAN_P"] = request.param
+    yield int(request.param)
+    if old is None:
+        del os.environ["MTTS_SCAN_P"]
+    else:
+        os.environ["MTTS_SCAN_P"] = old
+
+
+@pytest.mark.parametrize("name", ["scan_full.npz", "scan_plain.npz", "scan_short.npz"])
+def test_scan_fwd_bwd_vs_golden(golden, name, scan_p):
+    from mtts import ops
+    g = golden(name)
+    sp = bool(g["softplus"])
+    u, delta, z = cl(g["u"]), cl(g["delta"]), cl(g["z"]) if "z" in g else None
+    Bm, Cm = cl(g["B"]), cl(g["C"])
+    A = g32(g["A"])
+    D = g32(g["D"]) if "D" in g else None
+    bias = g32(g["delta_bias"]) if "delta_bias" in g else None
+    out, last, ckpt = ops.scan_fwd(u, delta, A, Bm, Cm, D, z, bias, sp, want_last=True, want_ckpt=True)
+    close(out.transpose(1, 2), g["out"], name="out")
+    close(last, g["last_state"], name="last_state")
+    du, dd, dz, dB, dC, dA, dD, db, _ = ops.scan_bwd(u, delta, A, Bm, Cm, D, z, bias, sp, None, ckpt, cl(g["dout"]))
+    close(du.transpose(1, 2), g["du"], name="du")
+    close(dd.transpose(1, 2), g["ddelta"], name="ddelta")
+    close(dB.transpose(1, 2), g["dB"], name="dB")
+    close(dC.transpose(1, 2), g["dC"], name="dC")
+    close(dA, g["dA"], name="dA")
+    if z is not None:
+        close(dz.transpose(1, 2), g["dz"], name="dz")
+    if D is not None:
+        close(dD, g["dD"], name="dD")
+    if bias is not None:
+        close(db, g["ddelta_bias"], name="ddelta_bias")
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (2, 3, 5), (3, 100, 37), (2, 70, 130), (1, 64, 1000)])
+def test_scan_ragged_shapes_and_h0_split(shape, scan_p):
+    """Ragged (B, D, L) incl. L=1, D not a multiple of 64, L not a multiple of
+    16; and scanning [0,L1) then [L1,L) from h0=last_state equals one scan."""
+    from mtts import ops
+    torch.manual_seed(sum(shape))
+    B, D, L = shape
+    u = torch.randn(B, L, D, device=DEV)
+    dl = torch.randn(B, L, D, device=DEV) * 0.5
+    z = torch.randn(B, L, D, device=DEV)
+    A = -torch.exp(torch.randn(D, 16, device=DEV) * 0.5)
+    Bm = torch.randn(B, L, 16, device=DEV)
+    Cm = torch.randn(B, L, 16, device=DEV)
+    Dp = torch.randn(D, device=DEV)
+    bias = torch.randn(D, device=DEV) * 0.1
+    out, last, _ = ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, want_last=True)
+    ref, rlast = R.selective_scan_ref(*(t.double().cpu() for t in (u.transpose(1, 2), dl.transpose(1, 2), A,
+                                                                  Bm.transpose(1, 2), Cm.transpose(1, 2), Dp,
+                                                                  z.transpose(1, 2), bias)),
+                                      delta_softplus=True, return_last_state=True)
+    close(out.transpose(1, 2), ref, name="out")
+    close(last, rlast, name="last")
+    if L > 1:
+        L1 = L // 2
+        o1, l1, _ = ops.scan_fwd(u[:, :L1], dl[:, :L1], A, Bm[:, :L1].contiguous(), Cm[:, :L1].contiguous(), Dp,
+                                 z[:, :L1], bias, True, want_last=True)
+        o2, l2, _ = ops.scan_fwd(u[:, L1:], dl[:, L1:], A, Bm[:, L1:].contiguous(), Cm[:, L1:].contiguous(), Dp,
+                                 z[:, L1:], bias, True, h0=l1, want_last=True)
+        close(torch.cat([o1, o2], 1), out, rtol=1e-5, name="split-out")
+        close(l2, last, rtol=1e-5, name="split-last")
+
+
+def test_scan_bf16_io(golden):
+    """bf16 u/delta/z/B/C/out with fp32 math: bounded by bf16 input rounding."""
+    from mtts import ops
+    g = golden("scan_full.npz")
+    bf = torch.bfloat16
+    out, _, _ = ops.scan_fwd(cl(g["u"], bf), cl(g["delta"], bf), g32(g["A"]), cl(g["B"], bf), cl(g["C"], bf),
+                             g32(g["D"]), cl(g["z"], bf), g32(g["delta_bias"]), True)
+    ref = R.selective_scan_ref(*(torch.from_numpy(g[k]).to(bf).double() for k in ("u", "delta")),
+                               torch.from_numpy(g["A"]).double(),
+                               *(torch.from_numpy(g[k]).to(bf).double() for k in ("B", "C")),
+                               torch.from_numpy(g["D"]).double(), torch.from_numpy(g["z"]).to(bf).double(),
+                               torch.from_numpy(g["delta_bias"]).double(), True)
+    close(out.transpose(1, 2), ref, rtol=1e-2, name="bf16 out")
+
+
+def test_scan_deterministic():
+    from mtts import ops
+    torch.manual_seed(0)
+    B, L, D = 2, 300, 256
+    args = [torch.randn(B, L, D, device=DEV), torch.randn(B, L, D, device=DEV) * 0.3,
+            -torch.rand(D, 16, device=DEV) - 0.1, torch.randn(B, L, 16, device=DEV), torch.randn(B, L, 16, device=DEV)]
+    o1, _, ck = ops.scan_fwd(*args, want_ckpt=True)
+    o2, _, _ = ops.scan_fwd(*args)
+    assert torch.equal(o1, o2)
+    g = torch.randn(B, L, D, device=DEV)
+    r1 = ops.scan_bwd(*args, None, None, None, True, None, ck, g)
+    r2 = ops.scan_bwd(*args, None, None, None, True, None, ck, g)
+    for a, b in zip(r1, r2):
+        if a is not None:
+            assert torch.equal(a, b)
+
+
+def test_conv1d_fwd_bwd_update_vs_golden(golden):
+    from mtts import ops
+    g = golden("conv1d.npz")
+    x = cl(g["x"])
+    w, b = g32(g["w"]), g32(g["b"])
+    out, st = ops.conv_fwd(x, w, b, True, want_state=True)
+    close(out.transpose(1, 2), g["out"], name="conv out")
+    close(st, g["x"][:, :, -4:], name="conv state")
+    dx, dw, db = ops.conv_bwd(x, w, b, cl(g["dout"]), True)
+    close(dx.transpose(1, 2), g["dx"], name="dx")
+    close(dw, g["dw"], name="dw")
+    close(db, g["db"], name="db")
+    xs = torch.from_numpy(g["xs"]).to(DEV)
+    state = torch.zeros(2, 64, 4, device=DEV)
+    outs = [ops.conv_update(xs[:, :, t].contiguous(), state, w, b, True) for t in range(xs.shape[-1])]
+    close(torch.stack(outs, -1), g["upd_out"], name="update out")
+    close(state, g["upd_state"], name="update state")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(1, 1, 8), (2, 37, 24), (2, 100, 512), (1, 33, 2048)])
+def test_conv1d_shapes_strided_and_prefix_state(shape, dtype):
+    """strided input view (xz[..., :D]), conv_state_in prefix == running on the
+    concatenated sequence, ragged L."""
+    from mtts import ops
+    torch.manual_seed(1)
+    B, L, D = shape
+    xz = torch.randn(B, L + 6, 2 * D, device=DEV).to(dtype)
+    x = xz[:, 6:, :D]
+    prefix = xz[:, :6, :D]
+    w = torch.randn(D, 4, device=DEV)
+    b = torch.randn(D, device=DEV)
+    _, st = ops.conv_fwd(prefix, w, b, True, want_state=True)
+    out, st2 = ops.conv_fwd(x, w, b, True, state_in=st, want_state=True)
+    full, stf = ops.conv_fwd(xz[:, :, :D], w, b, True, want_state=True)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    close(out.float(), full[:, 6:].float(), rtol=tol, name="prefix")
+    close(st2, stf, rtol=1e-6, name="state")
+    ref, _ = R.causal_conv1d_ref(x.transpose(1, 2).double().cpu(), w.double().cpu(), b.double().cpu(), "silu",
+                                 st.double().cpu())
+    close(out.transpose(1, 2).float(), ref, rtol=tol, name="vs oracle")
+    go = torch.randn(B, L, D, device=DEV).to(dtype)
+    dx, dw, db = ops.conv_bwd(xz[:, 6:, :D].contiguous(), w, b, go, True)
+    xr = x.transpose(1, 2).double().cpu().requires_grad_(True)
+    wr, br = w.double().cpu().requires_grad_(True), b.double().cpu().requires_grad_(True)
+    o, _ = R.causal_conv1d_ref(xr, wr, br, "silu")
+    (o * go.transpose(1, 2).double().cpu()).sum().backward()
+    close(dx.transpose(1, 2).float(), xr.grad, rtol=tol, name="dx")
+    close(dw, wr.grad, rtol=tol, name="dw")
+    close(db, br.grad, rtol=tol, name="db")
+
+
+def test_state_update_vs_golden(golden):
+    from mtts import ops
+    g = golden("state_update.npz")
+    A, D, bias = g32(g["A"]), g32(g["D"]), g32(g["delta_bias"])
+    st = torch.zeros(2, 32, 16, device=DEV)
+    outs = []
+    for t in range(g["u"].shape[-1]):
+        sl = lambda k: torch.from_numpy(np.ascontiguousarray(g[k][..., t])).to(DEV)  # noqa: E731
+        outs.append(ops.state_update(st, sl("u"), sl("delta"), A, sl("B"), sl("C"), D, sl("z"), bias, True))
+    close(torch.stack(outs, -1), g["step_out"], name="step out")
+    close(st, g["step_state"], name="step state")
+    close(torch.stack(outs, -1), g["full_out"], name="step == full scan")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols,rows,film", [(64, 6, False), (1024, 64, True), (512, 40, True), (2048, 17, False),
+                                            (96 * 2, 5, False)])
+def test_layernorm_res_film_fwd_bwd(dtype, cols, rows, film):
+    from mtts import ops
+    torch.manual_seed(cols + rows)
+    G = 2 if (film and rows % 2 == 0) else 1
+    rpg = rows // G
+    x = torch.randn(rows, cols, device=DEV, dtype=dtype, requires_grad=True)
+    res = torch.randn(rows, cols, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(cols, device=DEV)).requires_grad_(True)
+    b = (0.1 * torch.randn(cols, device=DEV)).requires_grad_(True)
+    gam = torch.randn(G, cols, device=DEV, requires_grad=True) if film else None
+    bet = torch.randn(G, cols, device=DEV, requires_grad=True) if film else None
+    y, xs = ops.layer_norm(x, w, b, 1e-5, res=res, gamma=gam, beta=bet, rows_per_group=rpg)
+    gy = torch.randn_like(y)
+    gs = torch.randn_like(xs)
+    (y.float() * gy.float()).sum().add((xs.float() * gs.float()).sum()).backward()
+    # fp64 reference
+    X, Rr, W, Bb = (t.detach().double().requires_grad_(True) for t in (x, res, w, b))
+    S = X + Rr
+    Y = R.layer_norm_ref(S, W, Bb)
+    if film:
+        Gm, Bt = (t.detach().double().requires_grad_(True) for t in (gam, bet))
+        Y = (Gm.repeat_interleave(rpg, 0) * Y + Bt.repeat_interleave(rpg, 0))
+    (Y * gy.double()).sum().add((S * gs.double()).sum()).backward()
+    tol = 1e-3 if dtype == torch.float32 else 2e-2
+    close(y.float(), Y.detach(), rtol=tol, name="y")
+    close(x.grad.float(), X.grad, rtol=tol, name="dx")
+    close(res.grad.float(), Rr.grad, rtol=tol, name="dres")
+    close(w.grad, W.grad, rtol=tol, name="dw")
+    close(b.grad, Bb.grad, rtol=tol, name="db")
+    if film:
+        close(gam.grad, Gm.grad, rtol=tol, name="dgamma")
+        close(bet.grad, Bt.grad, rtol=tol, name="dbeta")
+
+
+def test_upstream_signature_ops(golden):
+    """mamba-ssm-signature wrappers ((B, D, L) layout) incl. autograd."""
+    from mtts import ops
+    g = golden("scan_full.npz")
+    ins = {k: torch.from_numpy(g[k]).to(DEV).requires_grad_(True) for k in
+           ("u", "delta", "A", "B", "C", "D", "z", "delta_bias")}
+    out = ops.selective_scan_fn(ins["u"], ins["delta"], ins["A"], ins["B"], ins["C"], ins["D"], ins["z"],
+                                ins["delta_bias"], delta_softplus=True)
+    close(out, g["out"], name="out")
+    (out * torch.from_numpy(g["dout"]).to(DEV)).sum().backward()
+    for k, t in ins.items():
+        close(t.grad, g["d" + k], name="d" + k)
