@@ -84,8 +84,11 @@ typedef struct {
   void* out;
   float* last_state;       /* optional */
   float* ckpt;             /* optional */
+  void* workspace;         /* mtts_selective_scan_fwd_workspace() bytes */
 } MttsScanFwdArgs;
 
+/* Scratch for the sequence-segment pass (0 bytes when B*D fills the chip). */
+int64_t mtts_selective_scan_fwd_workspace(int batch, int dim, int seqlen, int dstate);
 int mtts_selective_scan_fwd(const MttsScanFwdArgs* a, void* stream);
 
 /* Backward of the forward above (requires the forward's ckpt).

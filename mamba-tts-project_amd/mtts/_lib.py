@@ -29,7 +29,8 @@ class ScanFwdArgs(C.Structure):
                 ("z_bs", i64), ("z_ls", i64), ("out_bs", i64), ("out_ls", i64),
                 ("B_bs", i64), ("B_ls", i64), ("C_bs", i64), ("C_ls", i64),
                 ("u", vp), ("delta", vp), ("A", vp), ("Bm", vp), ("Cm", vp), ("D", vp), ("z", vp),
-                ("delta_bias", vp), ("h0", vp), ("out", vp), ("last_state", vp), ("ckpt", vp)]
+                ("delta_bias", vp), ("h0", vp), ("out", vp), ("last_state", vp), ("ckpt", vp),
+                ("workspace", vp)]
 
 
 class ScanBwdArgs(C.Structure):
@@ -83,6 +84,7 @@ class LNBwdArgs(C.Structure):
 _SIGS = {
     "mtts_abi_version": ([], i32),
     "mtts_last_error": ([], C.c_char_p),
+    "mtts_selective_scan_fwd_workspace": ([i32, i32, i32, i32], i64),
     "mtts_selective_scan_fwd": ([C.POINTER(ScanFwdArgs), vp], i32),
     "mtts_selective_scan_bwd_workspace": ([i32, i32, i32, i32], i64),
     "mtts_selective_scan_bwd": ([C.POINTER(ScanBwdArgs), vp], i32),

@@ -12,6 +12,10 @@ namespace mtts {
 // ---------------------------------------------------------------- errors
 void set_error(const char* fmt, ...);
 
+// out[g * out_gstride + c] = sum over partials p in [g*ppg, (g+1)*ppg) of part[p * pstride + c]
+void colsum(const float* part, int nparts, int ppg, int64_t pstride, int ncols, float* out, int64_t out_gstride,
+            hipStream_t st);
+
 #define MTTS_CHECK(cond, ...)                                                 \
   do {                                                                        \
     if (!(cond)) {                                                            \
@@ -86,13 +90,25 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
-__device__ __forceinline__ float xor32(float v) {
+// v_permlane32_swap(v, v) returns {a, b}: a = v with its upper half replaced
+// by the lower half, b = v with its lower half replaced by the upper half.
+__device__ __forceinline__ float xor32(float v, int lane) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]);
+  return __uint_as_float((lane & 32) ? r[0] : r[1]);
 }
-__device__ __forceinline__ float xor16(float v) {
+// v_permlane16_swap(v, v): a = rows [0,0,2,2], b = rows [1,1,3,3] of v.
+__device__ __forceinline__ float xor16(float v, int lane) {
   auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]);
+  return __uint_as_float((lane & 16) ? r[0] : r[1]);
+}
+// v + v[lane ^ 16] and v + v[lane ^ 32] without selects
+__device__ __forceinline__ float sum_xor16(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 // lane ^ 4 within each 16-lane row
 __device__ __forceinline__ float xor4(float v, int lane) {
@@ -107,8 +123,8 @@ __device__ __forceinline__ float wave_sum(float v) {
   v += dpp<kQuadXor2>(v);
   v += xor4(v, threadIdx.x & 63);
   v += xor8(v);
-  v += xor16(v);
-  v += xor32(v);
+  v = sum_xor16(v);
+  v = sum_xor32(v);
   return v;
 }
 

@@ -195,14 +195,12 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(const MttsConvBwdArgs a, 
   }
 }
 
-__global__ void conv_bwd_reduce(const float* __restrict__ part, int nparts, int dim, float* dw, float* db) {
+__global__ void conv_bwd_split(const float* __restrict__ sums, int dim, float* dw, float* db) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= dim * (kK + 1)) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(int64_t)p * dim * (kK + 1) + idx];
   const int c = idx / (kK + 1), k = idx % (kK + 1);
-  if (k < kK) dw[c * kK + k] = s;
-  else if (db) db[c] = s;
+  if (k < kK) dw[c * kK + k] = sums[idx];
+  else if (db) db[c] = sums[idx];
 }
 
 template <typename T>
@@ -260,7 +258,7 @@ extern "C" int mtts_causal_conv1d_fwd(const MttsConvFwdArgs* a, void* stream) {
 extern "C" int64_t mtts_causal_conv1d_bwd_workspace(int batch, int dim, int seqlen, int width) {
   (void)width;
   const int64_t ntile = (seqlen + kTT - 1) / kTT;
-  return (int64_t)batch * ntile * dim * (kK + 1) * 4 + 256;
+  return ((int64_t)batch * ntile + 1) * dim * (kK + 1) * 4 + 256;
 }
 
 template <typename T, int CPT>
@@ -293,8 +291,10 @@ extern "C" int mtts_causal_conv1d_bwd(const MttsConvBwdArgs* a, void* stream) {
   }
   MTTS_LAUNCH_CHECK("causal_conv1d_bwd");
   const int nparts = f.batch * ((f.seqlen + kTT - 1) / kTT);
-  hipLaunchKernelGGL(conv_bwd_reduce, dim3((f.dim * (kK + 1) + 255) / 256), dim3(256), 0, st, part, nparts, f.dim,
-                     a->dw, a->dbias);
+  float* sums = part + (int64_t)nparts * f.dim * (kK + 1);
+  colsum(part, nparts, nparts, (int64_t)f.dim * (kK + 1), f.dim * (kK + 1), sums, 0, st);
+  hipLaunchKernelGGL(conv_bwd_split, dim3((f.dim * (kK + 1) + 255) / 256), dim3(256), 0, st, sums, f.dim, a->dw,
+                     a->dbias);
   MTTS_LAUNCH_CHECK("causal_conv1d_bwd_reduce");
   return MTTS_OK;
 }

@@ -207,29 +207,6 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const MttsLNBwdAr
   }
 }
 
-// dw/db: sum over all blocks; dgamma/dbeta: sum over the blocks of a group
-__global__ void ln_bwd_reduce(const float* __restrict__ part, int nblk, int cols, int blk_per_group, int ngroups,
-                              float* dw, float* db, float* dg, float* dbeta) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n1 = (int64_t)2 * cols;
-  if (idx < n1) {
-    const int which = idx / cols, c = idx % cols;
-    float s = 0.f;
-    for (int p = 0; p < nblk; ++p) s += part[((int64_t)which * nblk + p) * cols + c];
-    (which == 0 ? dw : db)[c] = s;
-    return;
-  }
-  if (!dg) return;
-  const int64_t j = idx - n1;
-  if (j >= (int64_t)2 * ngroups * cols) return;
-  const int which = 2 + j / ((int64_t)ngroups * cols);
-  const int g = (j / cols) % ngroups, c = j % cols;
-  float s = 0.f;
-  for (int p = g * blk_per_group; p < (g + 1) * blk_per_group && p < nblk; ++p)
-    s += part[((int64_t)which * nblk + p) * cols + c];
-  (which == 2 ? dg : dbeta)[(int64_t)g * cols + c] = s;
-}
-
 static int ln_rb(const MttsLNArgs* a) {
   if (!a->gamma) return 64;
   for (int rb = 64; rb > 1; rb >>= 1)
@@ -269,6 +246,8 @@ static int dispatch_ln(const MttsLNArgs* a, Args... args) {
         case 2: F<T, TG, VEC, 2>::run(a, args...); return MTTS_OK;
         case 3: F<T, TG, VEC, 3>::run(a, args...); return MTTS_OK;
         case 4: F<T, TG, VEC, 4>::run(a, args...); return MTTS_OK;
+        case 6: F<T, TG, VEC, 6>::run(a, args...); return MTTS_OK;
+        case 8: F<T, TG, VEC, 8>::run(a, args...); return MTTS_OK;
         default: break;
       }
     }
@@ -356,11 +335,14 @@ extern "C" int mtts_layernorm_bwd(const MttsLNBwdArgs* a, void* stream) {
   if (rc) return rc;
   MTTS_LAUNCH_CHECK("layernorm_bwd");
   const int nblk = (f.rows + rb - 1) / rb;
-  const int ngroups = f.gamma ? (f.rows + f.rows_per_group - 1) / f.rows_per_group : 0;
-  const int bpg = f.gamma ? f.rows_per_group / rb : 0;
-  const int64_t tot = (int64_t)2 * f.cols + (int64_t)2 * ngroups * f.cols;
-  hipLaunchKernelGGL(ln_bwd_reduce, dim3((tot + 255) / 256), dim3(256), 0, st, part, nblk, f.cols, bpg, ngroups,
-                     a->dw, a->db, a->dgamma, a->dbeta);
+  const int64_t slab = (int64_t)nblk * f.cols;
+  colsum(part, nblk, nblk, f.cols, f.cols, a->dw, 0, st);
+  colsum(part + slab, nblk, nblk, f.cols, f.cols, a->db, 0, st);
+  if (f.gamma) {
+    const int bpg = f.rows_per_group / rb;
+    colsum(part + 2 * slab, nblk, bpg, f.cols, f.cols, a->dgamma, f.cols, st);
+    colsum(part + 3 * slab, nblk, bpg, f.cols, f.cols, a->dbeta, f.cols, st);
+  }
   MTTS_LAUNCH_CHECK("layernorm_bwd_reduce");
   return MTTS_OK;
 }

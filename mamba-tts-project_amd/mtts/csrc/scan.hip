@@ -25,6 +25,8 @@
 //    waves in LDS, written as per-block slabs and reduced by a second
 //    deterministic kernel.
 #include "common.h"
+#include <algorithm>
+#include <utility>
 
 namespace mtts {
 
@@ -33,6 +35,15 @@ constexpr int kSub = 16;     // checkpoint chunk (timesteps)
 constexpr int kBlock = 256;  // threads per block
 
 // ------------------------------------------------------------- helpers
+// static_for<N>(f): f(integral_constant<int, 0..N-1>) fully unrolled at compile time
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 template <int P, int S>
 __device__ __forceinline__ float group_bcast(float v) {
   if constexpr (P == 1) {
@@ -76,6 +87,20 @@ __device__ __forceinline__ float group_allreduce(float v) {
 template <typename T, int NS>
 __device__ __forceinline__ void load_vec(const T* p, float (&o)[NS]);
 
+template <>
+__device__ __forceinline__ void load_vec<float, 1>(const float* p, float (&o)[1]) { o[0] = *p; }
+template <>
+__device__ __forceinline__ void load_vec<float, 2>(const float* p, float (&o)[2]) {
+  float2 v = *reinterpret_cast<const float2*>(p);
+  o[0] = v.x; o[1] = v.y;
+}
+template <>
+__device__ __forceinline__ void load_vec<bf16_t, 1>(const bf16_t* p, float (&o)[1]) { o[0] = bf2f(*p); }
+template <>
+__device__ __forceinline__ void load_vec<bf16_t, 2>(const bf16_t* p, float (&o)[2]) {
+  const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+  o[0] = __uint_as_float(w << 16); o[1] = __uint_as_float(w & 0xffff0000u);
+}
 template <>
 __device__ __forceinline__ void load_vec<float, 4>(const float* p, float (&o)[4]) {
   float4 v = *reinterpret_cast<const float4*>(p);
@@ -128,98 +153,219 @@ __device__ __forceinline__ void store_vec(float* p, const float (&v)[NS]) {
 }
 
 // ------------------------------------------------------------- forward
-template <int P, typename Tio, typename Tbc>
-__global__ __launch_bounds__(kBlock) void scan_fwd_kernel(const MttsScanFwdArgs a) {
-  constexpr int NS = kN / P;
-  const int j = threadIdx.x % P;
-  const int c_raw = blockIdx.x * (kBlock / P) + threadIdx.x / P;
-  const bool cvalid = c_raw < a.dim;
-  const int c = cvalid ? c_raw : a.dim - 1;
-  const int b = blockIdx.y;
-  const int L = a.seqlen;
+// L is cut into K segments of seg_len steps (K = 1 when B*D alone fills the
+// chip).  MODE kState (pass 1) scans segments 0..K-2 from h = 0 and writes
+// each segment's end state and sum(delta) to `seg`; MODE kFull (pass 2)
+// seeds segment k with  H_k = exp(A*S_{k-1}) H_{k-1} + h_{k-1}  (H_0 = h0)
+// and produces the outputs.  B/C tiles are staged once per block in LDS
+// (fp32); u/delta/z of the next tile are prefetched into registers while the
+// current tile computes.
+enum { kFull = 0, kState = 1 };
+constexpr int kTileG = 8;   // P-step groups per tile
 
-  const Tio* __restrict__ u = (const Tio*)a.u + (int64_t)b * a.u_bs + c;
-  const Tio* __restrict__ dl = (const Tio*)a.delta + (int64_t)b * a.delta_bs + c;
-  const Tio* __restrict__ zp = a.z ? (const Tio*)a.z + (int64_t)b * a.z_bs + c : nullptr;
-  Tio* __restrict__ out = (Tio*)a.out + (int64_t)b * a.out_bs + c;
-  const Tbc* __restrict__ Bp = (const Tbc*)a.Bm + (int64_t)b * a.B_bs + j * NS;
-  const Tbc* __restrict__ Cp = (const Tbc*)a.Cm + (int64_t)b * a.C_bs + j * NS;
+template <int P, typename Tio, typename Tbc, int MODE, bool SP>
+__global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdArgs a, const int seg_len,
+                                                             float* __restrict__ seg) {
+  constexpr int NS = kN / P;
+  constexpr int G = kTileG;
+  constexpr int TT = G * P;                       // timesteps per tile
+  constexpr int VPT = TT * 2 * kN / kBlock;       // staged B/C values per thread (= P)
+  __shared__ __attribute__((aligned(16))) float sBC[2][TT * 2 * kN];
+
+  const int j = threadIdx.x % P;
+  // lanes past `dim` recompute channel dim-1 bit-identically (benign duplicate stores)
+  const int c = min((int)(blockIdx.x * (kBlock / P) + threadIdx.x / P), a.dim - 1);
+  const int b = blockIdx.y;
+  const int k = blockIdx.z;
+  const int L = a.seqlen;
+  const int K = (L + seg_len - 1) / seg_len;
+  const int t_begin = k * seg_len;
+  const int t_end = min(L, t_begin + seg_len);
+
+  // Addressing: uniform (SGPR) base per timestep + one 32-bit per-lane offset,
+  // so loads/stores use the saddr form with no per-access VALU index math.
+  const Tio* __restrict__ u0 = (const Tio*)a.u + (int64_t)b * a.u_bs;
+  const Tio* __restrict__ d0 = (const Tio*)a.delta + (int64_t)b * a.delta_bs;
+  const Tio* __restrict__ z0 = a.z ? (const Tio*)a.z + (int64_t)b * a.z_bs : nullptr;
+  Tio* __restrict__ o0 = (Tio*)a.out + (int64_t)b * a.out_bs;
+  const uint32_t lu = (uint32_t)(j * a.u_ls + c), ld = (uint32_t)(j * a.delta_ls + c);
+  const uint32_t lz = (uint32_t)(j * a.z_ls + c), lo = (uint32_t)(j * a.out_ls + c);
+  const bool has_z = MODE == kFull && z0 != nullptr;
+
+  // this thread's slice of the cooperative B/C staging
+  const int e0 = threadIdx.x * VPT;
+  const int st_s = e0 / (2 * kN), st_col = e0 % (2 * kN);
+  const Tbc* __restrict__ st0 = st_col < kN ? (const Tbc*)a.Bm + (int64_t)b * a.B_bs
+                                            : (const Tbc*)a.Cm + (int64_t)b * a.C_bs;
+  const int64_t st_ls = st_col < kN ? a.B_ls : a.C_ls;
+  const uint32_t lst = (uint32_t)(st_s * st_ls + (st_col % kN));
 
   float A2[NS], h[NS];
 #pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    A2[i] = a.A[(int64_t)c * kN + j * NS + i] * kLog2e;
-    h[i] = a.h0 ? a.h0[((int64_t)b * a.dim + c) * kN + j * NS + i] : 0.f;
-  }
+  for (int i = 0; i < NS; ++i) A2[i] = a.A[(int64_t)c * kN + j * NS + i] * kLog2e;
   const float Dc = a.D ? a.D[c] : 0.f;
   const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
-  const bool has_z = zp != nullptr;
-  const int nck = a.ckpt ? (L + a.ckpt_chunk - 1) / a.ckpt_chunk : 0;
-
-  // software pipeline: the loads of group g+1 are issued before group g's math
-  float nu, nd, nz = 0.f;
-  float nB[P][NS], nC[P][NS];
-  auto issue = [&](int t0) {
-    const int ts = min(t0 + j, L - 1);
-    nu = ldf(u + (int64_t)ts * a.u_ls);
-    nd = ldf(dl + (int64_t)ts * a.delta_ls);
-    if (has_z) nz = ldf(zp + (int64_t)ts * a.z_ls);
+  float S = 0.f;
+  if constexpr (MODE == kFull) {
 #pragma unroll
-    for (int s = 0; s < P; ++s) {
-      const int tb = min(t0 + s, L - 1);
-      load_vec<Tbc, NS>(Bp + (int64_t)tb * a.B_ls, nB[s]);
-      load_vec<Tbc, NS>(Cp + (int64_t)tb * a.C_ls, nC[s]);
+    for (int i = 0; i < NS; ++i) h[i] = a.h0 ? a.h0[((int64_t)b * a.dim + c) * kN + j * NS + i] : 0.f;
+    for (int kk = 0; kk < k; ++kk) {
+      const float* sp = seg + (((int64_t)b * K + kk) * a.dim + c) * (kN + 1);
+      const float Sk = sp[kN];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) h[i] = fmaf(__builtin_amdgcn_exp2f(A2[i] * Sk), h[i], sp[j * NS + i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) h[i] = 0.f;
+  }
+  const int nck = (MODE == kFull && a.ckpt) ? (L + a.ckpt_chunk - 1) / a.ckpt_chunk : 0;
+  float* __restrict__ ck0 = nck ? a.ckpt + (int64_t)b * nck * a.dim * kN : nullptr;
+  const uint32_t lck = (uint32_t)(c * kN + j * NS);
+
+  float cu[G], cd[G], cz[G], nu[G], nd[G], nz[G], stv[VPT];
+  // TAIL: some timesteps of the tile are >= t_end -> clamp to the last valid one
+  auto load_regs = [&](auto tail, int t0, float (&uu)[G], float (&dd)[G], float (&zz)[G]) {
+    constexpr bool TAIL = decltype(tail)::value;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int tg = t0 + g * P;
+      if constexpr (TAIL) {
+        const int ts = min(tg + j, L - 1);
+        uu[g] = ldf(u0 + (int64_t)ts * a.u_ls + c);
+        dd[g] = ldf(d0 + (int64_t)ts * a.delta_ls + c);
+        zz[g] = has_z ? ldf(z0 + (int64_t)ts * a.z_ls + c) : 0.f;
+      } else {
+        uu[g] = ldf(u0 + (int64_t)tg * a.u_ls + lu);
+        dd[g] = ldf(d0 + (int64_t)tg * a.delta_ls + ld);
+        zz[g] = has_z ? ldf(z0 + (int64_t)tg * a.z_ls + lz) : 0.f;
+        static_assert(sizeof(lu) == 4, "32-bit lane offsets -> saddr loads");
+      }
     }
   };
-  if (L > 0) issue(0);
-
-  for (int t0 = 0; t0 < L; t0 += P) {
-    if (nck && (t0 % a.ckpt_chunk) == 0 && cvalid)
-      store_vec<NS>(a.ckpt + (((int64_t)b * nck + t0 / a.ckpt_chunk) * a.dim + c) * kN + j * NS, h);
-    const float uu = nu, dr = nd, zz = nz;
-    float Bv[P][NS], Cv[P][NS];
-#pragma unroll
-    for (int s = 0; s < P; ++s)
-#pragma unroll
-      for (int i = 0; i < NS; ++i) { Bv[s][i] = nB[s][i]; Cv[s][i] = nC[s][i]; }
-    if (t0 + P < L) issue(t0 + P);
-
-    const int ts = t0 + j;
-    const bool tv = ts < L;
-    float dt = dr + bias;
-    if (a.delta_softplus) dt = softplus_f(dt);
-    dt = tv ? dt : 0.f;  // padded steps are the identity map
-    const float dtu = dt * uu;
-    float yp[P];
-#pragma unroll
-    for (int s = 0; s < P; ++s) {
-      float dts, dtus;
-      if constexpr (P == 1) { dts = dt; dtus = dtu; }
-      else if constexpr (P == 2) {
-        dts = s == 0 ? group_bcast<2, 0>(dt) : group_bcast<2, 1>(dt);
-        dtus = s == 0 ? group_bcast<2, 0>(dtu) : group_bcast<2, 1>(dtu);
-      } else {
-        dts = s == 0 ? group_bcast<4, 0>(dt) : s == 1 ? group_bcast<4, 1>(dt)
-            : s == 2 ? group_bcast<4, 2>(dt) : group_bcast<4, 3>(dt);
-        dtus = s == 0 ? group_bcast<4, 0>(dtu) : s == 1 ? group_bcast<4, 1>(dtu)
-             : s == 2 ? group_bcast<4, 2>(dtu) : group_bcast<4, 3>(dtu);
-      }
-      float y = 0.f;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) {
-        const float dA = __builtin_amdgcn_exp2f(dts * A2[i]);
-        h[i] = fmaf(dA, h[i], dtus * Bv[s][i]);
-        y = fmaf(Cv[s][i], h[i], y);
-      }
-      yp[s] = y;
+  auto load_stage = [&](auto tail, int t0) {
+    constexpr bool TAIL = decltype(tail)::value;
+    if constexpr (TAIL) {
+      load_vec<Tbc, VPT>(st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN), stv);
+    } else {
+      load_vec<Tbc, VPT>(st0 + (int64_t)t0 * st_ls + lst, stv);
     }
-    float y = group_reduce_scatter<P>(yp, j);
-    y = fmaf(Dc, uu, y);
-    if (has_z) y *= silu_f(zz);
-    if (tv && cvalid) stf(out + (int64_t)ts * a.out_ls, y);
+  };
+  auto write_stage = [&](int buf) {
+    if constexpr (VPT == 4) {
+      *reinterpret_cast<float4*>(&sBC[buf][e0]) = make_float4(stv[0], stv[1], stv[2], stv[3]);
+    } else {
+#pragma unroll
+      for (int v = 0; v < VPT; ++v) sBC[buf][e0 + v] = stv[v];
+    }
+  };
+  auto compute_tile = [&](auto tail, int t0, int buf) {
+    constexpr bool TAIL = decltype(tail)::value;
+    static_for<G>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      const int tg = t0 + g * P;
+      if (nck && (tg % a.ckpt_chunk) == 0 && (!TAIL || tg < t_end))
+        store_vec<NS>(ck0 + (int64_t)(tg / a.ckpt_chunk) * a.dim * kN + lck, h);
+      const bool tv = !TAIL || (tg + j < t_end);
+      float dt = cd[g] + bias;
+      if constexpr (SP) dt = softplus_f(dt);
+      if constexpr (TAIL) dt = tv ? dt : 0.f;  // padded steps are the identity map
+      const float dtu = dt * cu[g];
+      if constexpr (MODE == kState) S += dt;
+      float yp[P];
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        float dts, dtus;
+        if constexpr (P == 2) {
+          dts = s == 0 ? group_bcast<2, 0>(dt) : group_bcast<2, 1>(dt);
+          dtus = s == 0 ? group_bcast<2, 0>(dtu) : group_bcast<2, 1>(dtu);
+        } else {
+          dts = s == 0 ? group_bcast<4, 0>(dt) : s == 1 ? group_bcast<4, 1>(dt)
+              : s == 2 ? group_bcast<4, 2>(dt) : group_bcast<4, 3>(dt);
+          dtus = s == 0 ? group_bcast<4, 0>(dtu) : s == 1 ? group_bcast<4, 1>(dtu)
+               : s == 2 ? group_bcast<4, 2>(dtu) : group_bcast<4, 3>(dtu);
+        }
+        const float* bc = &sBC[buf][(g * P + s) * 2 * kN];
+        float Bv[NS], Cv[NS];
+#pragma unroll
+        for (int q = 0; q < NS / 4; ++q) {
+          const float4 vb = *reinterpret_cast<const float4*>(bc + j * NS + 4 * q);
+          Bv[4 * q] = vb.x; Bv[4 * q + 1] = vb.y; Bv[4 * q + 2] = vb.z; Bv[4 * q + 3] = vb.w;
+          if constexpr (MODE == kFull) {
+            const float4 vc = *reinterpret_cast<const float4*>(bc + kN + j * NS + 4 * q);
+            Cv[4 * q] = vc.x; Cv[4 * q + 1] = vc.y; Cv[4 * q + 2] = vc.z; Cv[4 * q + 3] = vc.w;
+          }
+        }
+        float y = 0.f;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+          const float e = __builtin_amdgcn_exp2f(dts * A2[i]);
+          h[i] = fmaf(e, h[i], dtus * Bv[i]);
+          if constexpr (MODE == kFull) y = fmaf(Cv[i], h[i], y);
+        }
+        yp[s] = y;
+      }
+      if constexpr (MODE == kFull) {
+        float y = group_reduce_scatter<P>(yp, j);
+        y = fmaf(Dc, cu[g], y);
+        if (has_z) y *= silu_f(cz[g]);
+        if constexpr (TAIL) {
+          if (tv) stf(o0 + (int64_t)(tg + j) * a.out_ls + c, y);
+        } else {
+          stf(o0 + (int64_t)tg * a.out_ls + lo, y);
+        }
+      }
+      // materialise h here: otherwise (state-only mode) LLVM sinks every
+      // h-update to the tile end and keeps all staged B values live (spills)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) asm volatile("" : "+v"(h[i]));
+      __builtin_amdgcn_sched_barrier(0);  // keep each group's LDS reads local
+    });
+  };
+
+  using TrueT = std::integral_constant<bool, true>;
+  using FalseT = std::integral_constant<bool, false>;
+  const int nfull = (t_end - t_begin) / TT;
+  const int ntiles = (t_end - t_begin + TT - 1) / TT;
+  if (nfull > 0) {
+    load_regs(FalseT{}, t_begin, cu, cd, cz);
+    load_stage(FalseT{}, t_begin);
+  } else {
+    load_regs(TrueT{}, t_begin, cu, cd, cz);
+    load_stage(TrueT{}, t_begin);
   }
-  if (a.last_state && cvalid)
-    store_vec<NS>(a.last_state + ((int64_t)b * a.dim + c) * kN + j * NS, h);
+  write_stage(0);
+  for (int it = 0; it < ntiles; ++it) {
+    const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);  // keep time indices in SGPRs
+    const int buf = it & 1;
+    __syncthreads();
+    if (it + 1 < ntiles) {
+      if (it + 1 < nfull) {
+        load_regs(FalseT{}, t0 + TT, nu, nd, nz);
+        load_stage(FalseT{}, t0 + TT);
+      } else {
+        load_regs(TrueT{}, t0 + TT, nu, nd, nz);
+        load_stage(TrueT{}, t0 + TT);
+      }
+    }
+    if (it < nfull) compute_tile(FalseT{}, t0, buf);
+    else compute_tile(TrueT{}, t0, buf);
+    if (it + 1 < ntiles) {
+      write_stage(buf ^ 1);
+#pragma unroll
+      for (int g = 0; g < G; ++g) { cu[g] = nu[g]; cd[g] = nd[g]; cz[g] = nz[g]; }
+    }
+  }
+  if constexpr (MODE == kFull) {
+    if (k == K - 1 && a.last_state)
+      store_vec<NS>(a.last_state + ((int64_t)b * a.dim + c) * kN + j * NS, h);
+  } else {
+    S = group_allreduce<P>(S);
+    float* sp = seg + (((int64_t)b * K + k) * a.dim + c) * (kN + 1);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) sp[j * NS + i] = h[i];
+    if (j == 0) sp[kN] = S;
+  }
 }
 
 // ------------------------------------------------------------- backward
@@ -230,9 +376,7 @@ constexpr int kNSB = kN / kPB;
 constexpr int kGB = kSub / kPB;
 constexpr int kChB = kBlock / kPB;   // channels per block (64)
 constexpr int kWaves = kBlock / 64;
-#ifndef MTTS_BWD_STORE_E
-#define MTTS_BWD_STORE_E 0
-#endif
+
 
 template <int S>
 __device__ __forceinline__ float bcast4(float v) { return dpp<S * 0x55>(v); }
@@ -284,9 +428,73 @@ __device__ __forceinline__ void wave_reduce_scatter32(float (&v)[32], float& o0,
   }
 }
 
-template <typename Tio, typename Tbc>
+// Backward pass 1 (only when L is split into K > 1 segments): for segments
+// k = 1..K-1, run the adjoint recurrence  dh_t = dy_t C_t + exp(dt_{t+1} A) dh_{t+1}
+// from zero carry-in at the segment end and record the carry leaving the
+// segment start, g_k = exp(dt_{t0} A) dh_{t0}, plus S_k = sum(dt).  The carry
+// entering segment k is then G_k = sum_{j>k} exp(A (S_{k+1}+..+S_{j-1})) g_j.
+template <typename Tio, typename Tbc, bool SP>
+__global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsScanBwdArgs a, const int seg_len,
+                                                                   float* __restrict__ seg) {
+  const MttsScanFwdArgs& f = a.f;
+  const int j = threadIdx.x % kPB;
+  const int c_raw = blockIdx.x * kChB + threadIdx.x / kPB;
+  const bool cvalid = c_raw < f.dim;
+  const int c = cvalid ? c_raw : f.dim - 1;
+  const int b = blockIdx.y;
+  const int k = blockIdx.z + 1;
+  const int L = f.seqlen;
+  const int K = (L + seg_len - 1) / seg_len;
+  const int t_begin = k * seg_len;
+  const int t_end = min(L, t_begin + seg_len);
+  const Tio* __restrict__ dl = (const Tio*)f.delta + (int64_t)b * f.delta_bs + c;
+  const Tio* __restrict__ zp = f.z ? (const Tio*)f.z + (int64_t)b * f.z_bs + c : nullptr;
+  const Tio* __restrict__ dop = (const Tio*)a.dout + (int64_t)b * a.dout_bs + c;
+  const Tbc* __restrict__ Cp = (const Tbc*)f.Cm + (int64_t)b * f.C_bs + j * kNSB;
+  float A2[kNSB], carry[kNSB];
+#pragma unroll
+  for (int i = 0; i < kNSB; ++i) {
+    A2[i] = f.A[(int64_t)c * kN + j * kNSB + i] * kLog2e;
+    carry[i] = 0.f;
+  }
+  const float bias = f.delta_bias ? f.delta_bias[c] : 0.f;
+  float S = 0.f;
+  const int ng = (t_end - t_begin + kPB - 1) / kPB;
+  for (int g = ng - 1; g >= 0; --g) {
+    const int ts = t_begin + g * kPB + j;
+    const bool tv = ts < t_end;
+    const int tc = tv ? ts : L - 1;
+    float dt = ldf(dl + (int64_t)tc * f.delta_ls) + bias;
+    if constexpr (SP) dt = softplus_f(dt);
+    dt = tv ? dt : 0.f;
+    float dy = tv ? ldf(dop + (int64_t)tc * a.dout_ls) : 0.f;
+    if (zp) dy *= silu_f(ldf(zp + (int64_t)tc * f.z_ls));
+    S += dt;
+#pragma unroll
+    for (int s = kPB - 1; s >= 0; --s) {
+      const float dts = s == 0 ? bcast4<0>(dt) : s == 1 ? bcast4<1>(dt) : s == 2 ? bcast4<2>(dt) : bcast4<3>(dt);
+      const float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
+      const int tb = min(t_begin + g * kPB + s, L - 1);
+      float Cv[kNSB];
+      load_vec<Tbc, kNSB>(Cp + (int64_t)tb * f.C_ls, Cv);
+#pragma unroll
+      for (int i = 0; i < kNSB; ++i)
+        carry[i] = __builtin_amdgcn_exp2f(dts * A2[i]) * fmaf(dys, Cv[i], carry[i]);
+    }
+  }
+  S = group_allreduce<kPB>(S);
+  if (cvalid) {
+    float* sp = seg + (((int64_t)b * K + k) * f.dim + c) * (kN + 1);
+#pragma unroll
+    for (int i = 0; i < kNSB; ++i) sp[j * kNSB + i] = carry[i];
+    if (j == 0) sp[kN] = S;
+  }
+}
+
+template <typename Tio, typename Tbc, bool SP>
 __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdArgs a, float* __restrict__ slab,
-                                                             float* __restrict__ par) {
+                                                             float* __restrict__ par, const int seg_len,
+                                                             const float* __restrict__ seg) {
   const MttsScanFwdArgs& f = a.f;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -298,19 +506,33 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   const int L = f.seqlen;
   const int nck = (L + kSub - 1) / kSub;
   const int nblk = gridDim.x;
+  const int kseg = blockIdx.z;
+  const int K = gridDim.z;
+  const int ck_begin = kseg * seg_len / kSub;
+  const int ck_end = min(nck, (kseg + 1) * seg_len / kSub);
 
-  __shared__ float red[kWaves][kSub * 2 * kN];  // per-wave dB/dC partials of one chunk
+  __shared__ __attribute__((aligned(16))) float red[kWaves][kSub * 2 * kN];  // per-wave dB/dC of one chunk
+  __shared__ __attribute__((aligned(16))) float sBC[kSub * 2 * kN];          // B|C of the chunk, fp32
 
-  const Tio* __restrict__ u = (const Tio*)f.u + (int64_t)b * f.u_bs + c;
-  const Tio* __restrict__ dl = (const Tio*)f.delta + (int64_t)b * f.delta_bs + c;
-  const Tio* __restrict__ zp = f.z ? (const Tio*)f.z + (int64_t)b * f.z_bs + c : nullptr;
-  const Tio* __restrict__ dop = (const Tio*)a.dout + (int64_t)b * a.dout_bs + c;
-  Tio* __restrict__ dup = (Tio*)a.du + (int64_t)b * a.du_bs + c;
-  Tio* __restrict__ ddp = (Tio*)a.ddelta + (int64_t)b * a.ddelta_bs + c;
-  Tio* __restrict__ dzp = a.dz ? (Tio*)a.dz + (int64_t)b * a.dz_bs + c : nullptr;
-  const Tbc* __restrict__ Bp = (const Tbc*)f.Bm + (int64_t)b * f.B_bs + j * kNSB;
-  const Tbc* __restrict__ Cp = (const Tbc*)f.Cm + (int64_t)b * f.C_bs + j * kNSB;
-  const bool has_z = zp != nullptr;
+  // per-batch bases (uniform) + 32-bit per-lane offsets (lane j owns steps 4g+j)
+  const Tio* __restrict__ u0 = (const Tio*)f.u + (int64_t)b * f.u_bs;
+  const Tio* __restrict__ d0 = (const Tio*)f.delta + (int64_t)b * f.delta_bs;
+  const Tio* __restrict__ z0 = f.z ? (const Tio*)f.z + (int64_t)b * f.z_bs : nullptr;
+  const Tio* __restrict__ g0 = (const Tio*)a.dout + (int64_t)b * a.dout_bs;
+  Tio* __restrict__ du0 = (Tio*)a.du + (int64_t)b * a.du_bs;
+  Tio* __restrict__ dd0 = (Tio*)a.ddelta + (int64_t)b * a.ddelta_bs;
+  Tio* __restrict__ dz0 = a.dz ? (Tio*)a.dz + (int64_t)b * a.dz_bs : nullptr;
+  const uint32_t ou = (uint32_t)(j * f.u_ls + c), od = (uint32_t)(j * f.delta_ls + c);
+  const uint32_t oz = (uint32_t)(j * f.z_ls + c), og = (uint32_t)(j * a.dout_ls + c);
+  const uint32_t odu = (uint32_t)(j * a.du_ls + c), odd = (uint32_t)(j * a.ddelta_ls + c);
+  const uint32_t odz = (uint32_t)(j * a.dz_ls + c);
+  const bool has_z = z0 != nullptr;
+  // cooperative B/C staging: 2 values per thread per chunk
+  const int e0 = threadIdx.x * 2;
+  const int st_s = e0 / (2 * kN), st_col = e0 % (2 * kN);
+  const Tbc* __restrict__ st0 = st_col < kN ? (const Tbc*)f.Bm + (int64_t)b * f.B_bs : (const Tbc*)f.Cm + (int64_t)b * f.C_bs;
+  const int64_t st_ls = st_col < kN ? f.B_ls : f.C_ls;
+  const int st_n = st_col % kN;
 
   float An[kNSB], A2[kNSB];
 #pragma unroll
@@ -324,33 +546,51 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   float carry[kNSB], dA_acc[kNSB];
 #pragma unroll
   for (int i = 0; i < kNSB; ++i) { carry[i] = 0.f; dA_acc[i] = 0.f; }
+  for (int kk = K - 1; kk > kseg; --kk) {  // carry entering from later segments (pass 1)
+    const float* sp = seg + (((int64_t)b * K + kk) * f.dim + c) * (kN + 1);
+    const float Sk = sp[kN];
+#pragma unroll
+    for (int i = 0; i < kNSB; ++i) carry[i] = fmaf(__builtin_amdgcn_exp2f(A2[i] * Sk), carry[i], sp[j * kNSB + i]);
+  }
   float dD_acc = 0.f, dbias_acc = 0.f;
 
-  for (int k = nck - 1; k >= 0; --k) {
-    const int t_start = k * kSub;
-    float hs[kNSB];
-    load_vec<float, kNSB>(f.ckpt + (((int64_t)b * nck + k) * f.dim + c) * kN + j * kNSB, hs);
-
-    // ---- per-lane timestep data of the chunk (lane j owns steps g*4+j)
+  for (int k = ck_end - 1; k >= ck_begin; --k) {
+    const int t_start = __builtin_amdgcn_readfirstlane(k * kSub);
+    const bool full = t_start + kSub <= L;
+    // ---- stage B/C of the chunk; per-lane timestep data
+    {
+      float v[2];
+      const int t = full ? t_start + st_s : min(t_start + st_s, L - 1);
+      load_vec<Tbc, 2>(st0 + (int64_t)t * st_ls + st_n, v);
+      *reinterpret_cast<float2*>(&sBC[e0]) = make_float2(v[0], v[1]);
+    }
     float uu[kGB], xr[kGB], dt[kGB], zz[kGB], go[kGB];
 #pragma unroll
     for (int g = 0; g < kGB; ++g) {
-      const int ts = t_start + g * kPB + j;
-      const bool tv = ts < L;
-      const int tc = tv ? ts : L - 1;
-      uu[g] = ldf(u + (int64_t)tc * f.u_ls);
-      xr[g] = ldf(dl + (int64_t)tc * f.delta_ls) + bias;
-      zz[g] = has_z ? ldf(zp + (int64_t)tc * f.z_ls) : 0.f;
-      go[g] = tv ? ldf(dop + (int64_t)tc * a.dout_ls) : 0.f;
-      const float d = f.delta_softplus ? softplus_f(xr[g]) : xr[g];
-      dt[g] = tv ? d : 0.f;
+      const int tg = t_start + g * kPB;
+      if (full) {
+        uu[g] = ldf(u0 + (int64_t)tg * f.u_ls + ou);
+        xr[g] = ldf(d0 + (int64_t)tg * f.delta_ls + od) + bias;
+        zz[g] = has_z ? ldf(z0 + (int64_t)tg * f.z_ls + oz) : 0.f;
+        go[g] = ldf(g0 + (int64_t)tg * a.dout_ls + og);
+      } else {
+        const int ts = tg + j;
+        const int tc = min(ts, L - 1);
+        uu[g] = ldf(u0 + (int64_t)tc * f.u_ls + c);
+        xr[g] = ldf(d0 + (int64_t)tc * f.delta_ls + c) + bias;
+        zz[g] = has_z ? ldf(z0 + (int64_t)tc * f.z_ls + c) : 0.f;
+        go[g] = ts < L ? ldf(g0 + (int64_t)tc * a.dout_ls + c) : 0.f;
+      }
+      float d = xr[g];
+      if constexpr (SP) d = softplus_f(d);
+      dt[g] = (full || tg + j < L) ? d : 0.f;
     }
+    float hs[kNSB];
+    load_vec<float, kNSB>(f.ckpt + (((int64_t)b * nck + k) * f.dim + c) * kN + j * kNSB, hs);
+    __syncthreads();
 
-    // ---- replay the chunk forward: h_t and exp(dt*A) history in registers
+    // ---- replay the chunk forward: h history in registers
     float hh[kSub][kNSB];
-#if MTTS_BWD_STORE_E
-    float eh[kSub][kNSB];
-#endif
     {
       float h[kNSB];
 #pragma unroll
@@ -362,17 +602,12 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
         for (int s = 0; s < kPB; ++s) {
           const float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
           const float dtus = s == 0 ? bcast4<0>(dtu) : s == 1 ? bcast4<1>(dtu) : s == 2 ? bcast4<2>(dtu) : bcast4<3>(dtu);
-          const int tb = min(t_start + g * kPB + s, L - 1);
-          float Bv[kNSB];
-          load_vec<Tbc, kNSB>(Bp + (int64_t)tb * f.B_ls, Bv);
+          const float4 Bq = *reinterpret_cast<const float4*>(&sBC[(g * kPB + s) * 2 * kN + j * kNSB]);
+          const float Bv[kNSB] = {Bq.x, Bq.y, Bq.z, Bq.w};
 #pragma unroll
           for (int i = 0; i < kNSB; ++i) {
-            const float e = __builtin_amdgcn_exp2f(dts * A2[i]);
-            h[i] = fmaf(e, h[i], dtus * Bv[i]);
+            h[i] = fmaf(__builtin_amdgcn_exp2f(dts * A2[i]), h[i], dtus * Bv[i]);
             hh[g * kPB + s][i] = h[i];
-#if MTTS_BWD_STORE_E
-            eh[g * kPB + s][i] = e;
-#endif
           }
         }
       }
@@ -381,28 +616,22 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
     // ---- reverse pass
 #pragma unroll
     for (int g = kGB - 1; g >= 0; --g) {
-      float Cv[kPB][kNSB], Bv[kPB][kNSB];
       float yp[kPB];
 #pragma unroll
       for (int s = 0; s < kPB; ++s) {
-        const int tb = min(t_start + g * kPB + s, L - 1);
-        load_vec<Tbc, kNSB>(Cp + (int64_t)tb * f.C_ls, Cv[s]);
-        load_vec<Tbc, kNSB>(Bp + (int64_t)tb * f.B_ls, Bv[s]);
-        float y = 0.f;
-#pragma unroll
-        for (int i = 0; i < kNSB; ++i) y = fmaf(Cv[s][i], hh[g * kPB + s][i], y);
-        yp[s] = y;
+        const float4 Cq = *reinterpret_cast<const float4*>(&sBC[(g * kPB + s) * 2 * kN + kN + j * kNSB]);
+        yp[s] = fmaf(Cq.x, hh[g * kPB + s][0], fmaf(Cq.y, hh[g * kPB + s][1],
+                fmaf(Cq.z, hh[g * kPB + s][2], Cq.w * hh[g * kPB + s][3])));
       }
-      // lane j: gate for its own timestep
-      const float y = fmaf(Dc, uu[g], group_reduce_scatter<kPB>(yp, j));
+      const float y = fmaf(Dc, uu[g], group_reduce_scatter<kPB>(yp, j));  // pre-gate output, lane j's step
       float dy = go[g], dzv = 0.f;
       if (has_z) {
         const float sg = sigmoid_f(zz[g]);
-        const float sl = zz[g] * sg;
-        dy = go[g] * sl;
+        dy = go[g] * zz[g] * sg;
         dzv = go[g] * y * sg * (1.f + zz[g] * (1.f - sg));
       }
       dD_acc = fmaf(dy, uu[g], dD_acc);
+      const float dtu_g = dt[g] * uu[g];
 
       float ddt_p[kPB], du_p[kPB];
       float vals[32];  // [s][kind][i] = s*8 + kind*4 + i
@@ -410,83 +639,81 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       for (int s = kPB - 1; s >= 0; --s) {
         const float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
         const float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
-        const float us = s == 0 ? bcast4<0>(uu[g]) : s == 1 ? bcast4<1>(uu[g]) : s == 2 ? bcast4<2>(uu[g]) : bcast4<3>(uu[g]);
+        const float dtus = s == 0 ? bcast4<0>(dtu_g) : s == 1 ? bcast4<1>(dtu_g) : s == 2 ? bcast4<2>(dtu_g) : bcast4<3>(dtu_g);
         const int tl = g * kPB + s;
-        float ddt = 0.f, dus = 0.f;
+        const float4 Bq = *reinterpret_cast<const float4*>(&sBC[tl * 2 * kN + j * kNSB]);
+        const float4 Cq = *reinterpret_cast<const float4*>(&sBC[tl * 2 * kN + kN + j * kNSB]);
+        const float Bv[kNSB] = {Bq.x, Bq.y, Bq.z, Bq.w};
+        const float Cv[kNSB] = {Cq.x, Cq.y, Cq.z, Cq.w};
+        float ddtA = 0.f, dus = 0.f;
 #pragma unroll
         for (int i = 0; i < kNSB; ++i) {
-          const float dh = fmaf(dys, Cv[s][i], carry[i]);
+          const float dh = fmaf(dys, Cv[i], carry[i]);
           const float hp = tl > 0 ? hh[tl > 0 ? tl - 1 : 0][i] : hs[i];
-#if MTTS_BWD_STORE_E
-          const float e = eh[tl][i];
-#else
           const float e = __builtin_amdgcn_exp2f(dts * A2[i]);
-#endif
           const float t1 = dh * e * hp;
-          ddt = fmaf(An[i], t1, ddt);
-          ddt = fmaf(dh * Bv[s][i], us, ddt);
-          dus = fmaf(dh, Bv[s][i], dus);
+          ddtA = fmaf(An[i], t1, ddtA);
+          dus = fmaf(dh, Bv[i], dus);
           dA_acc[i] = fmaf(t1, dts, dA_acc[i]);
-          vals[s * 8 + i] = dh * dts * us;           // dB contribution
-          vals[s * 8 + 4 + i] = dys * hh[tl][i];     // dC contribution
+          vals[s * 8 + i] = dh * dtus;              // dB contribution
+          vals[s * 8 + 4 + i] = dys * hh[tl][i];    // dC contribution
           carry[i] = e * dh;
         }
-        ddt_p[s] = ddt;
+        ddt_p[s] = ddtA;   // + u_s * dus_s, added after the reduce (u is per step)
         du_p[s] = dus;
       }
-      // per-channel results for lane j's timestep
-      const float ddt_j = group_reduce_scatter<kPB>(ddt_p, j);
-      const float du_j = fmaf(group_reduce_scatter<kPB>(du_p, j), dt[g], Dc * dy);
-      const int ts = t_start + g * kPB + j;
-      const bool tv = ts < L;
-      const float ddr = f.delta_softplus ? ddt_j * softplus_grad(xr[g]) : ddt_j;
+      // per-channel results for lane j's timestep: ddt = sum_n A t1 + u * sum_n dh B
+      const float dus_j = group_reduce_scatter<kPB>(du_p, j);
+      const float ddt_j = fmaf(uu[g], dus_j, group_reduce_scatter<kPB>(ddt_p, j));
+      const float du_j = fmaf(dus_j, dt[g], Dc * dy);
+      const int tg = t_start + g * kPB;
+      const bool tv = full || tg + j < L;
+      float ddr = ddt_j;
+      if constexpr (SP) ddr *= softplus_grad(xr[g]);
       if (tv) dbias_acc += ddr;
-      if (tv && cvalid) {
-        stf(dup + (int64_t)ts * a.du_ls, du_j);
-        stf(ddp + (int64_t)ts * a.ddelta_ls, ddr);
-        if (has_z) stf(dzp + (int64_t)ts * a.dz_ls, dzv);
+      if (full) {
+        stf(du0 + (int64_t)tg * a.du_ls + odu, du_j);
+        stf(dd0 + (int64_t)tg * a.ddelta_ls + odd, ddr);
+        if (has_z) stf(dz0 + (int64_t)tg * a.dz_ls + odz, dzv);
+      } else if (tv) {
+        stf(du0 + (int64_t)(tg + j) * a.du_ls + c, du_j);
+        stf(dd0 + (int64_t)(tg + j) * a.ddelta_ls + c, ddr);
+        if (has_z) stf(dz0 + (int64_t)(tg + j) * a.dz_ls + c, dzv);
       }
-      // dB/dC: sum over the wave's 16 channels, then stash per wave in LDS
       if (!cvalid) {
 #pragma unroll
         for (int q = 0; q < 32; ++q) vals[q] = 0.f;
       }
       float o0, o1;
       wave_reduce_scatter32(vals, o0, o1, lane);
-      // lane holds v = (l2<<4)|(l3<<3)|(l4<<2)|(l5<<1)|e for state group j;
-      // v = s*8 + kind*4 + i.  Lanes l and l^... hold distinct v; write each.
       const int vb = (((lane >> 2) & 1) << 4) | (((lane >> 3) & 1) << 3) | (((lane >> 4) & 1) << 2) |
                      (((lane >> 5) & 1) << 1);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int v = vb | e;
         const int s = v >> 3, kind = (v >> 2) & 1, i = v & 3;
-        const int tl = g * kPB + s;
-        red[wave][(tl * 2 + kind) * kN + j * kNSB + i] = e ? o1 : o0;
+        red[wave][((g * kPB + s) * 2 + kind) * kN + j * kNSB + i] = e ? o1 : o0;
       }
     }
     __syncthreads();
     // block sum of the chunk's dB/dC -> slab[b][blk][t][2N]
     for (int q = threadIdx.x; q < kSub * 2 * kN; q += kBlock) {
-      float s = 0.f;
+      float sum = 0.f;
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) s += red[w][q];
-      const int tl = q / (2 * kN);
-      const int t = t_start + tl;
-      if (t < L) slab[(((int64_t)b * nblk + blockIdx.x) * L + t) * (2 * kN) + (q % (2 * kN))] = s;
+      for (int w = 0; w < kWaves; ++w) sum += red[w][q];
+      const int t = t_start + q / (2 * kN);
+      if (t < L) slab[(((int64_t)b * nblk + blockIdx.x) * L + t) * (2 * kN) + (q % (2 * kN))] = sum;
     }
-    __syncthreads();
   }
 
-  // per-(b, c) partials for the parameter grads
   dD_acc = group_allreduce<kPB>(dD_acc);
   dbias_acc = group_allreduce<kPB>(dbias_acc);
   if (cvalid) {
-    float* pp = par + ((int64_t)b * f.dim + c) * (kN + 2);
+    float* pp = par + (((int64_t)b * K + kseg) * f.dim + c) * (kN + 2);
 #pragma unroll
     for (int i = 0; i < kNSB; ++i) pp[j * kNSB + i] = dA_acc[i];
     if (j == 0) { pp[kN] = dD_acc; pp[kN + 1] = dbias_acc; }
-    if (a.dh0) {
+    if (a.dh0 && kseg == 0) {
 #pragma unroll
       for (int i = 0; i < kNSB; ++i) a.dh0[((int64_t)b * f.dim + c) * kN + j * kNSB + i] = carry[i];
     }
@@ -546,29 +773,71 @@ static int pick_p(int batch, int dim) {
   const char* e = getenv("MTTS_SCAN_P");
   if (e) {
     int p = atoi(e);
-    if (p == 1 || p == 2 || p == 4) return p;
+    if (p == 2 || p == 4) return p;
   }
   const int64_t ch = (int64_t)batch * dim;
   // aim for >= 4 waves per SIMD on 256 CUs (1024 SIMDs * 4 * 64 lanes)
-  if (ch >= 262144) return 1;
   if (ch >= 131072) return 2;
   return 4;
 }
 
+struct FwdPlan {
+  int P, K, seg_len;
+};
+
+static FwdPlan plan_fwd(int batch, int dim, int seqlen) {
+  FwdPlan pl;
+  pl.P = pick_p(batch, dim);
+  const int64_t lanes = (int64_t)batch * dim * pl.P;
+  int K = (int)((262144 + lanes - 1) / lanes);  // >= 4 waves per SIMD on 1024 SIMDs
+  K = std::max(1, std::min(K, seqlen / 128));
+  if (const char* e = getenv("MTTS_SCAN_SEGS")) K = std::max(1, atoi(e));
+  int seg = (seqlen + K - 1) / K;
+  seg = std::max(32, (seg + 31) / 32 * 32);
+  pl.seg_len = seg;
+  pl.K = std::max(1, (seqlen + seg - 1) / seg);
+  return pl;
+}
+
+// backward: P = 4 lanes per channel, 2 waves/SIMD resident (238 VGPRs)
+static FwdPlan plan_bwd(int batch, int dim, int seqlen) {
+  FwdPlan pl;
+  pl.P = kPB;
+  const int64_t lanes = (int64_t)batch * dim * kPB;
+  int K = (int)((131072 + lanes - 1) / lanes);
+  K = std::max(1, std::min(K, seqlen / 256));
+  if (const char* e = getenv("MTTS_SCAN_BWD_SEGS")) K = std::max(1, atoi(e));
+  int seg = (seqlen + K - 1) / K;
+  seg = std::max(kSub, (seg + kSub - 1) / kSub * kSub);
+  pl.seg_len = seg;
+  pl.K = std::max(1, (seqlen + seg - 1) / seg);
+  return pl;
+}
+
+template <int P, typename Tio, typename Tbc, bool SP>
+static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream_t st) {
+  const int nbx = (a->dim + kBlock / P - 1) / (kBlock / P);
+  float* seg = (float*)a->workspace;
+  if (pl.K > 1)
+    hipLaunchKernelGGL((scan_fwd_kernel<P, Tio, Tbc, kState, SP>), dim3(nbx, a->batch, pl.K - 1), dim3(kBlock), 0,
+                       st, *a, pl.seg_len, seg);
+  hipLaunchKernelGGL((scan_fwd_kernel<P, Tio, Tbc, kFull, SP>), dim3(nbx, a->batch, pl.K), dim3(kBlock), 0, st, *a,
+                     pl.seg_len, seg);
+}
 template <int P, typename Tio, typename Tbc>
-static void launch_fwd(const MttsScanFwdArgs* a, hipStream_t st) {
-  dim3 grid((a->dim + kBlock / P - 1) / (kBlock / P), a->batch);
-  hipLaunchKernelGGL((scan_fwd_kernel<P, Tio, Tbc>), grid, dim3(kBlock), 0, st, *a);
+static void launch_fwd(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream_t st) {
+  if (a->delta_softplus) launch_fwd_sp<P, Tio, Tbc, true>(a, pl, st);
+  else launch_fwd_sp<P, Tio, Tbc, false>(a, pl, st);
 }
 
 template <int P>
-static void launch_fwd_p(const MttsScanFwdArgs* a, hipStream_t st) {
+static void launch_fwd_p(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream_t st) {
   if (a->dtype_io == MTTS_F32) {
-    if (a->dtype_bc == MTTS_F32) launch_fwd<P, float, float>(a, st);
-    else launch_fwd<P, float, bf16_t>(a, st);
+    if (a->dtype_bc == MTTS_F32) launch_fwd<P, float, float>(a, pl, st);
+    else launch_fwd<P, float, bf16_t>(a, pl, st);
   } else {
-    if (a->dtype_bc == MTTS_F32) launch_fwd<P, bf16_t, float>(a, st);
-    else launch_fwd<P, bf16_t, bf16_t>(a, st);
+    if (a->dtype_bc == MTTS_F32) launch_fwd<P, bf16_t, float>(a, pl, st);
+    else launch_fwd<P, bf16_t, bf16_t>(a, pl, st);
   }
 }
 
@@ -576,26 +845,53 @@ static void launch_fwd_p(const MttsScanFwdArgs* a, hipStream_t st) {
 
 using namespace mtts;
 
+extern "C" int64_t mtts_selective_scan_fwd_workspace(int batch, int dim, int seqlen, int dstate) {
+  (void)dstate;
+  const FwdPlan pl = plan_fwd(batch, dim, seqlen);
+  return pl.K > 1 ? (int64_t)batch * pl.K * dim * (kN + 1) * 4 + 256 : 0;
+}
+
 extern "C" int mtts_selective_scan_fwd(const MttsScanFwdArgs* a, void* stream) {
   int rc = check_fwd(a);
   if (rc) return rc;
   if (a->seqlen == 0) return MTTS_OK;
   hipStream_t st = (hipStream_t)stream;
-  switch (pick_p(a->batch, a->dim)) {
-    case 1: launch_fwd_p<1>(a, st); break;
-    case 2: launch_fwd_p<2>(a, st); break;
-    default: launch_fwd_p<4>(a, st); break;
-  }
+  const FwdPlan pl = plan_fwd(a->batch, a->dim, a->seqlen);
+  if (pl.K > 1) MTTS_CHECK(a->workspace, "scan: workspace required (mtts_selective_scan_fwd_workspace)");
+  if (pl.P == 2) launch_fwd_p<2>(a, pl, st);
+  else launch_fwd_p<4>(a, pl, st);
   MTTS_LAUNCH_CHECK("selective_scan_fwd");
   return MTTS_OK;
 }
 
 extern "C" int64_t mtts_selective_scan_bwd_workspace(int batch, int dim, int seqlen, int dstate) {
   (void)dstate;
+  const FwdPlan pl = plan_bwd(batch, dim, seqlen);
   const int64_t nblk = (dim + kChB - 1) / kChB;
   const int64_t slab = (int64_t)batch * nblk * seqlen * 2 * kN;
-  const int64_t par = (int64_t)batch * dim * (kN + 2);
-  return (slab + par) * 4 + 256;
+  const int64_t par = (int64_t)batch * pl.K * dim * (kN + 2);
+  const int64_t segw = pl.K > 1 ? (int64_t)batch * pl.K * dim * (kN + 1) : 0;
+  return (slab + par + segw) * 4 + 256;
+}
+
+template <typename Tio, typename Tbc>
+static void launch_bwd(const MttsScanBwdArgs* a, const FwdPlan& pl, float* slab, float* par, float* segw,
+                       hipStream_t st) {
+  const int nblk = (a->f.dim + kChB - 1) / kChB;
+  if (pl.K > 1) {
+    if (a->f.delta_softplus)
+      hipLaunchKernelGGL((scan_bwd_carry_kernel<Tio, Tbc, true>), dim3(nblk, a->f.batch, pl.K - 1), dim3(kBlock), 0,
+                         st, *a, pl.seg_len, segw);
+    else
+      hipLaunchKernelGGL((scan_bwd_carry_kernel<Tio, Tbc, false>), dim3(nblk, a->f.batch, pl.K - 1), dim3(kBlock), 0,
+                         st, *a, pl.seg_len, segw);
+  }
+  if (a->f.delta_softplus)
+    hipLaunchKernelGGL((scan_bwd_kernel<Tio, Tbc, true>), dim3(nblk, a->f.batch, pl.K), dim3(kBlock), 0, st, *a, slab,
+                       par, pl.seg_len, (const float*)segw);
+  else
+    hipLaunchKernelGGL((scan_bwd_kernel<Tio, Tbc, false>), dim3(nblk, a->f.batch, pl.K), dim3(kBlock), 0, st, *a,
+                       slab, par, pl.seg_len, (const float*)segw);
 }
 
 extern "C" int mtts_selective_scan_bwd(const MttsScanBwdArgs* a, void* stream) {
@@ -608,16 +904,17 @@ extern "C" int mtts_selective_scan_bwd(const MttsScanBwdArgs* a, void* stream) {
   const int L = a->f.seqlen;
   if (L == 0) return MTTS_OK;
   hipStream_t st = (hipStream_t)stream;
+  const FwdPlan pl = plan_bwd(a->f.batch, a->f.dim, L);
   const int nblk = (a->f.dim + kChB - 1) / kChB;
   float* slab = (float*)a->workspace;
   float* par = slab + (int64_t)a->f.batch * nblk * L * 2 * kN;
-  dim3 grid(nblk, a->f.batch);
+  float* segw = par + (int64_t)a->f.batch * pl.K * a->f.dim * (kN + 2);
   if (a->f.dtype_io == MTTS_F32) {
-    if (a->f.dtype_bc == MTTS_F32) hipLaunchKernelGGL((scan_bwd_kernel<float, float>), grid, dim3(kBlock), 0, st, *a, slab, par);
-    else hipLaunchKernelGGL((scan_bwd_kernel<float, bf16_t>), grid, dim3(kBlock), 0, st, *a, slab, par);
+    if (a->f.dtype_bc == MTTS_F32) launch_bwd<float, float>(a, pl, slab, par, segw, st);
+    else launch_bwd<float, bf16_t>(a, pl, slab, par, segw, st);
   } else {
-    if (a->f.dtype_bc == MTTS_F32) hipLaunchKernelGGL((scan_bwd_kernel<bf16_t, float>), grid, dim3(kBlock), 0, st, *a, slab, par);
-    else hipLaunchKernelGGL((scan_bwd_kernel<bf16_t, bf16_t>), grid, dim3(kBlock), 0, st, *a, slab, par);
+    if (a->f.dtype_bc == MTTS_F32) launch_bwd<bf16_t, float>(a, pl, slab, par, segw, st);
+    else launch_bwd<bf16_t, bf16_t>(a, pl, slab, par, segw, st);
   }
   MTTS_LAUNCH_CHECK("selective_scan_bwd");
   const int64_t tot = (int64_t)a->f.batch * L * 2 * kN;
@@ -625,7 +922,7 @@ extern "C" int mtts_selective_scan_bwd(const MttsScanBwdArgs* a, void* stream) {
                      a->dB_bs, a->dB_ls, a->dC, a->dC_bs, a->dC_ls);
   MTTS_LAUNCH_CHECK("selective_scan_bwd_reduce_bc");
   hipLaunchKernelGGL(scan_bwd_reduce_par, dim3((a->f.dim * (kN + 2) + 255) / 256), dim3(256), 0, st, par,
-                     a->f.batch, a->f.dim, a->dA, a->dD, a->ddelta_bias);
+                     a->f.batch * pl.K, a->f.dim, a->dA, a->dD, a->ddelta_bias);
   MTTS_LAUNCH_CHECK("selective_scan_bwd_reduce_par");
   return MTTS_OK;
 }

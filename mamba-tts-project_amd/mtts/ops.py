@@ -86,6 +86,9 @@ def scan_fwd(u, delta, A, Bm, Cm, D=None, z=None, delta_bias=None, softplus=True
     ckpt = (torch.empty(Bsz, (Ln + SCAN_CKPT - 1) // SCAN_CKPT, Dm, N, device=u.device, dtype=torch.float32)
             if want_ckpt else None)
     a = _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, ckpt)
+    wsz = L.lib().mtts_selective_scan_fwd_workspace(Bsz, Dm, Ln, N)
+    ws = torch.empty(wsz, device=u.device, dtype=torch.uint8) if wsz > 0 else None
+    a.workspace = L.ptr(ws)
     L.call("mtts_selective_scan_fwd", a)
     return out, last, ckpt
 

@@ -34,15 +34,23 @@ def g32(a):
     return torch.from_numpy(np.asarray(a)).to(DEV, torch.float32)
 
 
-@pytest.fixture(params=["1", "2", "4"])
+@pytest.fixture(params=["2", "4", "4:s3"])
 def scan_p(request):
-    old = os.environ.get("MTTS_SCAN_P")
-    os.environ["MTTS_SCAN_P"] = request.param
-    yield int(request.param)
-    if old is None:
-        del os.environ["MTTS_SCAN_P"]
-    else:
-        os.environ["MTTS_SCAN_P"] = old
+    """P (lanes per channel) and, with ':sK', a forced split of L into K
+    segments for both the forward and the backward (two-pass path)."""
+    keys = ("MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_BWD_SEGS")
+    old = {k: os.environ.get(k) for k in keys}
+    p, _, segs = request.param.partition(":s")
+    os.environ["MTTS_SCAN_P"] = p
+    if segs:
+        os.environ["MTTS_SCAN_SEGS"] = segs
+        os.environ["MTTS_SCAN_BWD_SEGS"] = segs
+    yield request.param
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 @pytest.mark.parametrize("name", ["scan_full.npz", "scan_plain.npz", "scan_short.npz"])
