@@ -554,39 +554,50 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   }
   float dD_acc = 0.f, dbias_acc = 0.f;
 
-  for (int k = ck_end - 1; k >= ck_begin; --k) {
+  // next-chunk prefetch registers (issued one chunk ahead)
+  float n_u[kGB], n_x[kGB], n_z[kGB], n_g[kGB], n_st[2], n_hs[kNSB];
+  auto prefetch = [&](int k) {
     const int t_start = __builtin_amdgcn_readfirstlane(k * kSub);
     const bool full = t_start + kSub <= L;
-    // ---- stage B/C of the chunk; per-lane timestep data
-    {
-      float v[2];
-      const int t = full ? t_start + st_s : min(t_start + st_s, L - 1);
-      load_vec<Tbc, 2>(st0 + (int64_t)t * st_ls + st_n, v);
-      *reinterpret_cast<float2*>(&sBC[e0]) = make_float2(v[0], v[1]);
-    }
-    float uu[kGB], xr[kGB], dt[kGB], zz[kGB], go[kGB];
+    const int t = full ? t_start + st_s : min(t_start + st_s, L - 1);
+    load_vec<Tbc, 2>(st0 + (int64_t)t * st_ls + st_n, n_st);
 #pragma unroll
     for (int g = 0; g < kGB; ++g) {
       const int tg = t_start + g * kPB;
       if (full) {
-        uu[g] = ldf(u0 + (int64_t)tg * f.u_ls + ou);
-        xr[g] = ldf(d0 + (int64_t)tg * f.delta_ls + od) + bias;
-        zz[g] = has_z ? ldf(z0 + (int64_t)tg * f.z_ls + oz) : 0.f;
-        go[g] = ldf(g0 + (int64_t)tg * a.dout_ls + og);
+        n_u[g] = ldf(u0 + (int64_t)tg * f.u_ls + ou);
+        n_x[g] = ldf(d0 + (int64_t)tg * f.delta_ls + od);
+        n_z[g] = has_z ? ldf(z0 + (int64_t)tg * f.z_ls + oz) : 0.f;
+        n_g[g] = ldf(g0 + (int64_t)tg * a.dout_ls + og);
       } else {
         const int ts = tg + j;
         const int tc = min(ts, L - 1);
-        uu[g] = ldf(u0 + (int64_t)tc * f.u_ls + c);
-        xr[g] = ldf(d0 + (int64_t)tc * f.delta_ls + c) + bias;
-        zz[g] = has_z ? ldf(z0 + (int64_t)tc * f.z_ls + c) : 0.f;
-        go[g] = ts < L ? ldf(g0 + (int64_t)tc * a.dout_ls + c) : 0.f;
+        n_u[g] = ldf(u0 + (int64_t)tc * f.u_ls + c);
+        n_x[g] = ldf(d0 + (int64_t)tc * f.delta_ls + c);
+        n_z[g] = has_z ? ldf(z0 + (int64_t)tc * f.z_ls + c) : 0.f;
+        n_g[g] = ts < L ? ldf(g0 + (int64_t)tc * a.dout_ls + c) : 0.f;
       }
+    }
+    load_vec<float, kNSB>(f.ckpt + (((int64_t)b * nck + k) * f.dim + c) * kN + j * kNSB, n_hs);
+  };
+  if (ck_end > ck_begin) prefetch(ck_end - 1);
+
+  for (int k = ck_end - 1; k >= ck_begin; --k) {
+    const int t_start = __builtin_amdgcn_readfirstlane(k * kSub);
+    const bool full = t_start + kSub <= L;
+    *reinterpret_cast<float2*>(&sBC[e0]) = make_float2(n_st[0], n_st[1]);
+    float uu[kGB], xr[kGB], dt[kGB], zz[kGB], go[kGB], hs[kNSB];
+#pragma unroll
+    for (int g = 0; g < kGB; ++g) { uu[g] = n_u[g]; xr[g] = n_x[g] + bias; zz[g] = n_z[g]; go[g] = n_g[g]; }
+#pragma unroll
+    for (int i = 0; i < kNSB; ++i) hs[i] = n_hs[i];
+    if (k - 1 >= ck_begin) prefetch(k - 1);
+#pragma unroll
+    for (int g = 0; g < kGB; ++g) {
       float d = xr[g];
       if constexpr (SP) d = softplus_f(d);
-      dt[g] = (full || tg + j < L) ? d : 0.f;
+      dt[g] = (full || t_start + g * kPB + j < L) ? d : 0.f;
     }
-    float hs[kNSB];
-    load_vec<float, kNSB>(f.ckpt + (((int64_t)b * nck + k) * f.dim + c) * kN + j * kNSB, hs);
     __syncthreads();
 
     // ---- replay the chunk forward: h history in registers
@@ -634,9 +645,9 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       const float dtu_g = dt[g] * uu[g];
 
       float ddt_p[kPB], du_p[kPB];
-      float vals[32];  // [s][kind][i] = s*8 + kind*4 + i
 #pragma unroll
       for (int s = kPB - 1; s >= 0; --s) {
+        float vals[8];  // [kind][i]: dB_i, dC_i of this step
         const float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
         const float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
         const float dtus = s == 0 ? bcast4<0>(dtu_g) : s == 1 ? bcast4<1>(dtu_g) : s == 2 ? bcast4<2>(dtu_g) : bcast4<3>(dtu_g);
@@ -655,12 +666,23 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
           ddtA = fmaf(An[i], t1, ddtA);
           dus = fmaf(dh, Bv[i], dus);
           dA_acc[i] = fmaf(t1, dts, dA_acc[i]);
-          vals[s * 8 + i] = dh * dtus;              // dB contribution
-          vals[s * 8 + 4 + i] = dys * hh[tl][i];    // dC contribution
+          vals[i] = cvalid ? dh * dtus : 0.f;            // dB contribution
+          vals[4 + i] = cvalid ? dys * hh[tl][i] : 0.f;  // dC contribution
           carry[i] = e * dh;
         }
         ddt_p[s] = ddtA;   // + u_s * dus_s, added after the reduce (u is per step)
         du_p[s] = dus;
+        // sum the 8 values over the wave's 16 channels (lane bits 2..5):
+        // lane keeps kind = bit2, i = (bit3 << 1) | bit4
+        const bool q2 = lane & 4, q3 = lane & 8, q4 = lane & 16;
+        float a4[4], a2[2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a4[q] = (q2 ? vals[4 + q] : vals[q]) + xor4(q2 ? vals[q] : vals[4 + q], lane);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) a2[q] = (q3 ? a4[2 + q] : a4[q]) + xor8(q3 ? a4[q] : a4[2 + q]);
+        float a1 = (q4 ? a2[1] : a2[0]) + xor16(q4 ? a2[0] : a2[1], lane);
+        a1 = sum_xor32(a1);
+        if (lane < 32) red[wave][(tl * 2 + (q2 ? 1 : 0)) * kN + j * kNSB + ((q3 ? 2 : 0) | (q4 ? 1 : 0))] = a1;
       }
       // per-channel results for lane j's timestep: ddt = sum_n A t1 + u * sum_n dh B
       const float dus_j = group_reduce_scatter<kPB>(du_p, j);
@@ -679,20 +701,6 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
         stf(du0 + (int64_t)(tg + j) * a.du_ls + c, du_j);
         stf(dd0 + (int64_t)(tg + j) * a.ddelta_ls + c, ddr);
         if (has_z) stf(dz0 + (int64_t)(tg + j) * a.dz_ls + c, dzv);
-      }
-      if (!cvalid) {
-#pragma unroll
-        for (int q = 0; q < 32; ++q) vals[q] = 0.f;
-      }
-      float o0, o1;
-      wave_reduce_scatter32(vals, o0, o1, lane);
-      const int vb = (((lane >> 2) & 1) << 4) | (((lane >> 3) & 1) << 3) | (((lane >> 4) & 1) << 2) |
-                     (((lane >> 5) & 1) << 1);
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int v = vb | e;
-        const int s = v >> 3, kind = (v >> 2) & 1, i = v & 3;
-        red[wave][((g * kPB + s) * 2 + kind) * kN + j * kNSB + i] = e ? o1 : o0;
       }
     }
     __syncthreads();
