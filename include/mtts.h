@@ -237,6 +237,17 @@ typedef struct {
 int64_t mtts_layernorm_bwd_workspace(int rows, int cols, int rows_per_group);
 int mtts_layernorm_bwd(const MttsLNBwdArgs* a, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Column sums over row-major rows: out[g*out_gstride + c] = sum over rows r
+ * of group g (rows_per_group consecutive rows) of in[r*row_stride + c], fp32
+ * accumulation, deterministic order.  Used for bias gradients (sum of dy over
+ * tokens; torch Linear/MHA bias grads at mamba_decoder.py:32-48) and FiLM
+ * gradients.  dtype: MTTS_F32 / MTTS_BF16 input.
+ * ------------------------------------------------------------------------ */
+int64_t mtts_colsum_workspace(int rows, int cols, int rows_per_group);
+int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_t row_stride, int rows_per_group, float* out,
+                int64_t out_gstride, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,6 +27,7 @@ import torch.nn.functional as F
 from mtts.mamba import Mamba
 from mtts.attention import CrossAttention
 from mtts import ops
+from mtts.linear import cast_scope, linear
 
 
 class MambaTTSDecoderLayer(nn.Module):
@@ -51,10 +52,20 @@ class MambaTTSDecoderLayer(nn.Module):
         )
 
     def forward(self, x, text_hidden, z_style, text_mask=None, mamba_state=None):
-        cd = x.dtype
-        B, T, _ = x.shape
-        # 1) Mamba (mamba_decoder.py:59-64)
-        h, _ = ops.layer_norm(x, self.norm_mamba.weight, self.norm_mamba.bias, self.norm_mamba.eps)
+        with cast_scope():
+            x, ff_out, new_state = self.forward_fused(x, None, text_hidden, z_style, text_mask, mamba_state)
+        return x + ff_out, new_state                                          # :88-89
+
+    def forward_fused(self, x, pending, text_hidden, z_style, text_mask=None, mamba_state=None):
+        """Same math as forward(); the input residual `x + pending` and the
+        output residual `x + ff_out` are left to the neighbouring fused
+        residual+LayerNorm kernels.  Returns (x, ff_out, new_state)."""
+        T = x.shape[1]
+        # 1) (x += pending) ; h = norm_mamba(x) ; Mamba   (mamba_decoder.py:59-64)
+        h, xs = ops.layer_norm(x if pending is None else pending, self.norm_mamba.weight, self.norm_mamba.bias,
+                               self.norm_mamba.eps, res=None if pending is None else x)
+        if pending is not None:
+            x = xs
         h_mamba, new_state = self.mamba(h, mamba_state)
 
         # 2) x = x + h_mamba ; h = norm_cross(x)   (fused, :64-67)
@@ -67,14 +78,13 @@ class MambaTTSDecoderLayer(nn.Module):
 
         # 3) x = x + attn ; h = gamma * norm_ff(x) + beta   (fused, :78-86)
         gb = self.style_mlp(z_style.to(self.style_mlp[0].weight.dtype))
-        gamma, beta = torch.chunk(gb.to(cd), 2, dim=-1)
+        gamma, beta = torch.chunk(gb.to(h.dtype), 2, dim=-1)
         h, x = ops.layer_norm(attn_out, self.norm_ff.weight, self.norm_ff.bias, self.norm_ff.eps, res=x,
                               gamma=gamma, beta=beta, rows_per_group=T)
         f0, f2 = self.ff[0], self.ff[2]
-        ff_h = F.gelu(F.linear(h, f0.weight.to(cd), f0.bias.to(cd)))
-        ff_out = F.linear(ff_h, f2.weight.to(cd), f2.bias.to(cd))
-        x = x + ff_out                                                       # :88-89
-        return x, new_state
+        ff_h = F.gelu(linear(h, f0.weight, f0.bias))
+        ff_out = linear(ff_h, f2.weight, f2.bias)
+        return x, ff_out, new_state
 
 
 class MambaTTSDecoder(nn.Module):
@@ -127,10 +137,29 @@ class MambaTTSDecoder(nn.Module):
                 text_mask = torch.cat([ref_mask, text_mask], dim=1)
         return text_hidden, text_mask
 
-    def _tail(self, x):
-        x, _ = ops.layer_norm(x, self.norm_out.weight, self.norm_out.bias, self.norm_out.eps)
-        cd = x.dtype
-        return F.linear(x, self.head.weight.to(cd), self.head.bias.to(cd))
+    def _tail(self, x, pending=None):
+        """norm_out(x [+ pending]) -> head (mamba_decoder.py:184-185)."""
+        h, _ = ops.layer_norm(x if pending is None else pending, self.norm_out.weight, self.norm_out.bias,
+                              self.norm_out.eps, res=None if pending is None else x)
+        return linear(h, self.head.weight, self.head.bias)
+
+    def _gemm_weights(self):
+        ws = [self.head.weight, self.head.bias]
+        for l in self.layers:
+            m = l.mamba
+            ws += [m.in_proj.weight, m.x_proj.weight, m.dt_proj.weight, m.out_proj.weight,
+                   l.cross_attn.in_proj_weight, l.cross_attn.in_proj_bias, l.cross_attn.out_proj.weight,
+                   l.cross_attn.out_proj.bias, l.ff[0].weight, l.ff[0].bias, l.ff[2].weight, l.ff[2].bias]
+        return [w for w in ws if w is not None]
+
+    def _run_layers(self, x, text_hidden, z_style, text_mask, states):
+        pending = None
+        new_states = []
+        for i, layer in enumerate(self.layers):
+            x, pending, st = layer.forward_fused(x, pending, text_hidden, z_style, text_mask,
+                                                 None if states is None else states[i])
+            new_states.append(st)
+        return x, pending, new_states
 
     # -- API --------------------------------------------------------------
     def forward(self, audio_tokens, text_hidden, z_style, text_mask=None, ref_hidden=None, ref_mask=None):
@@ -167,9 +196,9 @@ class MambaTTSDecoder(nn.Module):
         pos = self.pos_embed(pos_ids)[None, :, :].expand(B, T, -1)
         x = (tok + pos + qemb).to(cd)
 
-        for layer in self.layers:
-            x, _ = layer(x=x, text_hidden=text_hidden, z_style=z_style, text_mask=text_mask, mamba_state=None)
-        return self._tail(x)
+        with cast_scope(self._gemm_weights(), cd):
+            x, pending, _ = self._run_layers(x, text_hidden, z_style, text_mask, None)
+            return self._tail(x, pending)
 
     def decode_step(
         self,
@@ -209,14 +238,6 @@ class MambaTTSDecoder(nn.Module):
         text_hidden = text_hidden.to(cd)
         text_hidden, text_mask = self._concat_ref(text_hidden, text_mask, ref_hidden, ref_mask, B_local, device)
 
-        new_states = [None] * len(self.layers)
-        for i, layer in enumerate(self.layers):
-            x, new_state = layer(
-                x=x,
-                text_hidden=text_hidden,
-                z_style=z_style,
-                text_mask=text_mask,
-                mamba_state=mamba_states[i] if mamba_states is not None else None,
-            )
-            new_states[i] = new_state
-        return self._tail(x), new_states
+        with cast_scope(self._gemm_weights(), cd):
+            x, pending, new_states = self._run_layers(x, text_hidden, z_style, text_mask, mamba_states)
+            return self._tail(x, pending), new_states

@@ -96,6 +96,8 @@ _SIGS = {
     "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
     "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),
     "mtts_layernorm_bwd": ([C.POINTER(LNBwdArgs), vp], i32),
+    "mtts_colsum_workspace": ([i32, i32, i32], i64),
+    "mtts_colsum": ([vp, i32, i32, i32, i64, i32, vp, i64, vp, vp], i32),
 }
 
 _lib = None
@@ -129,6 +131,14 @@ def call(name, args):
     L = lib()
     stream = torch.cuda.current_stream().cuda_stream
     rc = getattr(L, name)(C.byref(args), C.c_void_p(stream))
+    if rc != 0:
+        raise RuntimeError(f"{name} failed ({rc}): {L.mtts_last_error().decode()}")
+
+
+def call_raw(name, *args):
+    """Invoke a non-struct entry point; the current stream is appended."""
+    L = lib()
+    rc = getattr(L, name)(*args, C.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc != 0:
         raise RuntimeError(f"{name} failed ({rc}): {L.mtts_last_error().decode()}")
 

@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import attn_kernels
+from .linear import cast_scope, linear
 
 
 class CrossAttention(nn.Module):
@@ -39,18 +40,21 @@ class CrossAttention(nn.Module):
         nn.init.constant_(self.out_proj.bias, 0.0)
 
     def forward(self, query, key, value, key_padding_mask=None, need_weights=False):
+        with cast_scope():
+            return self._forward(query, key, value, key_padding_mask)
+
+    def _forward(self, query, key, value, key_padding_mask):
         cd = query.dtype
-        d, H, hd = self.embed_dim, self.num_heads, self.head_dim
-        W = self.in_proj_weight.to(cd)
-        bq = self.in_proj_bias.to(cd)
-        q = F.linear(query, W[:d], bq[:d])
+        d, H = self.embed_dim, self.num_heads
+        W, b = self.in_proj_weight, self.in_proj_bias
+        q = linear(query, W, b, rows=(0, d))
         if key is value:
-            kv = F.linear(key.to(cd), W[d:], bq[d:])
+            kv = linear(key.to(cd), W, b, rows=(d, 3 * d))
             k, v = kv[..., :d], kv[..., d:]
         else:
-            k = F.linear(key.to(cd), W[d:2 * d], bq[d:2 * d])
-            v = F.linear(value.to(cd), W[2 * d:], bq[2 * d:])
+            k = linear(key.to(cd), W, b, rows=(d, 2 * d))
+            v = linear(value.to(cd), W, b, rows=(2 * d, 3 * d))
         p_drop = self.dropout if self.training else 0.0
         o = attn_kernels.attention(q, k, v, H, key_padding_mask, p_drop)
-        out = F.linear(o, self.out_proj.weight.to(cd), self.out_proj.bias.to(cd))
+        out = linear(o, self.out_proj.weight, self.out_proj.bias)
         return out, None

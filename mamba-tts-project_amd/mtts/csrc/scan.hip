@@ -436,6 +436,9 @@ __device__ __forceinline__ void wave_reduce_scatter32(float (&v)[32], float& o0,
 template <typename Tio, typename Tbc, bool SP>
 __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsScanBwdArgs a, const int seg_len,
                                                                    float* __restrict__ seg) {
+  constexpr int G = kTileG;          // groups per tile
+  constexpr int TT = G * kPB;        // 32 timesteps per tile
+  __shared__ __attribute__((aligned(16))) float sC[2][TT * kN];
   const MttsScanFwdArgs& f = a.f;
   const int j = threadIdx.x % kPB;
   const int c_raw = blockIdx.x * kChB + threadIdx.x / kPB;
@@ -447,10 +450,14 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   const int K = (L + seg_len - 1) / seg_len;
   const int t_begin = k * seg_len;
   const int t_end = min(L, t_begin + seg_len);
-  const Tio* __restrict__ dl = (const Tio*)f.delta + (int64_t)b * f.delta_bs + c;
-  const Tio* __restrict__ zp = f.z ? (const Tio*)f.z + (int64_t)b * f.z_bs + c : nullptr;
-  const Tio* __restrict__ dop = (const Tio*)a.dout + (int64_t)b * a.dout_bs + c;
-  const Tbc* __restrict__ Cp = (const Tbc*)f.Cm + (int64_t)b * f.C_bs + j * kNSB;
+  const Tio* __restrict__ d0 = (const Tio*)f.delta + (int64_t)b * f.delta_bs;
+  const Tio* __restrict__ z0 = f.z ? (const Tio*)f.z + (int64_t)b * f.z_bs : nullptr;
+  const Tio* __restrict__ g0 = (const Tio*)a.dout + (int64_t)b * a.dout_bs;
+  const uint32_t od = (uint32_t)(j * f.delta_ls + c), oz = (uint32_t)(j * f.z_ls + c);
+  const uint32_t og = (uint32_t)(j * a.dout_ls + c);
+  const Tbc* __restrict__ C0 = (const Tbc*)f.Cm + (int64_t)b * f.C_bs;
+  const int e0 = threadIdx.x * 2;          // staged C values of this thread: step e0/16, state e0%16
+  const int st_s = e0 / kN, st_n = e0 % kN;
   float A2[kNSB], carry[kNSB];
 #pragma unroll
   for (int i = 0; i < kNSB; ++i) {
@@ -459,27 +466,61 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   }
   const float bias = f.delta_bias ? f.delta_bias[c] : 0.f;
   float S = 0.f;
-  const int ng = (t_end - t_begin + kPB - 1) / kPB;
-  for (int g = ng - 1; g >= 0; --g) {
-    const int ts = t_begin + g * kPB + j;
-    const bool tv = ts < t_end;
-    const int tc = tv ? ts : L - 1;
-    float dt = ldf(dl + (int64_t)tc * f.delta_ls) + bias;
-    if constexpr (SP) dt = softplus_f(dt);
-    dt = tv ? dt : 0.f;
-    float dy = tv ? ldf(dop + (int64_t)tc * a.dout_ls) : 0.f;
-    if (zp) dy *= silu_f(ldf(zp + (int64_t)tc * f.z_ls));
-    S += dt;
+  float cx[G], cg[G], cz[G], nx[G], ng[G], nz[G], st[2];
+  auto load = [&](int t0, float (&xx)[G], float (&gg)[G], float (&zz)[G]) {
+    const bool full = t0 + TT <= t_end;
 #pragma unroll
-    for (int s = kPB - 1; s >= 0; --s) {
-      const float dts = s == 0 ? bcast4<0>(dt) : s == 1 ? bcast4<1>(dt) : s == 2 ? bcast4<2>(dt) : bcast4<3>(dt);
-      const float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
-      const int tb = min(t_begin + g * kPB + s, L - 1);
-      float Cv[kNSB];
-      load_vec<Tbc, kNSB>(Cp + (int64_t)tb * f.C_ls, Cv);
+    for (int g = 0; g < G; ++g) {
+      const int tg = t0 + g * kPB;
+      if (full) {
+        xx[g] = ldf(d0 + (int64_t)tg * f.delta_ls + od);
+        gg[g] = ldf(g0 + (int64_t)tg * a.dout_ls + og);
+        zz[g] = z0 ? ldf(z0 + (int64_t)tg * f.z_ls + oz) : 0.f;
+      } else {
+        const int ts = tg + j;
+        const int tc = min(ts, L - 1);
+        xx[g] = ldf(d0 + (int64_t)tc * f.delta_ls + c);
+        gg[g] = ts < t_end ? ldf(g0 + (int64_t)tc * a.dout_ls + c) : 0.f;
+        zz[g] = z0 ? ldf(z0 + (int64_t)tc * f.z_ls + c) : 0.f;
+      }
+    }
+    load_vec<Tbc, 2>(C0 + (int64_t)min(t0 + st_s, L - 1) * f.C_ls + st_n, st);
+  };
+  const int ntiles = (t_end - t_begin + TT - 1) / TT;
+  load(t_begin + (ntiles - 1) * TT, cx, cg, cz);
+  *reinterpret_cast<float2*>(&sC[0][e0]) = make_float2(st[0], st[1]);
+  for (int q = 0; q < ntiles; ++q) {
+    const int it = ntiles - 1 - q;
+    const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
+    const int buf = q & 1;
+    __syncthreads();
+    if (it > 0) load(t0 - TT, nx, ng, nz);
+    static_for<G>([&](auto gc) {
+      constexpr int g = G - 1 - decltype(gc)::value;
+      const bool tv = t0 + g * kPB + j < t_end;
+      float dt = cx[g] + bias;
+      if constexpr (SP) dt = softplus_f(dt);
+      dt = tv ? dt : 0.f;
+      float dy = cg[g];
+      if (z0) dy *= silu_f(cz[g]);
+      S += dt;
 #pragma unroll
-      for (int i = 0; i < kNSB; ++i)
-        carry[i] = __builtin_amdgcn_exp2f(dts * A2[i]) * fmaf(dys, Cv[i], carry[i]);
+      for (int s = kPB - 1; s >= 0; --s) {
+        const float dts = s == 0 ? bcast4<0>(dt) : s == 1 ? bcast4<1>(dt) : s == 2 ? bcast4<2>(dt) : bcast4<3>(dt);
+        const float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
+        const float4 Cq = *reinterpret_cast<const float4*>(&sC[buf][(g * kPB + s) * kN + j * kNSB]);
+        const float Cv[kNSB] = {Cq.x, Cq.y, Cq.z, Cq.w};
+#pragma unroll
+        for (int i = 0; i < kNSB; ++i) carry[i] = __builtin_amdgcn_exp2f(dts * A2[i]) * fmaf(dys, Cv[i], carry[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < kNSB; ++i) asm volatile("" : "+v"(carry[i]));
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (it > 0) {
+      *reinterpret_cast<float2*>(&sC[buf ^ 1][e0]) = make_float2(st[0], st[1]);
+#pragma unroll
+      for (int g = 0; g < G; ++g) { cx[g] = nx[g]; cg[g] = ng[g]; cz[g] = nz[g]; }
     }
   }
   S = group_allreduce<kPB>(S);
@@ -812,8 +853,8 @@ static FwdPlan plan_bwd(int batch, int dim, int seqlen) {
   FwdPlan pl;
   pl.P = kPB;
   const int64_t lanes = (int64_t)batch * dim * kPB;
-  int K = (int)((131072 + lanes - 1) / lanes);
-  K = std::max(1, std::min(K, seqlen / 256));
+  int K = (int)((262144 + lanes - 1) / lanes);
+  K = std::max(1, std::min(K, seqlen / 128));
   if (const char* e = getenv("MTTS_SCAN_BWD_SEGS")) K = std::max(1, atoi(e));
   int seg = (seqlen + K - 1) / K;
   seg = std::max(kSub, (seg + kSub - 1) / kSub * kSub);

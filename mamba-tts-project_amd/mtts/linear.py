@@ -1,0 +1,152 @@
+"""Linear layers of the decoder hot path (projections, FFN, head).
+
+Forward/dgrad GEMMs go to hipBLASLt through torch (plain library GEMMs: they
+already run at 1.0-1.3 PF/s bf16 on MI355X for these shapes, see
+tools/bench_gemm.py).  Two things are done differently from nn.Linear:
+
+* weight gradients (small output, K = B*T tokens) are computed split-K with
+  fp32 partial products (4 K-chunks, summed in fp32): the stock `dy^T @ x`
+  runs at 47-650 TF/s on these shapes, the split form at 140-900 TF/s, and
+  the result is already the fp32 master-param gradient (no cast kernels);
+* bias gradients are a HIP column sum (mtts_colsum) with fp32 accumulation.
+
+Weights are fp32 masters.  Their compute-dtype copies are refreshed once per
+top-level forward (`cast_scope`): the decoder casts every GEMM weight with
+one multi-tensor copy into persistent buffers, nested module calls reuse
+them, and the backward uses the copies saved by the forward.  (Version
+counters are not used: fused optimizers update parameters without bumping
+them.)
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from . import _lib as L
+
+_scope = {"token": 0, "depth": 0}
+
+
+@contextlib.contextmanager
+def cast_scope(params=None, dtype=None):
+    """Open a weight-cast scope; the outermost scope invalidates all cached
+    casts and (optionally) pre-casts `params` to `dtype` in one foreach copy."""
+    if _scope["depth"] == 0:
+        _scope["token"] += 1
+        if params is not None and dtype is not None:
+            src = [p for p in params if p.dtype != dtype and p.is_cuda]
+            dst = []
+            for p in src:
+                ent = getattr(p, "_mtts_cast", None)
+                buf = ent[1] if (ent is not None and ent[1].dtype == dtype and ent[1].shape == p.shape) else \
+                    torch.empty(p.shape, device=p.device, dtype=dtype)
+                dst.append(buf)
+            if src:
+                with torch.no_grad():
+                    torch._foreach_copy_(dst, [p.detach() for p in src])
+                for p, b in zip(src, dst):
+                    p._mtts_cast = (_scope["token"], b)
+    _scope["depth"] += 1
+    try:
+        yield
+    finally:
+        _scope["depth"] -= 1
+
+
+def cast_weight(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Compute-dtype copy of a parameter, valid for the current cast scope."""
+    if w.dtype == dtype:
+        return w.detach()
+    ent = getattr(w, "_mtts_cast", None)
+    if ent is not None and ent[0] == _scope["token"] and ent[1].dtype == dtype and ent[1].device == w.device:
+        return ent[1]
+    if ent is not None and ent[1].dtype == dtype and ent[1].shape == w.shape:
+        t = ent[1]
+        with torch.no_grad():
+            t.copy_(w.detach())
+    else:
+        t = w.detach().to(dtype)
+    w._mtts_cast = (_scope["token"], t)
+    return t
+
+
+def colsum(x2d: torch.Tensor) -> torch.Tensor:
+    """fp32 column sums of a (rows, cols) tensor with unit column stride."""
+    if x2d.stride(-1) != 1:
+        x2d = x2d.contiguous()
+    rows, cols = x2d.shape
+    out = torch.empty(cols, device=x2d.device, dtype=torch.float32)
+    rpg = max(rows, 1)
+    wsz = L.lib().mtts_colsum_workspace(rows, cols, rpg)
+    ws = torch.empty(wsz, device=x2d.device, dtype=torch.uint8) if wsz > 0 else None
+    L.call_raw("mtts_colsum", x2d.data_ptr(), L.dtype_code(x2d), rows, cols, x2d.stride(0), rpg,
+               out.data_ptr(), 0, L.ptr(ws))
+    return out
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4) -> torch.Tensor:
+    """dW = dy^T @ x in fp32; dy (M, n), x (M, k) with the same dtype."""
+    M = dy.shape[0]
+    if dy.dtype == torch.float32:
+        return dy.t() @ x
+    if splits > 1 and M % splits == 0 and M >= 2048:
+        m = M // splits
+        part = torch.bmm(dy.reshape(splits, m, -1).transpose(1, 2), x.reshape(splits, m, -1),
+                         out_dtype=torch.float32)
+        return part.sum(0)
+    return torch.mm(dy.t(), x, out_dtype=torch.float32)
+
+
+class LinearFn(torch.autograd.Function):
+    """y = x @ weight[r0:r1]^T + bias[r0:r1] in dtype of x.  Gradients for the
+    full weight/bias (zero outside [r0, r1) when a row slice is used)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, r0, r1):
+        cd = x.dtype
+        w = cast_weight(weight, cd)
+        if r0 is not None:
+            w = w[r0:r1]
+        x2 = x.reshape(-1, x.shape[-1])
+        if bias is not None:
+            b = cast_weight(bias, cd)
+            if r0 is not None:
+                b = b[r0:r1]
+            y = torch.addmm(b, x2, w.t())
+        else:
+            y = x2 @ w.t()
+        ctx.save_for_backward(x2, w)
+        ctx.meta = (x.shape, weight.shape, weight.dtype, None if bias is None else bias.dtype, r0, r1)
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        xshape, wshape, wdt, bdt, r0, r1 = ctx.meta
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.dtype != w.dtype:
+            dy2 = dy2.to(w.dtype)
+        dx = (dy2 @ w).view(xshape) if ctx.needs_input_grad[0] else None
+        dW = db = None
+        if ctx.needs_input_grad[1]:
+            g = wgrad(dy2, x2).to(wdt)
+            if r0 is not None:
+                full = torch.zeros(wshape, device=g.device, dtype=wdt)
+                full[r0:r1] = g
+                g = full
+            dW = g
+        if bdt is not None and ctx.needs_input_grad[2]:
+            gb = colsum(dy2).to(bdt)
+            if r0 is not None:
+                full = torch.zeros(wshape[0], device=gb.device, dtype=bdt)
+                full[r0:r1] = gb
+                gb = full
+            db = gb
+        return dx, dW, db, None, None
+
+
+def linear(x, weight, bias=None, rows=None):
+    """Functional form; `rows=(r0, r1)` selects a row slice of weight/bias."""
+    r0, r1 = (None, None) if rows is None else rows
+    return LinearFn.apply(x, weight, bias, r0, r1)

@@ -30,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from .linear import cast_scope, cast_weight, linear, wgrad
 
 
 class MambaInnerFn(torch.autograd.Function):
@@ -37,14 +38,16 @@ class MambaInnerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, conv_state_in, h0):
+        cd = xz.dtype
         di = xz.shape[-1] // 2
         N = A_log.shape[1]
         r = W_dt.shape[1]
+        Wx, Wdt = cast_weight(W_x, cd), cast_weight(W_dt, cd)
         x, z = xz[..., :di], xz[..., di:]
         u, conv_state = ops.conv_fwd(x, conv_w, conv_b, True, state_in=conv_state_in, want_state=True)
-        x_dbl = F.linear(u, W_x)
+        x_dbl = u @ Wx.t()
         dt, Bm, Cm = x_dbl[..., :r], x_dbl[..., r:r + N], x_dbl[..., r + N:]
-        delta = F.linear(dt, W_dt)
+        delta = dt @ Wdt.t()
         A = -torch.exp(A_log.float())
         need = any(ctx.needs_input_grad)
         y, last, ckpt = ops.scan_fwd(u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, want_last=True, want_ckpt=need)
@@ -56,6 +59,8 @@ class MambaInnerFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dconv, _dlast):
         xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt = ctx.saved_tensors
+        cd = u.dtype
+        Wx, Wdt = cast_weight(W_x, cd), cast_weight(W_dt, cd)
         di = xz.shape[-1] // 2
         N = A_log.shape[1]
         r = W_dt.shape[1]
@@ -68,14 +73,14 @@ class MambaInnerFn(torch.autograd.Function):
         du, ddelta, _, _, _, dA, dD, dbias, _ = ops.scan_bwd(
             u, delta, A, Bm, Cm, D, z, dt_bias, True, None, ckpt, dy,
             dz=dxz[..., di:], dB=dx_dbl[..., r:r + N], dC=dx_dbl[..., r + N:])
-        cd = u.dtype
         # dt_proj: delta = dt @ W_dt^T
-        dx_dbl[..., :r] = (ddelta @ W_dt).float()
-        dW_dt = ddelta.reshape(-1, di).t() @ dt.reshape(-1, r)
+        dd2 = ddelta.reshape(-1, di)
+        dx_dbl[..., :r] = (ddelta @ Wdt).float()
+        dW_dt = wgrad(dd2, dt.reshape(-1, r))
         # x_proj: x_dbl = u @ W_x^T
         gx = dx_dbl.to(cd)
-        du = du + gx @ W_x
-        dW_x = gx.reshape(-1, r + 2 * N).t() @ u.reshape(-1, di)
+        du = du + gx @ Wx
+        dW_x = wgrad(gx.reshape(-1, r + 2 * N), u.reshape(-1, di))
         _, dw, db = ops.conv_bwd(x, conv_w, conv_b, du, True, dx=dxz[..., :di])
         dA_log = (dA * A).to(A_log.dtype)
         return (dxz, dw.reshape(conv_w.shape).to(conv_w.dtype), db.to(conv_b.dtype), dW_x.to(W_x.dtype),
@@ -117,25 +122,27 @@ class Mamba(nn.Module):
         self.out_proj = nn.Linear(di, d_model, bias=bias, **fk)
 
     def _w(self, lin, cd):
-        return lin.weight.to(cd)
+        return cast_weight(lin.weight, cd)
 
     def forward(self, x, state=None):
         """x (B, L, d) -> (out (B, L, d), (conv_state, ssm_state))."""
         if not x.is_cuda:
             raise RuntimeError("mtts.Mamba runs on the HIP kernels only (no CPU path)")
-        cd = x.dtype
+        with cast_scope():
+            return self._forward(x, state)
+
+    def _forward(self, x, state):
         Bsz, Ln, _ = x.shape
         if state is not None and Ln == 1:
             return self.step(x, state)
-        xz = F.linear(x, self._w(self.in_proj, cd), None if self.in_proj.bias is None else self.in_proj.bias.to(cd))
+        xz = linear(x, self.in_proj.weight, self.in_proj.bias)
         conv_state_in = h0 = None
         if state is not None:
             conv_state_in, h0 = state
         y, conv_state, ssm_state = MambaInnerFn.apply(
-            xz, self.conv1d.weight, self.conv1d.bias, self._w(self.x_proj, cd), self._w(self.dt_proj, cd),
+            xz, self.conv1d.weight, self.conv1d.bias, self.x_proj.weight, self.dt_proj.weight,
             self.A_log, self.D, self.dt_proj.bias, conv_state_in, h0)
-        out = F.linear(y, self._w(self.out_proj, cd),
-                       None if self.out_proj.bias is None else self.out_proj.bias.to(cd))
+        out = linear(y, self.out_proj.weight, self.out_proj.bias)
         return out, (conv_state, ssm_state)
 
     @torch.no_grad()

@@ -259,3 +259,35 @@ def test_upstream_signature_ops(golden):
     (out * torch.from_numpy(g["dout"]).to(DEV)).sum().backward()
     for k, t in ins.items():
         close(t.grad, g["d" + k], name="d" + k)
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 5), (300, 64), (16384, 1024), (4097, 96), (20000, 2050)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_colsum(rows, cols, dtype):
+    from mtts.linear import colsum
+    torch.manual_seed(rows)
+    x = torch.randn(rows, cols, device=DEV).to(dtype)
+    close(colsum(x), x.double().sum(0), rtol=1e-5, name="colsum")
+    if rows > 1:
+        close(colsum(x[:, 1:]), x[:, 1:].double().sum(0), rtol=1e-5, name="colsum strided")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_linear_fn_grads(dtype):
+    from mtts.linear import linear
+    torch.manual_seed(0)
+    x = torch.randn(4, 1024, 96, device=DEV).to(dtype).requires_grad_(True)
+    w = torch.randn(160, 96, device=DEV, requires_grad=True)
+    b = torch.randn(160, device=DEV, requires_grad=True)
+    y = linear(x, w, b, rows=(32, 128))
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xr, wr, br = x.detach().double().requires_grad_(True), w.detach().double().requires_grad_(True), \
+        b.detach().double().requires_grad_(True)
+    yr = xr @ wr[32:128].t() + br[32:128]
+    (yr * g.double()).sum().backward()
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    close(y.float(), yr, rtol=tol, name="y")
+    close(x.grad.float(), xr.grad, rtol=tol, name="dx")
+    close(w.grad, wr.grad, rtol=tol, name="dw")
+    close(b.grad, br.grad, rtol=tol, name="db")
