@@ -73,9 +73,10 @@ def train_bench(args, rank, world, dev):
                                           n_heads=c["n_heads"], d_ff=c["d_ff"], d_style=c["d_style"]).to(dev)
     model.compute_dtype = torch.bfloat16
     params = list(model.parameters())
+    dp = None
     if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], bucket_cap_mb=100,
-                                                          gradient_as_bucket_view=True)
+        from mtts.dp import GradAllReduce
+        dp = GradAllReduce(params, bucket_mb=128)   # bucketed RCCL all-reduce overlapped with backward
     opt = torch.optim.Adam(params, lr=1e-4, fused=True)
     tokens, text, z, mask = make_batch(c, dev, seed=1234 + rank)
 
@@ -83,8 +84,13 @@ def train_bench(args, rank, world, dev):
         logits = model(tokens, text, z, text_mask=mask)
         loss = torch.nn.functional.cross_entropy(logits.float().view(-1, c["vocab"]), tokens.view(-1),
                                                  ignore_index=0)
-        opt.zero_grad(set_to_none=False)
+        if dp is not None:
+            dp.zero_grad()
+        else:
+            opt.zero_grad(set_to_none=False)
         loss.backward()
+        if dp is not None:
+            dp.finish()
         torch.nn.utils.clip_grad_norm_(params, 1.0)
         opt.step()
         return loss
@@ -168,7 +174,7 @@ def decode_bench(steps, B=32):
             lat.append((time.perf_counter() - t0) * 1e3)
     lat = sorted(lat[min(100, steps // 4):])
     return {"B": B, "steps": steps, "p50_ms": lat[len(lat) // 2], "p90_ms": lat[int(len(lat) * 0.9)],
-            "mode": "eager"}
+            "mode": m.decode_mode, "layers": c["n_layers"], "d_model": c["d_model"], "T_text": c["T_text"]}
 
 
 def cpu_baseline(budget_s=20.0):

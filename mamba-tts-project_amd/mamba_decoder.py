@@ -28,6 +28,7 @@ from mtts.mamba import Mamba
 from mtts.attention import CrossAttention
 from mtts import ops
 from mtts.linear import cast_scope, linear
+from mtts.decode import DecodeEngine
 
 
 class MambaTTSDecoderLayer(nn.Module):
@@ -113,6 +114,15 @@ class MambaTTSDecoder(nn.Module):
         self.norm_out = nn.LayerNorm(d_model)
         self.head = nn.Linear(d_model, vocab_size_audio)
         self.compute_dtype = None  # e.g. torch.bfloat16
+        # decode_step under torch.no_grad on HIP tensors runs the incremental
+        # engine (mtts/decode.py): "graph" (hipGraph replay), "eager", or None
+        # for the generic per-module path.
+        self.decode_mode = "graph"
+        self._engine = None
+
+    def reset_decode_cache(self):
+        """Drop cached conditioning K/V, FiLM and graphs (call after editing weights)."""
+        self._engine = None
 
     # -- helpers ----------------------------------------------------------
     def _cd(self):
@@ -229,6 +239,12 @@ class MambaTTSDecoder(nn.Module):
         B_local = last_token.shape[0]
         device = last_token.device
         cd = self._cd()
+        if self.decode_mode and not torch.is_grad_enabled() and last_token.is_cuda:
+            use_graph = self.decode_mode == "graph"
+            if self._engine is None or self._engine.use_graph != use_graph:
+                self._engine = DecodeEngine(self, use_graph=use_graph)
+            return self._engine.step(last_token, text_hidden, z_style, mamba_states, step_index, text_mask,
+                                     ref_hidden, ref_mask)
 
         tok = self.token_embed(last_token)
         pos_id = torch.tensor([step_index], device=device)

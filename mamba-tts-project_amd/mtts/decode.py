@@ -1,0 +1,172 @@
+"""Incremental decoding engine for MambaTTSDecoder.decode_step (C4).
+
+Reference: mamba_decoder.py:188-256.  Each AR step embeds one token (no
+quant_embed, pos = step_index), runs every layer with its Mamba state and
+cross-attends to [ref ‖ text].  The reference recomputes, every step, the
+K/V projections of the (constant) conditioning sequence and the FiLM
+gamma/beta of the (constant) style vector; the engine computes them once per
+conditioning context and keeps them in HBM with the per-layer SSM/conv state.
+
+Engine path (inference only: torch.no_grad, HIP tensors):
+  * context cache keyed on the identity/version/shape of text_hidden,
+    text_mask, ref_hidden, ref_mask, z_style and the compute dtype;
+  * per step: token+pos embedding, then per layer LN -> Mamba.step (HIP
+    conv-window + state-update kernels, states updated in place) -> fused
+    residual+LN -> q-projection + attention over cached K/V -> fused
+    residual+LN+FiLM -> FFN; the FFN residual is fused into the next LN;
+  * optional hipGraph capture of the whole step (static token / position /
+    state buffers): replay costs one launch instead of ~25 per layer.
+Numerics are those of the eager module path (tests/test_gpu_modules.py).
+Call `reset()` after modifying weights in place between decode steps.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from .attn_kernels import attention
+from .linear import cast_weight
+
+
+def _key(t):
+    if t is None:
+        return None
+    return (t.data_ptr(), t._version, tuple(t.shape), t.dtype)
+
+
+class DecodeEngine:
+    def __init__(self, model, use_graph=True):
+        self.m = model
+        self.use_graph = use_graph
+        self.reset()
+
+    def reset(self):
+        self.ctx_key = None
+        self.ctx = None
+        self.graph = None
+        self.states = None
+
+    # -- conditioning context -------------------------------------------------
+    def _build_ctx(self, text_hidden, z_style, text_mask, ref_hidden, ref_mask, cd):
+        m = self.m
+        B = text_hidden.shape[0]
+        th = text_hidden.to(cd)
+        th, tm = m._concat_ref(th, text_mask, ref_hidden, ref_mask, B, th.device)
+        kpm = None if tm is None else ~tm                                   # mamba_decoder.py:68-70
+        d = m.token_embed.weight.shape[1]
+        layers = []
+        for l in m.layers:
+            ca = l.cross_attn
+            W = cast_weight(ca.in_proj_weight, cd)
+            b = cast_weight(ca.in_proj_bias, cd)
+            kv = torch.addmm(b[d:], th.reshape(-1, d), W[d:].t()).view(B, -1, 2 * d)
+            gb = torch.tanh(F.linear(z_style.to(l.style_mlp[0].weight.dtype), l.style_mlp[0].weight,
+                                     l.style_mlp[0].bias)).to(cd)
+            gamma, beta = gb[:, :d].contiguous(), gb[:, d:].contiguous()
+            mm = l.mamba
+            di = mm.d_inner
+            layers.append(dict(
+                k=kv[..., :d], v=kv[..., d:], gamma=gamma, beta=beta,
+                Wq=W[:d], bq=b[:d], Wo=cast_weight(ca.out_proj.weight, cd), bo=cast_weight(ca.out_proj.bias, cd),
+                W1=cast_weight(l.ff[0].weight, cd), b1=cast_weight(l.ff[0].bias, cd),
+                W2=cast_weight(l.ff[2].weight, cd), b2=cast_weight(l.ff[2].bias, cd),
+                Win=cast_weight(mm.in_proj.weight, cd), Wx=cast_weight(mm.x_proj.weight, cd),
+                Wdt=cast_weight(mm.dt_proj.weight, cd), Wout=cast_weight(mm.out_proj.weight, cd),
+                conv_w=mm.conv1d.weight.detach().reshape(di, -1).float().contiguous(),
+                conv_b=mm.conv1d.bias.detach().float().contiguous(),
+                A=(-torch.exp(mm.A_log.detach().float())).contiguous(), D=mm.D.detach().float().contiguous(),
+                dt_bias=mm.dt_proj.bias.detach().float().contiguous(),
+            ))
+        return dict(B=B, kpm=kpm, layers=layers, cd=cd,
+                    Wh=cast_weight(m.head.weight, cd), bh=cast_weight(m.head.bias, cd))
+
+    # -- one step, eager -----------------------------------------------------
+    def _step(self, tok, pos, states):
+        m, c = self.m, self.ctx
+        cd = c["cd"]
+        x = (F.embedding(tok, m.token_embed.weight) + F.embedding(pos, m.pos_embed.weight)[None]).to(cd)
+        x = x.view(c["B"], -1)                                               # (B, d)
+        pending = None
+        for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
+            conv_state, ssm_state = states[i]
+            h, xs = ops.layer_norm(x if pending is None else pending, l.norm_mamba.weight, l.norm_mamba.bias,
+                                   l.norm_mamba.eps, res=None if pending is None else x)
+            if pending is not None:
+                x = xs
+            mm = l.mamba
+            di, N, r = mm.d_inner, mm.d_state, mm.dt_rank
+            xz = h @ p["Win"].t()
+            u = ops.conv_update(xz[:, :di], conv_state, p["conv_w"], p["conv_b"], True)
+            x_dbl = u @ p["Wx"].t()
+            delta = x_dbl[:, :r] @ p["Wdt"].t()
+            y = ops.state_update(ssm_state, u, delta, p["A"], x_dbl[:, r:r + N].contiguous(),
+                                 x_dbl[:, r + N:].contiguous(), p["D"], xz[:, di:], p["dt_bias"], True)
+            h_m = y @ p["Wout"].t()
+            h, x = ops.layer_norm(h_m, l.norm_cross.weight, l.norm_cross.bias, l.norm_cross.eps, res=x)
+            q = torch.addmm(p["bq"], h, p["Wq"].t())
+            o = attention(q[:, None], p["k"], p["v"], l.cross_attn.num_heads, c["kpm"])[:, 0]
+            a = torch.addmm(p["bo"], o, p["Wo"].t())
+            h, x = ops.layer_norm(a, l.norm_ff.weight, l.norm_ff.bias, l.norm_ff.eps, res=x,
+                                  gamma=p["gamma"], beta=p["beta"], rows_per_group=1)
+            pending = torch.addmm(p["b2"], F.gelu(torch.addmm(p["b1"], h, p["W1"].t())), p["W2"].t())
+        h, _ = ops.layer_norm(pending, m.norm_out.weight, m.norm_out.bias, m.norm_out.eps, res=x)
+        return torch.addmm(c["bh"], h, c["Wh"].t())[:, None]
+
+    # -- public ----------------------------------------------------------------
+    @torch.no_grad()
+    def step(self, last_token, text_hidden, z_style, mamba_states, step_index, text_mask=None, ref_hidden=None,
+             ref_mask=None):
+        m = self.m
+        cd = m._cd()
+        key = (_key(text_hidden), _key(z_style), _key(text_mask), _key(ref_hidden), _key(ref_mask), cd,
+               tuple(last_token.shape))
+        if key != self.ctx_key:
+            self.ctx = self._build_ctx(text_hidden, z_style, text_mask, ref_hidden, ref_mask, cd)
+            self.ctx_key = key
+            self.graph = None
+            self.states = None
+        B = last_token.shape[0]
+        dev = last_token.device
+        if self.states is None:
+            self.states = []
+            for l in m.layers:
+                mm = l.mamba
+                self.states.append((torch.zeros(B, mm.d_inner, mm.d_conv, device=dev),
+                                    torch.zeros(B, mm.d_inner, mm.d_state, device=dev)))
+            self.tok_buf = torch.zeros(B, 1, dtype=torch.long, device=dev)
+            self.pos_buf = torch.zeros(1, dtype=torch.long, device=dev)
+        # adopt the caller's states (None = start of sequence)
+        for i, st in enumerate(self.states):
+            given = None if mamba_states is None else mamba_states[i]
+            if given is None:
+                st[0].zero_()
+                st[1].zero_()
+            elif given[0] is not st[0] or given[1] is not st[1]:
+                st[0].copy_(given[0])
+                st[1].copy_(given[1])
+        self.tok_buf.copy_(last_token)
+        self.pos_buf.fill_(int(step_index))
+        if not self.use_graph:
+            logits = self._step(self.tok_buf, self.pos_buf, self.states)
+            return logits, list(self.states)
+        if self.graph is None:
+            saved = [(a.clone(), b.clone()) for a, b in self.states]
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):  # warm up (allocator, library handles)
+                    self._step(self.tok_buf, self.pos_buf, self.states)
+            torch.cuda.current_stream().wait_stream(s)
+            for (a, b), (sa, sb) in zip(self.states, saved):
+                a.copy_(sa)
+                b.copy_(sb)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.out_buf = self._step(self.tok_buf, self.pos_buf, self.states)
+            for (a, b), (sa, sb) in zip(self.states, saved):  # capture ran the step once
+                a.copy_(sa)
+                b.copy_(sb)
+            self.graph = g
+        self.graph.replay()
+        return self.out_buf.clone(), list(self.states)

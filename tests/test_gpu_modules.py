@@ -140,3 +140,32 @@ def test_reference_module_runs_on_mamba_ssm_shim(golden, tmp_path):
     assert mamba_ssm.Mamba.__module__ == "mtts.mamba"
     mod = importlib.import_module("mamba_decoder")
     assert mod.Mamba is mamba_ssm.Mamba
+
+
+@pytest.mark.parametrize("mode", ["graph", "eager"])
+def test_decode_engine_matches_module_path(golden, mode):
+    """The incremental engine (cached K/V + FiLM, in-place states, hipGraph
+    replay) equals the generic per-module decode path step by step, and its
+    states equal the reference goldens."""
+    m, g = _decoder(golden)
+    m.eval()
+    tokens = torch.from_numpy(g["tokens"]).to(DEV)
+    kw = dict(text_mask=torch.from_numpy(g["text_mask"]).to(DEV), ref_hidden=torch.from_numpy(g["ref"]).to(DEV),
+              ref_mask=torch.from_numpy(g["ref_mask"]).to(DEV))
+    text = torch.from_numpy(g["text"]).to(DEV)
+    z = torch.from_numpy(g["z_style"]).to(DEV)
+    outs = {}
+    for dm in (None, mode):
+        m.decode_mode = dm
+        m.reset_decode_cache()
+        states = [None, None]
+        seq = []
+        with torch.no_grad():
+            for t in range(g["decode/logits"].shape[1]):
+                lg, states = m.decode_step(tokens[:, t:t + 1], text, z, states, t, **kw)
+                seq.append(lg.clone())
+        outs[dm] = (torch.cat(seq, 1), [(a.clone(), b.clone()) for a, b in states])
+    close(outs[mode][0], outs[None][0], rtol=1e-5, name="engine logits")
+    close(outs[mode][0], g["decode/logits"], name="engine vs reference")
+    for i in range(2):
+        close(outs[mode][1][i][1], g[f"decode/ssm_state{i}"], name="ssm state")
