@@ -152,6 +152,19 @@ def scan_roofline(dtype, B=32, L=8192, D=2048, iters=10):
     return ms, nbytes, nbytes / (ms * 1e-3)
 
 
+def pmc_traffic(dtype_key):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
+    PMC passes (profiles/r01_scan_pmc_summary.json, made by scripts_pmc.sh):
+    2 x FETCH_SIZE (gfx950 counts half of wide coalesced streaming reads,
+    MI355X_MICROARCH.md HBM section) + WRITE_SIZE, both KB x 1024."""
+    path = os.path.join(ROOT, "profiles", "r01_scan_pmc_summary.json")
+    try:
+        with open(path) as f:
+            return json.load(f)[dtype_key]["traffic_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def decode_bench(steps, B=32):
     import mamba_decoder
     c = dict(C2)
@@ -247,11 +260,12 @@ def main():
         log(f"[bench] scan bf16 north-star {sms:.3f} ms {sbw / 1e9:.0f} GB/s")
         rec["roofline"] = {"kernel": "selective_scan_fwd (north-star B=32 L=8192 d_inner=2048 N=16, bf16 I/O)",
                            "bound": "hbm", "achieved": sbw / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                           "frac": sbw / HBM_PEAK, "traffic": None, "ms": sms, "algorithmic_bytes": sb}
+                           "frac": sbw / HBM_PEAK, "traffic": pmc_traffic("bf16"), "ms": sms, "algorithmic_bytes": sb,
+                           "traffic_source": "profiles/r01_scan_pmc_summary.json (2*FETCH_SIZE+WRITE_SIZE)"}
         fms, fb, fbw = scan_roofline(torch.float32)
         log(f"[bench] scan fp32 north-star {fms:.3f} ms {fbw / 1e9:.0f} GB/s")
         rec["scan_fp32"] = {"bound": "hbm", "achieved": fbw / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                            "frac": fbw / HBM_PEAK, "ms": fms, "algorithmic_bytes": fb}
+                            "frac": fbw / HBM_PEAK, "ms": fms, "algorithmic_bytes": fb, "traffic": pmc_traffic("fp32")}
         if args.decode_steps > 0:
             rec["decode"] = decode_bench(args.decode_steps)
             log(f"[bench] decode {rec['decode']}")
