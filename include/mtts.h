@@ -248,6 +248,51 @@ int64_t mtts_colsum_workspace(int rows, int cols, int rows_per_group);
 int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_t row_stride, int rows_per_group, float* out,
                 int64_t out_gstride, void* workspace, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Multi-head cross-attention core (no projections):
+ *   out[b, t, h*hd:(h+1)*hd] = softmax_s(scale * q_h[t] . k_h[s] + mask) v_h
+ * Replaces the attention inside nn.MultiheadAttention(batch_first=True) as
+ * called at mamba_decoder.py:72-77 (decoder -> [ref ‖ text]) and
+ * style_cross_attention.py:125-131,270-276 (torch's
+ * F.multi_head_attention_forward / scaled_dot_product_attention).
+ * q (B, Tq, H*hd), k/v (B, Tk, H*hd) channel-last with unit channel stride;
+ * key_padding_mask (B, Tk) bytes, nonzero = ignore the key (torch's
+ * key_padding_mask=True), NULL = none.  A query whose keys are ALL masked
+ * yields NaN, as torch MHA does.  lse (B, H, Tq) fp32 receives
+ * ln sum_s exp(scale * q.k_s) (-inf for fully masked rows); the backward
+ * needs it.  hd in {16, 32, 64, 128}; bf16 uses bf16 MFMA, f32 uses f32 MFMA.
+ * Strides and q/k/v/out base pointers must be 16-byte aligned.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int batch, heads, head_dim, q_len, kv_len;
+  int dtype;                 /* MTTS_F32 / MTTS_BF16 for q, k, v, out */
+  float scale;               /* usually 1/sqrt(head_dim) */
+  int64_t q_bs, q_ls, k_bs, k_ls, v_bs, v_ls, o_bs, o_ls;  /* element strides */
+  int64_t mask_bs;           /* key_padding_mask batch stride (bytes) */
+  const void* q;
+  const void* k;
+  const void* v;
+  const uint8_t* key_padding_mask;
+  void* out;
+  float* lse;                /* may be NULL (inference) */
+} MttsAttnFwdArgs;
+
+int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream);
+
+/* Backward: dout -> dq, dk, dv (same dtype as q).  f.out / f.lse must hold
+ * the forward's results.  Deterministic (no atomics). */
+typedef struct {
+  MttsAttnFwdArgs f;
+  const void* dout; int64_t do_bs, do_ls;
+  void* dq;         int64_t dq_bs, dq_ls;
+  void* dk;         int64_t dk_bs, dk_ls;
+  void* dv;         int64_t dv_bs, dv_ls;
+  void* workspace;           /* mtts_attention_bwd_workspace() bytes */
+} MttsAttnBwdArgs;
+
+int64_t mtts_attention_bwd_workspace(int batch, int heads, int head_dim, int q_len, int kv_len, int dtype);
+int mtts_attention_bwd(const MttsAttnBwdArgs* a, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -81,6 +81,20 @@ class LNBwdArgs(C.Structure):
                 ("workspace", vp)]
 
 
+class AttnFwdArgs(C.Structure):
+    _fields_ = [("batch", i32), ("heads", i32), ("head_dim", i32), ("q_len", i32), ("kv_len", i32),
+                ("dtype", i32), ("scale", f32),
+                ("q_bs", i64), ("q_ls", i64), ("k_bs", i64), ("k_ls", i64), ("v_bs", i64), ("v_ls", i64),
+                ("o_bs", i64), ("o_ls", i64), ("mask_bs", i64),
+                ("q", vp), ("k", vp), ("v", vp), ("key_padding_mask", vp), ("out", vp), ("lse", vp)]
+
+
+class AttnBwdArgs(C.Structure):
+    _fields_ = [("f", AttnFwdArgs), ("dout", vp), ("do_bs", i64), ("do_ls", i64),
+                ("dq", vp), ("dq_bs", i64), ("dq_ls", i64), ("dk", vp), ("dk_bs", i64), ("dk_ls", i64),
+                ("dv", vp), ("dv_bs", i64), ("dv_ls", i64), ("workspace", vp)]
+
+
 _SIGS = {
     "mtts_abi_version": ([], i32),
     "mtts_last_error": ([], C.c_char_p),
@@ -98,6 +112,9 @@ _SIGS = {
     "mtts_layernorm_bwd": ([C.POINTER(LNBwdArgs), vp], i32),
     "mtts_colsum_workspace": ([i32, i32, i32], i64),
     "mtts_colsum": ([vp, i32, i32, i32, i64, i32, vp, i64, vp, vp], i32),
+    "mtts_attention_fwd": ([C.POINTER(AttnFwdArgs), vp], i32),
+    "mtts_attention_bwd_workspace": ([i32, i32, i32, i32, i32, i32], i64),
+    "mtts_attention_bwd": ([C.POINTER(AttnBwdArgs), vp], i32),
 }
 
 _lib = None

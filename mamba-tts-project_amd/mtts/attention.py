@@ -48,13 +48,13 @@ class CrossAttention(nn.Module):
         d, H = self.embed_dim, self.num_heads
         W, b = self.in_proj_weight, self.in_proj_bias
         q = linear(query, W, b, rows=(0, d))
+        p_drop = self.dropout if self.training else 0.0
         if key is value:
             kv = linear(key.to(cd), W, b, rows=(d, 3 * d))
-            k, v = kv[..., :d], kv[..., d:]
+            o = attn_kernels.attention_kv(q, kv, H, key_padding_mask, p_drop)
         else:
             k = linear(key.to(cd), W, b, rows=(d, 2 * d))
             v = linear(value.to(cd), W, b, rows=(2 * d, 3 * d))
-        p_drop = self.dropout if self.training else 0.0
-        o = attn_kernels.attention(q, k, v, H, key_padding_mask, p_drop)
+            o = attn_kernels.attention(q, k, v, H, key_padding_mask, p_drop)
         out = linear(o, self.out_proj.weight, self.out_proj.bias)
         return out, None

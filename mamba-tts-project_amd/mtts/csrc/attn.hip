@@ -1,0 +1,666 @@
+// Cross-attention core (decoder -> [ref ‖ text], style blocks) on gfx950 MFMA.
+//
+// Reference: nn.MultiheadAttention(batch_first=True) at mamba_decoder.py:32-36
+// called at :72-77, and style_cross_attention.py:91-96/125-131, 237-242/270-276;
+// torch computes softmax(q k^T * scale + key_padding_mask(-inf)) v per head,
+// and a query whose keys are all masked comes out NaN.  The key side here is
+// short (text + reference frames, 10^2 keys) and the query side long (audio
+// frames, 10^3-10^4), so:
+//
+// Forward (one wave = 32 queries, workgroup = up to 4 waves):
+//   * S^T = K . Q^T with the QUERY on the MFMA lane and 32 keys in registers:
+//     the softmax row max / sum are lane-local plus one permlane32 swap, and
+//     the exponentiated tile is directly the B operand of O^T += V^T . P^T
+//     (guide §3 "accumulator tile as the next MFMA's operand");
+//   * K/V blocks of 64 keys staged in LDS; V^T fragments come from the
+//     row-major V image through ds_read_b64_tr_b16 (no transposing copy),
+//     with a pitch that makes those reads bank-conflict free;
+//   * online softmax across key tiles; l = 0 at the end gives 0/0 = NaN for a
+//     fully masked query, exactly torch's result; lse = ln sum exp saved for
+//     the backward.
+// Backward (workgroup = all keys of one (batch, head) key group of 128, one
+// wave per 32 keys; sweeps a chunk of 32-query slices):
+//   * S and dP with the KEY on the lane, preloaded with -lse/scale and
+//     -delta so that P = exp2(c S) and dS = P dP need no row reductions;
+//   * dV += P^T dO and dK += dS^T Q from the accumulators as A operands, the
+//     dO / Q B-fragments via transposed LDS reads;  dK/dV stay in registers
+//     for the whole sweep;
+//   * dS goes through LDS once (transposed image) for dQ = dS K, computed by
+//     the wave that owns a 32-column slice of the head dim;
+//   * query chunks > 1 write fp32 dK/dV partials that a second pass sums in
+//     fixed order (deterministic, no atomics).
+// fp32 I/O uses the exact-f32 MFMA (v_mfma_f32_32x32x2_f32) with the same
+// structure.
+#include <type_traits>
+
+#include "common.h"
+
+namespace {
+using mtts::bf16_t;
+using mtts::kLn2;
+using mtts::kLog2e;
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kKB = 64;  // forward: keys per LDS block
+
+__device__ __forceinline__ f32x16 mfma_bf16(s16x8 a, s16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                  0);
+}
+__device__ __forceinline__ f32x16 mfma_f32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q / cols
+// 4p..4p+3 of a 4x16 block; lane i receives column i, row q in element q.
+__device__ __forceinline__ s16x4 tr_read(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+}
+__device__ __forceinline__ s16x8 cat(s16x4 lo, s16x4 hi) {
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+__device__ __forceinline__ short bfbits(float x) { return __builtin_bit_cast(short, (__bf16)x); }
+// registers 8s..8s+7 of a 32x32 accumulator as the bf16 fragment of k-step s:
+// element j of lane half h is accumulator row 16s + 8(j>>2) + 4h + (j&3)
+__device__ __forceinline__ s16x8 pack8(const f32x16& x, int s) {
+  s16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = bfbits(x[8 * s + j]);
+  return r;
+}
+// accumulator row held in register i by lane half h (32x32 C/D layout)
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+__device__ __forceinline__ float exp2_raw(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// LDS pitch (elements) of a bf16 [rows][hd] image read with tr_read:
+// row pitch = 16 or 48 dwords mod 64 makes the 4 rows x 32 columns of a
+// 32-lane half hit 64 distinct banks.
+constexpr int tr_pitch(int hd) {
+  int dw = hd / 2 < 16 ? 16 : hd / 2;
+  while (dw % 64 != 16 && dw % 64 != 48) ++dw;
+  return dw * 2;
+}
+
+template <int NL>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < NL; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ============================================================== forward
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(MttsAttnFwdArgs a) {
+  constexpr bool BF = sizeof(T) == 2;
+  constexpr int KP = BF ? HD + 8 : HD + 4;   // K image: conflict-free row reads
+  constexpr int VP = BF ? tr_pitch(HD) : HD;  // V image: conflict-free column reads
+  constexpr int ND = (HD + 31) / 32;          // 32-row dim tiles of O^T
+  constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
+  __shared__ __attribute__((aligned(16))) T sK[kKB * KP];
+  __shared__ __attribute__((aligned(16))) T sV[kKB * VP + 32];
+  __shared__ uint32_t sMask[kKB / 32];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
+  const int r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, hh = blockIdx.y;
+  const int q = (blockIdx.x * (nthr >> 6) + wave) * 32 + r;
+  const bool qv = q < a.q_len;
+  const T* qp = (const T*)a.q + b * a.q_bs + (int64_t)(qv ? q : 0) * a.q_ls + hh * HD;
+  const T* kbase = (const T*)a.k + b * a.k_bs + hh * HD;
+  const T* vbase = (const T*)a.v + b * a.v_bs + hh * HD;
+  const uint8_t* mb = a.key_padding_mask ? a.key_padding_mask + b * a.mask_bs : nullptr;
+  const float c = a.scale * kLog2e;
+
+  // Q^T as the B operand (k = head dim)
+  constexpr int NQ = BF ? HD / 16 : HD / 2;
+  typedef typename std::conditional<BF, s16x8, float>::type QFrag;
+  QFrag QF[NQ];
+  if constexpr (BF) {
+#pragma unroll
+    for (int s = 0; s < NQ; ++s) QF[s] = qv ? *(const s16x8*)((const bf16_t*)qp + 16 * s + 8 * h) : s16x8{};
+  } else {
+    // f32: k-step s, lane half h <-> dim HD/2*h + s
+#pragma unroll
+    for (int s = 0; s < NQ; s += 4) {
+      f32x4 v = qv ? *(const f32x4*)((const float*)qp + HD / 2 * h + s) : f32x4{};
+      QF[s] = v[0]; QF[s + 1] = v[1]; QF[s + 2] = v[2]; QF[s + 3] = v[3];
+    }
+  }
+
+  float m = -INFINITY, l = 0.f;
+  f32x16 O[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) O[dt] = f32x16{};
+
+  for (int k0 = 0; k0 < a.kv_len; k0 += kKB) {
+    __syncthreads();
+    for (int i = tid; i < kKB * HD / CH; i += nthr) {
+      const int row = i / (HD / CH), cc = (i % (HD / CH)) * CH;
+      const int key = k0 + row;
+      f32x4 kv = {}, vv = {};
+      if (key < a.kv_len) {
+        kv = *(const f32x4*)(kbase + key * a.k_ls + cc);
+        vv = *(const f32x4*)(vbase + key * a.v_ls + cc);
+      }
+      *(f32x4*)(sK + row * KP + cc) = kv;
+      *(f32x4*)(sV + row * VP + cc) = vv;
+    }
+    if (wave == 0) {
+      const int key = k0 + lane;
+      const bool ok = key < a.kv_len && !(mb && mb[key]);
+      const uint64_t bal = __ballot(ok);
+      if (lane == 0) {
+        sMask[0] = (uint32_t)bal;
+        sMask[1] = (uint32_t)(bal >> 32);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kKB / 32; ++t) {
+      if (k0 + t * 32 >= a.kv_len) break;
+      // S^T tile: rows = 32 keys (registers), cols = 32 queries (lanes)
+      f32x16 S = {};
+      if constexpr (BF) {
+        const bf16_t* kr = (const bf16_t*)sK + (t * 32 + r) * KP + 8 * h;
+#pragma unroll
+        for (int s = 0; s < NQ; ++s) S = mfma_bf16(*(const s16x8*)(kr + 16 * s), QF[s], S);
+      } else {
+        const float* kr = (const float*)sK + (t * 32 + r) * KP + HD / 2 * h;
+#pragma unroll
+        for (int s = 0; s < NQ; ++s) S = mfma_f32(kr[s], QF[s], S);
+      }
+      const uint32_t w = sMask[t] >> (4 * h);
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const bool ok = (w >> ((i & 3) + 8 * (i >> 2))) & 1u;
+        S[i] = ok ? S[i] * c : -INFINITY;
+        tmax = fmaxf(tmax, S[i]);
+      }
+      tmax = fmaxf(tmax, mtts::xor32(tmax, lane));
+      const float mn = fmaxf(m, tmax);
+      const float ms = mn == -INFINITY ? 0.f : mn;
+      const float alpha = exp2_raw(m - ms);
+      float ps = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        S[i] = exp2_raw(S[i] - ms);
+        ps += S[i];
+      }
+      l = l * alpha + ps;
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) O[dt][i] *= alpha;
+      // O^T += V^T P^T
+      if constexpr (BF) {
+        const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const s16x8 pb = pack8(S, s);
+#pragma unroll
+          for (int dt = 0; dt < ND; ++dt) {
+            const bf16_t* p0 = (const bf16_t*)sV + (t * 32 + 16 * s + 4 * h + qq) * VP + dt * 32 + 16 * g + 4 * pp;
+            O[dt] = mfma_bf16(cat(tr_read(p0), tr_read(p0 + 8 * VP)), pb, O[dt]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float* vr = (const float*)sV + (t * 32 + acc_row(i, h)) * VP + r;
+#pragma unroll
+          for (int dt = 0; dt < ND; ++dt) O[dt] = mfma_f32(vr[dt * 32], S[i], O[dt]);
+        }
+      }
+    }
+  }
+
+  const float lt = mtts::sum_xor32(l);
+  const float inv = 1.f / lt;  // fully masked: 0 * inf = NaN (torch MHA)
+  if (qv) {
+    T* op = (T*)a.out + b * a.o_bs + (int64_t)q * a.o_ls + hh * HD;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = dt * 32 + 8 * g4 + 4 * h;
+        if (d0 < HD) {
+          if constexpr (BF) {
+            s16x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = bfbits(O[dt][4 * g4 + e] * inv);
+            *(s16x4*)((bf16_t*)op + d0) = v;
+          } else {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = O[dt][4 * g4 + e] * inv;
+            *(f32x4*)((float*)op + d0) = v;
+          }
+        }
+      }
+    if (a.lse && h == 0) a.lse[((int64_t)b * a.heads + hh) * a.q_len + q] = (m + __builtin_amdgcn_logf(lt)) * kLn2;
+  }
+}
+
+// ============================================================== backward
+struct BwdParams {
+  MttsAttnBwdArgs a;
+  int nchunk, qchunk;  // query chunks (grid.x) and queries per chunk (multiple of 32)
+  float* part;         // nchunk > 1: fp32 dK|dV partials [nchunk][B][Tk][2*H*hd]
+  float* dq_acc;       // > 1 key group: fp32 dq accumulator [B][Tq][H*hd]
+};
+
+template <typename T, int HD>
+struct BwdCfg {
+  static constexpr bool BF = sizeof(T) == 2;
+  static constexpr int KG = (!BF && HD > 64) ? 64 : 128;  // keys per group = 32 x waves
+  static constexpr int NW = KG / 32;
+  static constexpr int P = BF ? HD + 8 : HD + 4;           // Q / dO / K / V image pitch
+  static constexpr int PS = BF ? 32 : 36;                  // dS^T image pitch (queries)
+  static constexpr int ND = (HD + 31) / 32;
+};
+
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
+  using C = BwdCfg<T, HD>;
+  constexpr bool BF = C::BF;
+  constexpr int KG = C::KG, NW = C::NW, P = C::P, PS = C::PS, ND = C::ND;
+  constexpr int CH = 16 / sizeof(T);
+  constexpr int NQ = BF ? HD / 16 : HD / 2;
+  __shared__ __attribute__((aligned(16))) T sK[KG * P + 32];
+  __shared__ __attribute__((aligned(16))) T sV[KG * P + 32];
+  __shared__ __attribute__((aligned(16))) T sQ[32 * P + 32];
+  __shared__ __attribute__((aligned(16))) T sO[32 * P + 32];  // dO image
+  __shared__ __attribute__((aligned(16))) T sS[KG * PS + 32];  // dS^T [key][query]
+  __shared__ float sL[32], sD[32];
+  __shared__ uint32_t sMask[KG / 32];
+
+  const MttsAttnBwdArgs& a = p.a;
+  const MttsAttnFwdArgs& f = a.f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int nthr = NW * 64;
+  const int r = lane & 31, h = lane >> 5;
+  const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;  // tr_read addressing
+  const int b = blockIdx.z, hh = blockIdx.y, chunk = blockIdx.x;
+  const int d = f.heads * HD;
+  const int qbeg = chunk * p.qchunk, qend = min(f.q_len, qbeg + p.qchunk);
+  const float c = f.scale * kLog2e;
+  const float inv_scale = 1.f / f.scale;
+  const uint8_t* mb = f.key_padding_mask ? f.key_padding_mask + b * f.mask_bs : nullptr;
+  const int nkg = (f.kv_len + KG - 1) / KG;
+
+  for (int kg = 0; kg < nkg; ++kg) {
+    const int kg0 = kg * KG;
+    __syncthreads();
+    {
+      const T* kb = (const T*)f.k + b * f.k_bs + hh * HD;
+      const T* vb = (const T*)f.v + b * f.v_bs + hh * HD;
+      for (int i = tid; i < KG * HD / CH; i += nthr) {
+        const int row = i / (HD / CH), cc = (i % (HD / CH)) * CH;
+        const int key = kg0 + row;
+        f32x4 kv = {}, vv = {};
+        if (key < f.kv_len) {
+          kv = *(const f32x4*)(kb + key * f.k_ls + cc);
+          vv = *(const f32x4*)(vb + key * f.v_ls + cc);
+        }
+        *(f32x4*)(sK + row * P + cc) = kv;
+        *(f32x4*)(sV + row * P + cc) = vv;
+      }
+      if (wave < KG / 64) {
+        const int key = kg0 + 64 * wave + lane;
+        const bool ok = key < f.kv_len && !(mb && mb[key]);
+        const uint64_t bal = __ballot(ok);
+        if (lane == 0) {
+          sMask[2 * wave] = (uint32_t)bal;
+          sMask[2 * wave + 1] = (uint32_t)(bal >> 32);
+        }
+      }
+    }
+    f32x16 dK[ND], dV[ND];
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) dK[dt] = dV[dt] = f32x16{};
+
+    for (int q0 = qbeg; q0 < qend; q0 += 32) {
+      __syncthreads();
+      // ---- stage Q, dO images; delta = rowsum(dO * O); -lse/scale
+      {
+        const T* qb = (const T*)f.q + b * f.q_bs + hh * HD;
+        const T* ob = (const T*)f.out + b * f.o_bs + hh * HD;
+        const T* gb = (const T*)a.dout + b * a.do_bs + hh * HD;
+        for (int i = tid; i < 32 * HD / CH; i += nthr) {
+          const int row = i / (HD / CH), cc = (i % (HD / CH)) * CH;
+          const int qi = q0 + row;
+          f32x4 qv = {}, gv = {}, ov = {};
+          if (qi < qend) {
+            qv = *(const f32x4*)(qb + qi * f.q_ls + cc);
+            gv = *(const f32x4*)(gb + qi * a.do_ls + cc);
+            ov = *(const f32x4*)(ob + qi * f.o_ls + cc);
+          }
+          *(f32x4*)(sQ + row * P + cc) = qv;
+          *(f32x4*)(sO + row * P + cc) = gv;
+          float dl = 0.f;
+          if constexpr (BF) {
+            const s16x8 g8 = __builtin_bit_cast(s16x8, gv), o8 = __builtin_bit_cast(s16x8, ov);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dl += mtts::bf2f((bf16_t)g8[e]) * mtts::bf2f((bf16_t)o8[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dl += gv[e] * ov[e];
+          }
+          dl = group_sum<HD / CH>(dl);
+          if (i % (HD / CH) == 0) sD[row] = -dl;
+        }
+        if (tid < 32) {
+          const int qi = q0 + tid;
+          float L = 0.f;
+          if (qi < qend) L = -f.lse[((int64_t)b * f.heads + hh) * f.q_len + qi] * inv_scale;  // P = exp2(c (S + L))
+          sL[tid] = L;
+        }
+      }
+      __syncthreads();
+      // ---- S = Q K^T - lse/scale and dP = dO V^T - delta (key on the lane)
+      f32x16 S, D;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        S[i] = sL[acc_row(i, h)];
+        D[i] = sD[acc_row(i, h)];
+      }
+      const int key = wave * 32 + r;  // within the group
+      if constexpr (BF) {
+        const bf16_t* qr = (const bf16_t*)sQ + r * P + 8 * h;
+        const bf16_t* orow = (const bf16_t*)sO + r * P + 8 * h;
+        const bf16_t* kr = (const bf16_t*)sK + key * P + 8 * h;
+        const bf16_t* vr = (const bf16_t*)sV + key * P + 8 * h;
+#pragma unroll
+        for (int s = 0; s < NQ; ++s) {
+          S = mfma_bf16(*(const s16x8*)(qr + 16 * s), *(const s16x8*)(kr + 16 * s), S);
+          D = mfma_bf16(*(const s16x8*)(orow + 16 * s), *(const s16x8*)(vr + 16 * s), D);
+        }
+      } else {
+        const float* qr = (const float*)sQ + r * P + HD / 2 * h;
+        const float* orow = (const float*)sO + r * P + HD / 2 * h;
+        const float* kr = (const float*)sK + key * P + HD / 2 * h;
+        const float* vr = (const float*)sV + key * P + HD / 2 * h;
+#pragma unroll
+        for (int s = 0; s < NQ; ++s) {
+          S = mfma_f32(qr[s], kr[s], S);
+          D = mfma_f32(orow[s], vr[s], D);
+        }
+      }
+      const bool kvalid = (sMask[wave] >> r) & 1u;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        S[i] = kvalid ? exp2_raw(c * S[i]) : 0.f;  // P
+        D[i] = S[i] * D[i];                         // dS (unscaled)
+      }
+      // ---- dV += P^T dO, dK += dS^T Q (accumulators as A operands)
+      if constexpr (BF) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const s16x8 pa = pack8(S, s), da = pack8(D, s);
+#pragma unroll
+          for (int dt = 0; dt < ND; ++dt) {
+            const int off = (16 * s + 4 * h + qq) * P + dt * 32 + 16 * g + 4 * pp;
+            const bf16_t* po = (const bf16_t*)sO + off;
+            const bf16_t* pq = (const bf16_t*)sQ + off;
+            dV[dt] = mfma_bf16(pa, cat(tr_read(po), tr_read(po + 8 * P)), dV[dt]);
+            dK[dt] = mfma_bf16(da, cat(tr_read(pq), tr_read(pq + 8 * P)), dK[dt]);
+          }
+        }
+        // dS^T image: lane (key) stores query rows 8g4+4h..+3
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          s16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = bfbits(D[4 * g4 + e]);
+          *(s16x4*)((bf16_t*)sS + key * PS + 8 * g4 + 4 * h) = v;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = acc_row(i, h);
+          const float* po = (const float*)sO + row * P + r;
+          const float* pq = (const float*)sQ + row * P + r;
+#pragma unroll
+          for (int dt = 0; dt < ND; ++dt) {
+            dV[dt] = mfma_f32(S[i], po[dt * 32], dV[dt]);
+            dK[dt] = mfma_f32(D[i], pq[dt * 32], dK[dt]);
+          }
+        }
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          *(f32x4*)((float*)sS + key * PS + 8 * g4 + 4 * h) =
+              f32x4{D[4 * g4], D[4 * g4 + 1], D[4 * g4 + 2], D[4 * g4 + 3]};
+      }
+      __syncthreads();
+      // ---- dQ[q][dims of tile dt] = scale * dS K over the group's keys
+      for (int dt = wave; dt < ND; dt += NW) {
+        f32x16 Q = {};
+        if constexpr (BF) {
+#pragma unroll
+          for (int s = 0; s < KG / 16; ++s) {
+            const bf16_t* ps = (const bf16_t*)sS + (16 * s + 8 * h + qq) * PS + 16 * g + 4 * pp;
+            const bf16_t* pk = (const bf16_t*)sK + (16 * s + 8 * h + qq) * P + dt * 32 + 16 * g + 4 * pp;
+            Q = mfma_bf16(cat(tr_read(ps), tr_read(ps + 4 * PS)), cat(tr_read(pk), tr_read(pk + 4 * P)), Q);
+          }
+        } else {
+#pragma unroll 8
+          for (int s = 0; s < KG / 2; ++s) {
+            const int kk = KG / 2 * h + s;
+            Q = mfma_f32(((const float*)sS)[kk * PS + r], ((const float*)sK)[kk * P + dt * 32 + r], Q);
+          }
+        }
+        const int dim = dt * 32 + r;
+        if (dim < HD) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int qi = q0 + acc_row(i, h);
+            if (qi < qend) {
+              float v = Q[i] * f.scale;
+              if (nkg > 1) {
+                float* acc = p.dq_acc + ((int64_t)b * f.q_len + qi) * d + hh * HD + dim;
+                if (kg > 0) v += *acc;
+                if (kg + 1 < nkg) {
+                  *acc = v;
+                  continue;
+                }
+              }
+              mtts::stf((T*)a.dq + b * a.dq_bs + (int64_t)qi * a.dq_ls + hh * HD + dim, v);
+            }
+          }
+        }
+      }
+    }
+    // ---- dK (scaled), dV of this wave's 32 keys: rows = keys (registers), cols = dims (lanes)
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int dim = dt * 32 + r;
+      if (dim >= HD) continue;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kk = kg0 + wave * 32 + acc_row(i, h);
+        if (kk >= f.kv_len) continue;
+        const float vk = dK[dt][i] * f.scale, vv = dV[dt][i];
+        if (p.nchunk > 1) {
+          float* pr = p.part + (((int64_t)chunk * f.batch + b) * f.kv_len + kk) * (2 * d) + hh * HD + dim;
+          pr[0] = vk;
+          pr[d] = vv;
+        } else {
+          mtts::stf((T*)a.dk + b * a.dk_bs + (int64_t)kk * a.dk_ls + hh * HD + dim, vk);
+          mtts::stf((T*)a.dv + b * a.dv_bs + (int64_t)kk * a.dv_ls + hh * HD + dim, vv);
+        }
+      }
+    }
+  }
+}
+
+// sum of the query-chunk partials -> dk, dv (fixed order)
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_reduce_kernel(BwdParams p) {
+  const MttsAttnBwdArgs& a = p.a;
+  const MttsAttnFwdArgs& f = a.f;
+  const int d = f.heads * f.head_dim;
+  const int64_t n = (int64_t)f.batch * f.kv_len * 2 * d;
+  const int64_t stride = (int64_t)f.batch * f.kv_len * 2 * d;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int cix = 0; cix < p.nchunk; ++cix) s += p.part[cix * stride + e];
+    const int col = (int)(e % (2 * d));
+    const int64_t bk = e / (2 * d);
+    const int b = (int)(bk / f.kv_len), kk = (int)(bk % f.kv_len);
+    if (col < d)
+      mtts::stf((T*)a.dk + b * a.dk_bs + (int64_t)kk * a.dk_ls + col, s);
+    else
+      mtts::stf((T*)a.dv + b * a.dv_bs + (int64_t)kk * a.dv_ls + col - d, s);
+  }
+}
+
+// ============================================================== host side
+bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
+
+int check_fwd(const MttsAttnFwdArgs* a, const char* who) {
+  MTTS_CHECK(a, "%s: null args", who);
+  MTTS_CHECK(a->dtype == MTTS_F32 || a->dtype == MTTS_BF16, "%s: dtype must be F32 or BF16", who);
+  MTTS_CHECK(a->head_dim == 16 || a->head_dim == 32 || a->head_dim == 64 || a->head_dim == 128,
+             "%s: head_dim %d not in {16,32,64,128}", who, a->head_dim);
+  MTTS_CHECK(a->batch >= 0 && a->heads > 0 && a->q_len >= 0 && a->kv_len >= 0, "%s: bad sizes", who);
+  MTTS_CHECK(a->q && a->k && a->v && a->out, "%s: null tensor", who);
+  const int64_t al = a->dtype == MTTS_BF16 ? 8 : 4;
+  MTTS_CHECK(aligned16(a->q) && aligned16(a->k) && aligned16(a->v) && aligned16(a->out),
+             "%s: q/k/v/out must be 16-byte aligned", who);
+  MTTS_CHECK(a->q_bs % al == 0 && a->q_ls % al == 0 && a->k_bs % al == 0 && a->k_ls % al == 0 && a->v_bs % al == 0 &&
+                 a->v_ls % al == 0 && a->o_bs % al == 0 && a->o_ls % al == 0,
+             "%s: strides must be multiples of 16 bytes", who);
+  return MTTS_OK;
+}
+
+template <typename T, int HD>
+void launch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
+  const int nw = a->q_len >= 128 ? 4 : (a->q_len + 31) / 32;
+  dim3 grid((a->q_len + 32 * nw - 1) / (32 * nw), a->heads, a->batch);
+  attn_fwd_kernel<T, HD><<<grid, 64 * nw, 0, st>>>(*a);
+}
+
+template <typename T>
+void dispatch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
+  switch (a->head_dim) {
+    case 16: launch_fwd<T, 16>(a, st); break;
+    case 32: launch_fwd<T, 32>(a, st); break;
+    case 64: launch_fwd<T, 64>(a, st); break;
+    default: launch_fwd<T, 128>(a, st); break;
+  }
+}
+
+struct BwdPlan {
+  int nchunk, qchunk, kg;
+  int64_t part_bytes, dq_bytes;
+};
+
+BwdPlan plan_bwd(int batch, int heads, int head_dim, int q_len, int kv_len, int dtype) {
+  BwdPlan pl{};
+  pl.kg = (dtype == MTTS_F32 && head_dim > 64) ? 64 : 128;
+  const int slices = (q_len + 31) / 32;
+  const int base = batch * heads;
+  int nchunk = base >= 256 ? 1 : (256 + base - 1) / base;
+  if (const char* e = getenv("MTTS_ATTN_CHUNKS")) nchunk = atoi(e);
+  nchunk = nchunk < 1 ? 1 : (nchunk > slices ? (slices > 0 ? slices : 1) : nchunk);
+  const int per = (slices + nchunk - 1) / nchunk;
+  pl.qchunk = 32 * (per > 0 ? per : 1);
+  pl.nchunk = (q_len + pl.qchunk - 1) / pl.qchunk;
+  if (pl.nchunk < 1) pl.nchunk = 1;
+  const int64_t d = (int64_t)heads * head_dim;
+  pl.part_bytes = pl.nchunk > 1 ? (int64_t)pl.nchunk * batch * kv_len * 2 * d * 4 : 0;
+  pl.dq_bytes = kv_len > pl.kg ? (int64_t)batch * q_len * d * 4 : 0;
+  return pl;
+}
+
+template <typename T, int HD>
+void launch_bwd(const BwdParams& p, hipStream_t st) {
+  dim3 grid(p.nchunk, p.a.f.heads, p.a.f.batch);
+  attn_bwd_kernel<T, HD><<<grid, BwdCfg<T, HD>::NW * 64, 0, st>>>(p);
+}
+
+template <typename T>
+void dispatch_bwd(const BwdParams& p, hipStream_t st) {
+  switch (p.a.f.head_dim) {
+    case 16: launch_bwd<T, 16>(p, st); break;
+    case 32: launch_bwd<T, 32>(p, st); break;
+    case 64: launch_bwd<T, 64>(p, st); break;
+    default: launch_bwd<T, 128>(p, st); break;
+  }
+  if (p.nchunk > 1) {
+    const int64_t n = (int64_t)p.a.f.batch * p.a.f.kv_len * 2 * p.a.f.heads * p.a.f.head_dim;
+    int blocks = (int)((n + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    attn_bwd_reduce_kernel<T><<<blocks, 256, 0, st>>>(p);
+  }
+}
+
+}  // namespace
+
+extern "C" int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream) {
+  int rc = check_fwd(a, "attention_fwd");
+  if (rc) return rc;
+  if (a->batch == 0 || a->q_len == 0) return MTTS_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (a->dtype == MTTS_BF16)
+    dispatch_fwd<bf16_t>(a, st);
+  else
+    dispatch_fwd<float>(a, st);
+  MTTS_LAUNCH_CHECK("attention_fwd");
+  return MTTS_OK;
+}
+
+extern "C" int64_t mtts_attention_bwd_workspace(int batch, int heads, int head_dim, int q_len, int kv_len, int dtype) {
+  const BwdPlan pl = plan_bwd(batch, heads, head_dim, q_len, kv_len, dtype);
+  return pl.part_bytes + pl.dq_bytes + 256;
+}
+
+extern "C" int mtts_attention_bwd(const MttsAttnBwdArgs* a, void* stream) {
+  MTTS_CHECK(a, "attention_bwd: null args");
+  int rc = check_fwd(&a->f, "attention_bwd");
+  if (rc) return rc;
+  const MttsAttnFwdArgs& f = a->f;
+  MTTS_CHECK(a->dout && a->dq && a->dk && a->dv && f.lse, "attention_bwd: null tensor (dout/dq/dk/dv/lse)");
+  const int64_t al = f.dtype == MTTS_BF16 ? 8 : 4;
+  MTTS_CHECK(aligned16(a->dout) && a->do_bs % al == 0 && a->do_ls % al == 0,
+             "attention_bwd: dout must be 16-byte aligned with 16-byte strides");
+  hipStream_t st = (hipStream_t)stream;
+  const int es = f.dtype == MTTS_BF16 ? 2 : 4;
+  const int64_t d = (int64_t)f.heads * f.head_dim;
+  if (f.batch == 0) return MTTS_OK;
+  if (f.q_len == 0 || f.kv_len == 0) {
+    // no queries: dk = dv = 0 (dq is empty or has no keys: zero as well)
+    for (int b = 0; b < f.batch; ++b) {
+      for (int64_t t = 0; t < f.kv_len; ++t) {
+        (void)hipMemsetAsync((char*)a->dk + (b * a->dk_bs + t * a->dk_ls) * es, 0, d * es, st);
+        (void)hipMemsetAsync((char*)a->dv + (b * a->dv_bs + t * a->dv_ls) * es, 0, d * es, st);
+      }
+      for (int64_t t = 0; t < f.q_len; ++t)
+        (void)hipMemsetAsync((char*)a->dq + (b * a->dq_bs + t * a->dq_ls) * es, 0, d * es, st);
+    }
+    return MTTS_OK;
+  }
+  const BwdPlan pl = plan_bwd(f.batch, f.heads, f.head_dim, f.q_len, f.kv_len, f.dtype);
+  MTTS_CHECK(a->workspace || (pl.part_bytes + pl.dq_bytes) == 0, "attention_bwd: workspace required");
+  BwdParams p;
+  p.a = *a;
+  p.nchunk = pl.nchunk;
+  p.qchunk = pl.qchunk;
+  p.part = pl.part_bytes ? (float*)a->workspace : nullptr;
+  p.dq_acc = pl.dq_bytes ? (float*)((char*)a->workspace + pl.part_bytes) : nullptr;
+  if (f.dtype == MTTS_BF16)
+    dispatch_bwd<bf16_t>(p, st);
+  else
+    dispatch_bwd<float>(p, st);
+  MTTS_LAUNCH_CHECK("attention_bwd");
+  return MTTS_OK;
+}

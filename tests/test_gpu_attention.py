@@ -1,0 +1,161 @@
+"""HIP cross-attention (mtts_attention_fwd / _bwd) against a float64 PyTorch
+restatement of nn.MultiheadAttention's core (softmax(q k^T/sqrt(hd) + kpm) v,
+reference call sites mamba_decoder.py:72-77, style_cross_attention.py:125-131).
+
+Tolerances: fp32 I/O runs exact-f32 MFMA, so 2e-5 relative to the output
+scale; bf16 I/O rounds P / dS to bf16 before the P.V / dS.K products
+(flash-attention practice), checked at 2e-2 of the output scale."""
+import math
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_attention(q, k, v, H, kpm):
+    B, T, d = q.shape
+    S = k.shape[1]
+    hd = d // H
+    qh = q.double().view(B, T, H, hd).transpose(1, 2)
+    kh = k.double().reshape(B, S, H, hd).transpose(1, 2)
+    vh = v.double().reshape(B, S, H, hd).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) / math.sqrt(hd)
+    if kpm is not None:
+        s = s.masked_fill(kpm[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, -1)
+    return (p @ vh).transpose(1, 2).reshape(B, T, d), torch.logsumexp(s, -1)
+
+
+def make(B, T, S, H, hd, dtype, seed=0, mask=True, full_mask_batch=None):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    d = H * hd
+    q = torch.randn(B, T, d, device="cuda", generator=g).to(dtype)
+    kv = torch.randn(B, S, 2 * d, device="cuda", generator=g).to(dtype)
+    kpm = None
+    if mask:
+        kpm = torch.rand(B, S, device="cuda", generator=g) < 0.3
+        kpm[:, 0] = False
+        if full_mask_batch is not None:
+            kpm[full_mask_batch] = True
+    return q, kv, kpm
+
+
+def close(got, ref, tol):
+    scale = ref.abs().max().item() + 1e-6
+    err = (got.double() - ref).abs().max().item()
+    assert err <= tol * scale, f"max err {err:.3e} > {tol} * {scale:.3e}"
+
+
+CASES = [  # B, T, S, H, hd
+    (2, 64, 12, 4, 16),
+    (3, 70, 20, 4, 16),
+    (2, 33, 64, 2, 32),
+    (2, 130, 100, 4, 64),
+    (2, 256, 128, 8, 128),
+    (1, 40, 130, 2, 128),
+    (2, 1, 128, 8, 128),
+    (1, 5, 300, 2, 64),
+    (2, 17, 1, 2, 32),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES)
+def test_forward_matches_reference(case, dtype):
+    from mtts import attn_kernels as A
+    B, T, S, H, hd = case
+    q, kv, kpm = make(B, T, S, H, hd, dtype, mask=S > 1)
+    d = H * hd
+    out, lse = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+    ref, ref_lse = ref_attention(q, kv[..., :d], kv[..., d:], H, kpm)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    close(out, ref, tol)
+    close(lse, ref_lse, 1e-5 if dtype == torch.float32 else 1e-2)
+
+
+def test_fully_masked_rows_are_nan_and_others_exact():
+    from mtts import attn_kernels as A
+    B, T, S, H, hd = 3, 40, 24, 4, 16
+    q, kv, kpm = make(B, T, S, H, hd, torch.float32, full_mask_batch=1)
+    d = H * hd
+    out, lse = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+    assert torch.isnan(out[1]).all()
+    assert torch.isinf(lse[1]).all() and (lse[1] < 0).all()
+    ref, _ = ref_attention(q, kv[..., :d], kv[..., d:], H, kpm)
+    close(out[[0, 2]], ref[[0, 2]], 2e-5)
+
+
+def test_no_mask_and_separate_k_v_tensors():
+    from mtts import attn_kernels as A
+    B, T, S, H, hd = 2, 50, 37, 4, 32
+    q, kv, _ = make(B, T, S, H, hd, torch.float32, mask=False)
+    d = H * hd
+    k, v = kv[..., :d].contiguous(), kv[..., d:].contiguous()
+    out = A.attention(q, k, v, H)
+    ref, _ = ref_attention(q, k, v, H, None)
+    close(out, ref, 2e-5)
+
+
+def _grads(q, kv, H, kpm, fused):
+    from mtts import attn_kernels as A
+    d = q.shape[-1]
+    q = q.detach().requires_grad_(True)
+    kv = kv.detach().requires_grad_(True)
+    if fused:
+        o = A.attention_kv(q, kv, H, kpm)
+    else:
+        o = A.attention(q, kv[..., :d], kv[..., d:], H, kpm)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    do = torch.randn(o.shape, device="cuda", generator=g).to(o.dtype)
+    o.backward(do)
+    return o, q.grad, kv.grad, do
+
+
+def _ref_grads(q, kv, H, kpm, do):
+    d = q.shape[-1]
+    q = q.detach().double().requires_grad_(True)
+    kv = kv.detach().double().requires_grad_(True)
+    o, _ = ref_attention(q, kv[..., :d], kv[..., d:], H, kpm)
+    o.backward(do.double())
+    return q.grad, kv.grad
+
+
+@pytest.mark.parametrize("chunks", [None, "1", "3"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES[:-3] + [(1, 5, 300, 2, 64)])
+def test_backward_matches_reference(case, dtype, chunks, monkeypatch):
+    if chunks is not None:
+        monkeypatch.setenv("MTTS_ATTN_CHUNKS", chunks)
+    B, T, S, H, hd = case
+    q, kv, kpm = make(B, T, S, H, hd, dtype, seed=3)
+    o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
+    rq, rkv = _ref_grads(q, kv, H, kpm, do)
+    tol = 5e-5 if dtype == torch.float32 else 3e-2
+    close(dq, rq, tol)
+    close(dkv, rkv, tol)
+
+
+def test_backward_separate_kv_and_determinism():
+    B, T, S, H, hd = 2, 96, 50, 4, 64
+    q, kv, kpm = make(B, T, S, H, hd, torch.bfloat16, seed=9)
+    _, dq1, dkv1, do = _grads(q, kv, H, kpm, fused=False)
+    _, dq2, dkv2, _ = _grads(q, kv, H, kpm, fused=True)
+    assert torch.equal(dq1, dq2) and torch.equal(dkv1, dkv2)
+    rq, rkv = _ref_grads(q, kv, H, kpm, do)
+    close(dq1, rq, 3e-2)
+    close(dkv1, rkv, 3e-2)
+
+
+def test_north_star_shape_bf16():
+    """C2 decoder shape: B=8, T_audio=2048, T_text=128 (10 % padded), d=1024, H=8."""
+    B, T, S, H, hd = 8, 2048, 128, 8, 128
+    q, kv, _ = make(B, T, S, H, hd, torch.bfloat16, seed=11, mask=False)
+    kpm = torch.zeros(B, S, dtype=torch.bool, device="cuda")
+    kpm[:, int(S * 0.9):] = True
+    o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
+    # reference on two batches (float64 on the full batch is slow but fine)
+    rq, rkv = _ref_grads(q[:2], kv[:2], H, kpm[:2], do[:2])
+    close(dq[:2], rq, 3e-2)
+    close(dkv[:2], rkv, 3e-2)
