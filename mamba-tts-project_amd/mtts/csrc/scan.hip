@@ -152,6 +152,49 @@ __device__ __forceinline__ void store_vec(float* p, const float (&v)[NS]) {
     *reinterpret_cast<float4*>(p + 4 * q) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
 }
 
+// Prefetched activations stay in their storage format until used: converting
+// right after the load would make the compiler wait for the load there (the
+// prefetch would then cost a full memory latency per group).
+template <typename T> struct RawT;
+template <> struct RawT<float> { using type = float; };
+template <> struct RawT<bf16_t> { using type = uint32_t; };
+template <typename T> using raw_t = typename RawT<T>::type;
+__device__ __forceinline__ float cvt_raw(float v) { return v; }
+__device__ __forceinline__ float cvt_raw(uint32_t v) { return __uint_as_float(v << 16); }
+template <typename T>
+__device__ __forceinline__ raw_t<T> ldr(const T* p) { return (raw_t<T>)*p; }
+
+// N consecutive elements as raw 32-bit words (one vector load), unpacked at use
+template <typename T, int N>
+struct RawVec {
+  static constexpr int W = N * (int)sizeof(T) / 4;
+  static_assert(W == 1 || W == 2 || W == 4 || W == 8, "RawVec width");
+  uint32_t w[W];
+  __device__ __forceinline__ void load(const T* p) {
+    if constexpr (W == 1) {
+      w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (W == 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      w[0] = v.x; w[1] = v.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < W / 4; ++q) {
+        const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint32_t*>(p) + 4 * q);
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      }
+    }
+  }
+  __device__ __forceinline__ void unpack(float (&o)[N]) const {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) o[i] = __uint_as_float(w[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < W; ++i) unpack_bf2(w[i], o[2 * i], o[2 * i + 1]);
+    }
+  }
+};
+
 // ------------------------------------------------------------- forward
 // L is cut into K segments of seg_len steps (K = 1 when B*D alone fills the
 // chip).  MODE kState (pass 1) scans segments 0..K-2 from h = 0 and writes
@@ -186,11 +229,13 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
   // so loads/stores use the saddr form with no per-access VALU index math.
   const Tio* __restrict__ u0 = (const Tio*)a.u + (int64_t)b * a.u_bs;
   const Tio* __restrict__ d0 = (const Tio*)a.delta + (int64_t)b * a.delta_bs;
-  const Tio* __restrict__ z0 = a.z ? (const Tio*)a.z + (int64_t)b * a.z_bs : nullptr;
+  const bool has_z = MODE == kFull && a.z != nullptr;
+  // without z the z loads read u (never used): no conditional loads in the loop
+  const Tio* __restrict__ z0 = has_z ? (const Tio*)a.z + (int64_t)b * a.z_bs : u0;
+  const int64_t z_ls = has_z ? a.z_ls : a.u_ls;
   Tio* __restrict__ o0 = (Tio*)a.out + (int64_t)b * a.out_bs;
   const uint32_t lu = (uint32_t)(j * a.u_ls + c), ld = (uint32_t)(j * a.delta_ls + c);
-  const uint32_t lz = (uint32_t)(j * a.z_ls + c), lo = (uint32_t)(j * a.out_ls + c);
-  const bool has_z = MODE == kFull && z0 != nullptr;
+  const uint32_t lz = (uint32_t)(j * z_ls + c), lo = (uint32_t)(j * a.out_ls + c);
 
   // this thread's slice of the cooperative B/C staging
   const int e0 = threadIdx.x * VPT;
@@ -223,22 +268,24 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
   float* __restrict__ ck0 = nck ? a.ckpt + (int64_t)b * nck * a.dim * kN : nullptr;
   const uint32_t lck = (uint32_t)(c * kN + j * NS);
 
-  float cu[G], cd[G], cz[G], nu[G], nd[G], nz[G], stv[VPT];
+  using R = raw_t<Tio>;
+  R cu[G], cd[G], cz[G], nu[G], nd[G], nz[G];
+  RawVec<Tbc, VPT> stv;
   // TAIL: some timesteps of the tile are >= t_end -> clamp to the last valid one
-  auto load_regs = [&](auto tail, int t0, float (&uu)[G], float (&dd)[G], float (&zz)[G]) {
+  auto load_regs = [&](auto tail, int t0, R (&uu)[G], R (&dd)[G], R (&zz)[G]) {
     constexpr bool TAIL = decltype(tail)::value;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int tg = t0 + g * P;
       if constexpr (TAIL) {
         const int ts = min(tg + j, L - 1);
-        uu[g] = ldf(u0 + (int64_t)ts * a.u_ls + c);
-        dd[g] = ldf(d0 + (int64_t)ts * a.delta_ls + c);
-        zz[g] = has_z ? ldf(z0 + (int64_t)ts * a.z_ls + c) : 0.f;
+        uu[g] = ldr(u0 + (int64_t)ts * a.u_ls + c);
+        dd[g] = ldr(d0 + (int64_t)ts * a.delta_ls + c);
+        if constexpr (MODE == kFull) zz[g] = ldr(z0 + (int64_t)ts * z_ls + c);
       } else {
-        uu[g] = ldf(u0 + (int64_t)tg * a.u_ls + lu);
-        dd[g] = ldf(d0 + (int64_t)tg * a.delta_ls + ld);
-        zz[g] = has_z ? ldf(z0 + (int64_t)tg * a.z_ls + lz) : 0.f;
+        uu[g] = ldr(u0 + (int64_t)tg * a.u_ls + lu);
+        dd[g] = ldr(d0 + (int64_t)tg * a.delta_ls + ld);
+        if constexpr (MODE == kFull) zz[g] = ldr(z0 + (int64_t)tg * z_ls + lz);
         static_assert(sizeof(lu) == 4, "32-bit lane offsets -> saddr loads");
       }
     }
@@ -246,17 +293,19 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
   auto load_stage = [&](auto tail, int t0) {
     constexpr bool TAIL = decltype(tail)::value;
     if constexpr (TAIL) {
-      load_vec<Tbc, VPT>(st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN), stv);
+      stv.load(st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN));
     } else {
-      load_vec<Tbc, VPT>(st0 + (int64_t)t0 * st_ls + lst, stv);
+      stv.load(st0 + (int64_t)t0 * st_ls + lst);
     }
   };
   auto write_stage = [&](int buf) {
+    float v[VPT];
+    stv.unpack(v);
     if constexpr (VPT == 4) {
-      *reinterpret_cast<float4*>(&sBC[buf][e0]) = make_float4(stv[0], stv[1], stv[2], stv[3]);
+      *reinterpret_cast<float4*>(&sBC[buf][e0]) = make_float4(v[0], v[1], v[2], v[3]);
     } else {
 #pragma unroll
-      for (int v = 0; v < VPT; ++v) sBC[buf][e0 + v] = stv[v];
+      for (int q = 0; q < VPT; ++q) sBC[buf][e0 + q] = v[q];
     }
   };
   auto compute_tile = [&](auto tail, int t0, int buf) {
@@ -267,10 +316,11 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
       if (nck && (tg % a.ckpt_chunk) == 0 && (!TAIL || tg < t_end))
         store_vec<NS>(ck0 + (int64_t)(tg / a.ckpt_chunk) * a.dim * kN + lck, h);
       const bool tv = !TAIL || (tg + j < t_end);
-      float dt = cd[g] + bias;
+      float dt = cvt_raw(cd[g]) + bias;
       if constexpr (SP) dt = softplus_f(dt);
       if constexpr (TAIL) dt = tv ? dt : 0.f;  // padded steps are the identity map
-      const float dtu = dt * cu[g];
+      const float ug = cvt_raw(cu[g]);
+      const float dtu = dt * ug;
       if constexpr (MODE == kState) S += dt;
       float yp[P];
 #pragma unroll
@@ -307,8 +357,8 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
       }
       if constexpr (MODE == kFull) {
         float y = group_reduce_scatter<P>(yp, j);
-        y = fmaf(Dc, cu[g], y);
-        if (has_z) y *= silu_f(cz[g]);
+        y = fmaf(Dc, ug, y);
+        if (has_z) y *= silu_f(cvt_raw(cz[g]));
         if constexpr (TAIL) {
           if (tv) stf(o0 + (int64_t)(tg + j) * a.out_ls + c, y);
         } else {
@@ -381,6 +431,18 @@ constexpr int kWaves = kBlock / 64;
 template <int S>
 __device__ __forceinline__ float bcast4(float v) { return dpp<S * 0x55>(v); }
 
+// reduce-scatter stages with the swap instructions (no lane selects):
+// lanes 0-31 get a + a[lane+32], lanes 32-63 get b + b[lane-32]
+__device__ __forceinline__ float rs_swap32(float a, float b) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// rows 0,2 get a + a[lane+16], rows 1,3 get b + b[lane-16]
+__device__ __forceinline__ float rs_swap16(float a, float b) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // Reduce 32 values per lane over the 16 channel-lanes of the wave (lane bits
 // 2..5), keeping the state-group bits 0..1.  On return lane holds 2 values:
 // value index v = (l2<<4)|(l3<<3)|(l4<<2)|(l5<<1)|e  (e = 0, 1).
@@ -451,9 +513,11 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   const int t_begin = k * seg_len;
   const int t_end = min(L, t_begin + seg_len);
   const Tio* __restrict__ d0 = (const Tio*)f.delta + (int64_t)b * f.delta_bs;
-  const Tio* __restrict__ z0 = f.z ? (const Tio*)f.z + (int64_t)b * f.z_bs : nullptr;
+  const bool has_z = f.z != nullptr;
+  const Tio* __restrict__ z0 = has_z ? (const Tio*)f.z + (int64_t)b * f.z_bs : d0;  // no z: loads ignored
+  const int64_t z_ls = has_z ? f.z_ls : f.delta_ls;
   const Tio* __restrict__ g0 = (const Tio*)a.dout + (int64_t)b * a.dout_bs;
-  const uint32_t od = (uint32_t)(j * f.delta_ls + c), oz = (uint32_t)(j * f.z_ls + c);
+  const uint32_t od = (uint32_t)(j * f.delta_ls + c), oz = (uint32_t)(j * z_ls + c);
   const uint32_t og = (uint32_t)(j * a.dout_ls + c);
   const Tbc* __restrict__ C0 = (const Tbc*)f.Cm + (int64_t)b * f.C_bs;
   const int e0 = threadIdx.x * 2;          // staged C values of this thread: step e0/16, state e0%16
@@ -466,29 +530,36 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   }
   const float bias = f.delta_bias ? f.delta_bias[c] : 0.f;
   float S = 0.f;
-  float cx[G], cg[G], cz[G], nx[G], ng[G], nz[G], st[2];
-  auto load = [&](int t0, float (&xx)[G], float (&gg)[G], float (&zz)[G]) {
+  using R = raw_t<Tio>;
+  R cx[G], cg[G], cz[G], nx[G], ng[G], nz[G];
+  RawVec<Tbc, 2> st;
+  // steps >= t_end load a clamped index; their dy is zeroed at use
+  auto load = [&](int t0, R (&xx)[G], R (&gg)[G], R (&zz)[G]) {
     const bool full = t0 + TT <= t_end;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int tg = t0 + g * kPB;
       if (full) {
-        xx[g] = ldf(d0 + (int64_t)tg * f.delta_ls + od);
-        gg[g] = ldf(g0 + (int64_t)tg * a.dout_ls + og);
-        zz[g] = z0 ? ldf(z0 + (int64_t)tg * f.z_ls + oz) : 0.f;
+        xx[g] = ldr(d0 + (int64_t)tg * f.delta_ls + od);
+        gg[g] = ldr(g0 + (int64_t)tg * a.dout_ls + og);
+        zz[g] = ldr(z0 + (int64_t)tg * z_ls + oz);
       } else {
-        const int ts = tg + j;
-        const int tc = min(ts, L - 1);
-        xx[g] = ldf(d0 + (int64_t)tc * f.delta_ls + c);
-        gg[g] = ts < t_end ? ldf(g0 + (int64_t)tc * a.dout_ls + c) : 0.f;
-        zz[g] = z0 ? ldf(z0 + (int64_t)tc * f.z_ls + c) : 0.f;
+        const int tc = min(tg + j, L - 1);
+        xx[g] = ldr(d0 + (int64_t)tc * f.delta_ls + c);
+        gg[g] = ldr(g0 + (int64_t)tc * a.dout_ls + c);
+        zz[g] = ldr(z0 + (int64_t)tc * z_ls + c);
       }
     }
-    load_vec<Tbc, 2>(C0 + (int64_t)min(t0 + st_s, L - 1) * f.C_ls + st_n, st);
+    st.load(C0 + (int64_t)min(t0 + st_s, L - 1) * f.C_ls + st_n);
+  };
+  auto write_stage = [&](int buf) {
+    float v[2];
+    st.unpack(v);
+    *reinterpret_cast<float2*>(&sC[buf][e0]) = make_float2(v[0], v[1]);
   };
   const int ntiles = (t_end - t_begin + TT - 1) / TT;
   load(t_begin + (ntiles - 1) * TT, cx, cg, cz);
-  *reinterpret_cast<float2*>(&sC[0][e0]) = make_float2(st[0], st[1]);
+  write_stage(0);
   for (int q = 0; q < ntiles; ++q) {
     const int it = ntiles - 1 - q;
     const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
@@ -498,11 +569,11 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
     static_for<G>([&](auto gc) {
       constexpr int g = G - 1 - decltype(gc)::value;
       const bool tv = t0 + g * kPB + j < t_end;
-      float dt = cx[g] + bias;
+      float dt = cvt_raw(cx[g]) + bias;
       if constexpr (SP) dt = softplus_f(dt);
       dt = tv ? dt : 0.f;
-      float dy = cg[g];
-      if (z0) dy *= silu_f(cz[g]);
+      float dy = tv ? cvt_raw(cg[g]) : 0.f;
+      if (has_z) dy *= silu_f(cvt_raw(cz[g]));
       S += dt;
 #pragma unroll
       for (int s = kPB - 1; s >= 0; --s) {
@@ -518,7 +589,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
       __builtin_amdgcn_sched_barrier(0);
     });
     if (it > 0) {
-      *reinterpret_cast<float2*>(&sC[buf ^ 1][e0]) = make_float2(st[0], st[1]);
+      write_stage(buf ^ 1);
 #pragma unroll
       for (int g = 0; g < G; ++g) { cx[g] = nx[g]; cg[g] = ng[g]; cz[g] = nz[g]; }
     }
@@ -558,16 +629,17 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   // per-batch bases (uniform) + 32-bit per-lane offsets (lane j owns steps 4g+j)
   const Tio* __restrict__ u0 = (const Tio*)f.u + (int64_t)b * f.u_bs;
   const Tio* __restrict__ d0 = (const Tio*)f.delta + (int64_t)b * f.delta_bs;
-  const Tio* __restrict__ z0 = f.z ? (const Tio*)f.z + (int64_t)b * f.z_bs : nullptr;
+  const bool has_z = f.z != nullptr;
+  const Tio* __restrict__ z0 = has_z ? (const Tio*)f.z + (int64_t)b * f.z_bs : u0;  // no z: loads ignored
+  const int64_t z_ls = has_z ? f.z_ls : f.u_ls;
   const Tio* __restrict__ g0 = (const Tio*)a.dout + (int64_t)b * a.dout_bs;
   Tio* __restrict__ du0 = (Tio*)a.du + (int64_t)b * a.du_bs;
   Tio* __restrict__ dd0 = (Tio*)a.ddelta + (int64_t)b * a.ddelta_bs;
   Tio* __restrict__ dz0 = a.dz ? (Tio*)a.dz + (int64_t)b * a.dz_bs : nullptr;
   const uint32_t ou = (uint32_t)(j * f.u_ls + c), od = (uint32_t)(j * f.delta_ls + c);
-  const uint32_t oz = (uint32_t)(j * f.z_ls + c), og = (uint32_t)(j * a.dout_ls + c);
+  const uint32_t oz = (uint32_t)(j * z_ls + c), og = (uint32_t)(j * a.dout_ls + c);
   const uint32_t odu = (uint32_t)(j * a.du_ls + c), odd = (uint32_t)(j * a.ddelta_ls + c);
   const uint32_t odz = (uint32_t)(j * a.dz_ls + c);
-  const bool has_z = z0 != nullptr;
   // cooperative B/C staging: 2 values per thread per chunk
   const int e0 = threadIdx.x * 2;
   const int st_s = e0 / (2 * kN), st_col = e0 % (2 * kN);
@@ -593,30 +665,37 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
 #pragma unroll
     for (int i = 0; i < kNSB; ++i) carry[i] = fmaf(__builtin_amdgcn_exp2f(A2[i] * Sk), carry[i], sp[j * kNSB + i]);
   }
+  if (!cvalid) {
+#pragma unroll
+    for (int i = 0; i < kNSB; ++i) carry[i] = 0.f;  // with dy = 0 the lane's adjoint stays 0
+  }
   float dD_acc = 0.f, dbias_acc = 0.f;
 
   // next-chunk prefetch registers (issued one chunk ahead)
-  float n_u[kGB], n_x[kGB], n_z[kGB], n_g[kGB], n_st[2], n_hs[kNSB];
+  using R = raw_t<Tio>;
+  R n_u[kGB], n_x[kGB], n_z[kGB], n_g[kGB];
+  RawVec<Tbc, 2> n_st;
+  float n_hs[kNSB];
+  // steps >= L load a clamped index; their dy is zeroed at use
   auto prefetch = [&](int k) {
     const int t_start = __builtin_amdgcn_readfirstlane(k * kSub);
     const bool full = t_start + kSub <= L;
     const int t = full ? t_start + st_s : min(t_start + st_s, L - 1);
-    load_vec<Tbc, 2>(st0 + (int64_t)t * st_ls + st_n, n_st);
+    n_st.load(st0 + (int64_t)t * st_ls + st_n);
 #pragma unroll
     for (int g = 0; g < kGB; ++g) {
       const int tg = t_start + g * kPB;
       if (full) {
-        n_u[g] = ldf(u0 + (int64_t)tg * f.u_ls + ou);
-        n_x[g] = ldf(d0 + (int64_t)tg * f.delta_ls + od);
-        n_z[g] = has_z ? ldf(z0 + (int64_t)tg * f.z_ls + oz) : 0.f;
-        n_g[g] = ldf(g0 + (int64_t)tg * a.dout_ls + og);
+        n_u[g] = ldr(u0 + (int64_t)tg * f.u_ls + ou);
+        n_x[g] = ldr(d0 + (int64_t)tg * f.delta_ls + od);
+        n_z[g] = ldr(z0 + (int64_t)tg * z_ls + oz);
+        n_g[g] = ldr(g0 + (int64_t)tg * a.dout_ls + og);
       } else {
-        const int ts = tg + j;
-        const int tc = min(ts, L - 1);
-        n_u[g] = ldf(u0 + (int64_t)tc * f.u_ls + c);
-        n_x[g] = ldf(d0 + (int64_t)tc * f.delta_ls + c);
-        n_z[g] = has_z ? ldf(z0 + (int64_t)tc * f.z_ls + c) : 0.f;
-        n_g[g] = ts < L ? ldf(g0 + (int64_t)tc * a.dout_ls + c) : 0.f;
+        const int tc = min(tg + j, L - 1);
+        n_u[g] = ldr(u0 + (int64_t)tc * f.u_ls + c);
+        n_x[g] = ldr(d0 + (int64_t)tc * f.delta_ls + c);
+        n_z[g] = ldr(z0 + (int64_t)tc * z_ls + c);
+        n_g[g] = ldr(g0 + (int64_t)tc * a.dout_ls + c);
       }
     }
     load_vec<float, kNSB>(f.ckpt + (((int64_t)b * nck + k) * f.dim + c) * kN + j * kNSB, n_hs);
@@ -626,10 +705,20 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   for (int k = ck_end - 1; k >= ck_begin; --k) {
     const int t_start = __builtin_amdgcn_readfirstlane(k * kSub);
     const bool full = t_start + kSub <= L;
-    *reinterpret_cast<float2*>(&sBC[e0]) = make_float2(n_st[0], n_st[1]);
+    {
+      float v[2];
+      n_st.unpack(v);
+      *reinterpret_cast<float2*>(&sBC[e0]) = make_float2(v[0], v[1]);
+    }
     float uu[kGB], xr[kGB], dt[kGB], zz[kGB], go[kGB], hs[kNSB];
 #pragma unroll
-    for (int g = 0; g < kGB; ++g) { uu[g] = n_u[g]; xr[g] = n_x[g] + bias; zz[g] = n_z[g]; go[g] = n_g[g]; }
+    for (int g = 0; g < kGB; ++g) {
+      uu[g] = cvt_raw(n_u[g]);
+      xr[g] = cvt_raw(n_x[g]) + bias;
+      zz[g] = cvt_raw(n_z[g]);
+      // padded steps (>= L) and lanes past `dim` contribute nothing
+      go[g] = (cvalid && (full || t_start + g * kPB + j < L)) ? cvt_raw(n_g[g]) : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < kNSB; ++i) hs[i] = n_hs[i];
     if (k - 1 >= ck_begin) prefetch(k - 1);
@@ -707,23 +796,25 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
           ddtA = fmaf(An[i], t1, ddtA);
           dus = fmaf(dh, Bv[i], dus);
           dA_acc[i] = fmaf(t1, dts, dA_acc[i]);
-          vals[i] = cvalid ? dh * dtus : 0.f;            // dB contribution
-          vals[4 + i] = cvalid ? dys * hh[tl][i] : 0.f;  // dC contribution
+          vals[i] = dh * dtus;            // dB contribution (0 on lanes past `dim`)
+          vals[4 + i] = dys * hh[tl][i];  // dC contribution
           carry[i] = e * dh;
         }
         ddt_p[s] = ddtA;   // + u_s * dus_s, added after the reduce (u is per step)
         du_p[s] = dus;
         // sum the 8 values over the wave's 16 channels (lane bits 2..5):
-        // lane keeps kind = bit2, i = (bit3 << 1) | bit4
-        const bool q2 = lane & 4, q3 = lane & 8, q4 = lane & 16;
+        // bit5 <- kind (permlane32 swap), bit4 <- i>>1 (permlane16 swap),
+        // bit3 <- i&1 (DPP), bit2 all-reduced; no selects in the swap stages
         float a4[4], a2[2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a4[q] = (q2 ? vals[4 + q] : vals[q]) + xor4(q2 ? vals[q] : vals[4 + q], lane);
+        for (int q = 0; q < 4; ++q) a4[q] = rs_swap32(vals[q], vals[4 + q]);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) a2[q] = (q3 ? a4[2 + q] : a4[q]) + xor8(q3 ? a4[q] : a4[2 + q]);
-        float a1 = (q4 ? a2[1] : a2[0]) + xor16(q4 ? a2[0] : a2[1], lane);
-        a1 = sum_xor32(a1);
-        if (lane < 32) red[wave][(tl * 2 + (q2 ? 1 : 0)) * kN + j * kNSB + ((q3 ? 2 : 0) | (q4 ? 1 : 0))] = a1;
+        for (int q = 0; q < 2; ++q) a2[q] = rs_swap16(a4[q], a4[q + 2]);
+        const bool q3 = lane & 8;
+        float a1 = (q3 ? a2[1] : a2[0]) + xor8(q3 ? a2[0] : a2[1]);
+        a1 += xor4(a1, lane);
+        if (!(lane & 4))
+          red[wave][(tl * 2 + (lane >> 5)) * kN + j * kNSB + (((lane >> 4) & 1) << 1) + ((lane >> 3) & 1)] = a1;
       }
       // per-channel results for lane j's timestep: ddt = sum_n A t1 + u * sum_n dh B
       const float dus_j = group_reduce_scatter<kPB>(du_p, j);
@@ -734,11 +825,12 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       float ddr = ddt_j;
       if constexpr (SP) ddr *= softplus_grad(xr[g]);
       if (tv) dbias_acc += ddr;
-      if (full) {
+      // lanes past `dim` computed zeros for channel dim-1: they must not store
+      if (full && cvalid) {
         stf(du0 + (int64_t)tg * a.du_ls + odu, du_j);
         stf(dd0 + (int64_t)tg * a.ddelta_ls + odd, ddr);
         if (has_z) stf(dz0 + (int64_t)tg * a.dz_ls + odz, dzv);
-      } else if (tv) {
+      } else if (tv && cvalid) {
         stf(du0 + (int64_t)(tg + j) * a.du_ls + c, du_j);
         stf(dd0 + (int64_t)(tg + j) * a.ddelta_ls + c, ddr);
         if (has_z) stf(dz0 + (int64_t)(tg + j) * a.dz_ls + c, dzv);

@@ -1,0 +1,10 @@
+#!/bin/bash
+# scan kernels after the raw-prefetch / swap-reduce change: parity, sweep, C2 step
+mkdir -p gpurun_out/scan2
+timeout -k 10 600 python -m pytest tests/test_gpu_ops.py tests/test_gpu_modules.py -x -q > gpurun_out/scan2/tests.log 2>&1; rc=$?
+tail -5 gpurun_out/scan2/tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/bench_scan.py > gpurun_out/scan2/bench_scan.log 2>&1 || exit 1
+cat gpurun_out/scan2/bench_scan.log
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --decode-steps 0 --cpu-budget 0 > gpurun_out/scan2/bench.log 2>&1 || exit 1
+grep "\[bench\]" gpurun_out/scan2/bench.log
