@@ -85,9 +85,9 @@ def train_bench(args, rank, world, dev):
         loss = torch.nn.functional.cross_entropy(logits.float().view(-1, c["vocab"]), tokens.view(-1),
                                                  ignore_index=0)
         if dp is not None:
-            dp.zero_grad()
+            dp.zero_grad()         # grads are views into the flat all-reduce buffer
         else:
-            opt.zero_grad(set_to_none=False)
+            opt.zero_grad(set_to_none=True)
         loss.backward()
         if dp is not None:
             dp.finish()

@@ -65,7 +65,7 @@ typedef struct {
   int batch, dim, seqlen, dstate;
   int dtype_io, dtype_bc;
   int delta_softplus;
-  int ckpt_chunk;                 /* >0 iff ckpt != NULL; multiple of 16 */
+  int ckpt_chunk;                 /* 16 iff ckpt != NULL (the backward chunk) */
   int64_t u_bs, u_ls;             /* element strides (batch, time)       */
   int64_t delta_bs, delta_ls;
   int64_t z_bs, z_ls;

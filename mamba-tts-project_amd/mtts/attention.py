@@ -17,7 +17,49 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import attn_kernels
-from .linear import cast_scope, linear
+from .linear import cast_scope, cast_weight, colsum, linear, wgrad
+
+
+class InProjFn(torch.autograd.Function):
+    """q = query W[:d]^T + b[:d] and kv = key W[d:]^T + b[d:] (key is value):
+    the packed in-projection of nn.MultiheadAttention
+    (F.multi_head_attention_forward's _in_projection_packed).  The backward
+    writes the full (3d, d) weight / (3d) bias gradients in place, slice by
+    slice (no zero-padded per-slice gradients to add up)."""
+
+    @staticmethod
+    def forward(ctx, query, key, weight, bias):
+        cd = query.dtype
+        d = query.shape[-1]
+        Wc, bc = cast_weight(weight, cd), cast_weight(bias, cd)
+        x2, k2 = query.reshape(-1, d), key.reshape(-1, d)
+        q = torch.addmm(bc[:d], x2, Wc[:d].t())
+        kv = torch.addmm(bc[d:], k2, Wc[d:].t())
+        ctx.save_for_backward(x2, k2, Wc)
+        ctx.meta = (query.shape, key.shape, weight.dtype, bias.dtype)
+        return q.view(*query.shape[:-1], d), kv.view(*key.shape[:-1], 2 * d)
+
+    @staticmethod
+    def backward(ctx, dq, dkv):
+        x2, k2, Wc = ctx.saved_tensors
+        qshape, kshape, wdt, bdt = ctx.meta
+        d = x2.shape[1]
+        dq2 = dq.reshape(-1, d).to(Wc.dtype)
+        dkv2 = dkv.reshape(-1, 2 * d).to(Wc.dtype)
+        dquery = (dq2 @ Wc[:d]).view(qshape) if ctx.needs_input_grad[0] else None
+        dkey = (dkv2 @ Wc[d:]).view(kshape) if ctx.needs_input_grad[1] else None
+        dW = db = None
+        if ctx.needs_input_grad[2]:
+            dW = torch.empty(3 * d, d, device=x2.device, dtype=torch.float32)
+            wgrad(dq2, x2, out=dW[:d])
+            wgrad(dkv2, k2, out=dW[d:])
+            dW = dW.to(wdt)
+        if ctx.needs_input_grad[3]:
+            db = torch.empty(3 * d, device=x2.device, dtype=torch.float32)
+            colsum(dq2, out=db[:d])
+            colsum(dkv2, out=db[d:])
+            db = db.to(bdt)
+        return dquery, dkey, dW, db
 
 
 class CrossAttention(nn.Module):
@@ -47,12 +89,12 @@ class CrossAttention(nn.Module):
         cd = query.dtype
         d, H = self.embed_dim, self.num_heads
         W, b = self.in_proj_weight, self.in_proj_bias
-        q = linear(query, W, b, rows=(0, d))
         p_drop = self.dropout if self.training else 0.0
         if key is value:
-            kv = linear(key.to(cd), W, b, rows=(d, 3 * d))
+            q, kv = InProjFn.apply(query, key.to(cd), W, b)
             o = attn_kernels.attention_kv(q, kv, H, key_padding_mask, p_drop)
         else:
+            q = linear(query, W, b, rows=(0, d))
             k = linear(key.to(cd), W, b, rows=(d, 2 * d))
             v = linear(value.to(cd), W, b, rows=(2 * d, 3 * d))
             o = attn_kernels.attention(q, k, v, H, key_padding_mask, p_drop)

@@ -31,6 +31,8 @@
 namespace mtts {
 
 constexpr int kN = 16;       // d_state
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int kSub = 16;     // checkpoint chunk (timesteps)
 constexpr int kBlock = 256;  // threads per block
 
@@ -313,8 +315,10 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
     static_for<G>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
       const int tg = t0 + g * P;
-      if (nck && (tg % a.ckpt_chunk) == 0 && (!TAIL || tg < t_end))
-        store_vec<NS>(ck0 + (int64_t)(tg / a.ckpt_chunk) * a.dim * kN + lck, h);
+      // checkpoints every kSub steps; tiles start at multiples of kSub
+      if constexpr ((g * P) % kSub == 0) {
+        if (nck && (!TAIL || tg < t_end)) store_vec<NS>(ck0 + (int64_t)(tg / kSub) * a.dim * kN + lck, h);
+      }
       const bool tv = !TAIL || (tg + j < t_end);
       float dt = cvt_raw(cd[g]) + bias;
       if constexpr (SP) dt = softplus_f(dt);
@@ -335,25 +339,33 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
           dtus = s == 0 ? group_bcast<4, 0>(dtu) : s == 1 ? group_bcast<4, 1>(dtu)
                : s == 2 ? group_bcast<4, 2>(dtu) : group_bcast<4, 3>(dtu);
         }
+        // one broadcast per step into a register (not a DPP operand per use),
+        // so the state math below can use packed f32 instructions
+        asm volatile("" : "+v"(dts), "+v"(dtus));
+        const f2 dts2 = {dts, dts}, dtus2 = {dtus, dtus};
         const float* bc = &sBC[buf][(g * P + s) * 2 * kN];
-        float Bv[NS], Cv[NS];
+        f2 y2 = {0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < NS / 4; ++q) {
-          const float4 vb = *reinterpret_cast<const float4*>(bc + j * NS + 4 * q);
-          Bv[4 * q] = vb.x; Bv[4 * q + 1] = vb.y; Bv[4 * q + 2] = vb.z; Bv[4 * q + 3] = vb.w;
-          if constexpr (MODE == kFull) {
-            const float4 vc = *reinterpret_cast<const float4*>(bc + kN + j * NS + 4 * q);
-            Cv[4 * q] = vc.x; Cv[4 * q + 1] = vc.y; Cv[4 * q + 2] = vc.z; Cv[4 * q + 3] = vc.w;
+          const f4 vb = *reinterpret_cast<const f4*>(bc + j * NS + 4 * q);
+          f4 vc = {};
+          if constexpr (MODE == kFull) vc = *reinterpret_cast<const f4*>(bc + kN + j * NS + 4 * q);
+#pragma unroll
+          for (int p2 = 0; p2 < 2; ++p2) {
+            const int i = 4 * q + 2 * p2;
+            const f2 x = dts2 * f2{A2[i], A2[i + 1]};
+            const f2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+            const f2 bv = p2 ? f2{vb[2], vb[3]} : f2{vb[0], vb[1]};
+            const f2 hn = __builtin_elementwise_fma(e, f2{h[i], h[i + 1]}, dtus2 * bv);
+            h[i] = hn[0];
+            h[i + 1] = hn[1];
+            if constexpr (MODE == kFull) {
+              const f2 cv = p2 ? f2{vc[2], vc[3]} : f2{vc[0], vc[1]};
+              y2 = __builtin_elementwise_fma(cv, hn, y2);
+            }
           }
         }
-        float y = 0.f;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-          const float e = __builtin_amdgcn_exp2f(dts * A2[i]);
-          h[i] = fmaf(e, h[i], dtus * Bv[i]);
-          if constexpr (MODE == kFull) y = fmaf(Cv[i], h[i], y);
-        }
-        yp[s] = y;
+        yp[s] = y2[0] + y2[1];
       }
       if constexpr (MODE == kFull) {
         float y = group_reduce_scatter<P>(yp, j);
@@ -522,12 +534,11 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   const Tbc* __restrict__ C0 = (const Tbc*)f.Cm + (int64_t)b * f.C_bs;
   const int e0 = threadIdx.x * 2;          // staged C values of this thread: step e0/16, state e0%16
   const int st_s = e0 / kN, st_n = e0 % kN;
-  float A2[kNSB], carry[kNSB];
+  float A2[kNSB];
 #pragma unroll
-  for (int i = 0; i < kNSB; ++i) {
-    A2[i] = f.A[(int64_t)c * kN + j * kNSB + i] * kLog2e;
-    carry[i] = 0.f;
-  }
+  for (int i = 0; i < kNSB; ++i) A2[i] = f.A[(int64_t)c * kN + j * kNSB + i] * kLog2e;
+  const f2 A2v[2] = {f2{A2[0], A2[1]}, f2{A2[2], A2[3]}};
+  f2 carry2[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
   const float bias = f.delta_bias ? f.delta_bias[c] : 0.f;
   float S = 0.f;
   using R = raw_t<Tio>;
@@ -577,15 +588,20 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
       S += dt;
 #pragma unroll
       for (int s = kPB - 1; s >= 0; --s) {
-        const float dts = s == 0 ? bcast4<0>(dt) : s == 1 ? bcast4<1>(dt) : s == 2 ? bcast4<2>(dt) : bcast4<3>(dt);
-        const float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
-        const float4 Cq = *reinterpret_cast<const float4*>(&sC[buf][(g * kPB + s) * kN + j * kNSB]);
-        const float Cv[kNSB] = {Cq.x, Cq.y, Cq.z, Cq.w};
+        float dts = s == 0 ? bcast4<0>(dt) : s == 1 ? bcast4<1>(dt) : s == 2 ? bcast4<2>(dt) : bcast4<3>(dt);
+        float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
+        asm volatile("" : "+v"(dts), "+v"(dys));
+        const f4 Cq = *reinterpret_cast<const f4*>(&sC[buf][(g * kPB + s) * kN + j * kNSB]);
 #pragma unroll
-        for (int i = 0; i < kNSB; ++i) carry[i] = __builtin_amdgcn_exp2f(dts * A2[i]) * fmaf(dys, Cv[i], carry[i]);
+        for (int p = 0; p < 2; ++p) {
+          const f2 x = f2{dts, dts} * A2v[p];
+          const f2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+          const f2 cv = p ? f2{Cq[2], Cq[3]} : f2{Cq[0], Cq[1]};
+          carry2[p] = e * __builtin_elementwise_fma(f2{dys, dys}, cv, carry2[p]);
+        }
       }
 #pragma unroll
-      for (int i = 0; i < kNSB; ++i) asm volatile("" : "+v"(carry[i]));
+      for (int p = 0; p < 2; ++p) asm volatile("" : "+v"(carry2[p]));
       __builtin_amdgcn_sched_barrier(0);
     });
     if (it > 0) {
@@ -598,7 +614,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   if (cvalid) {
     float* sp = seg + (((int64_t)b * K + k) * f.dim + c) * (kN + 1);
 #pragma unroll
-    for (int i = 0; i < kNSB; ++i) sp[j * kNSB + i] = carry[i];
+    for (int i = 0; i < kNSB; ++i) sp[j * kNSB + i] = carry2[i >> 1][i & 1];
     if (j == 0) sp[kN] = S;
   }
 }
@@ -653,12 +669,14 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
     An[i] = f.A[(int64_t)c * kN + j * kNSB + i];
     A2[i] = An[i] * kLog2e;
   }
+  const f2 Anv[2] = {f2{An[0], An[1]}, f2{An[2], An[3]}};
+  const f2 A2v[2] = {f2{A2[0], A2[1]}, f2{A2[2], A2[3]}};
   const float Dc = f.D ? f.D[c] : 0.f;
   const float bias = f.delta_bias ? f.delta_bias[c] : 0.f;
 
-  float carry[kNSB], dA_acc[kNSB];
+  float carry[kNSB];
 #pragma unroll
-  for (int i = 0; i < kNSB; ++i) { carry[i] = 0.f; dA_acc[i] = 0.f; }
+  for (int i = 0; i < kNSB; ++i) carry[i] = 0.f;
   for (int kk = K - 1; kk > kseg; --kk) {  // carry entering from later segments (pass 1)
     const float* sp = seg + (((int64_t)b * K + kk) * f.dim + c) * (kN + 1);
     const float Sk = sp[kN];
@@ -669,6 +687,8 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
 #pragma unroll
     for (int i = 0; i < kNSB; ++i) carry[i] = 0.f;  // with dy = 0 the lane's adjoint stays 0
   }
+  f2 carry2[2] = {f2{carry[0], carry[1]}, f2{carry[2], carry[3]}};
+  f2 dA2[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
   float dD_acc = 0.f, dbias_acc = 0.f;
 
   // next-chunk prefetch registers (issued one chunk ahead)
@@ -730,25 +750,27 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
     }
     __syncthreads();
 
-    // ---- replay the chunk forward: h history in registers
-    float hh[kSub][kNSB];
+    // ---- replay the chunk forward: h history in registers (state pairs, packed f32)
+    f2 hh[kSub][2];
+    const f2 hs2[2] = {f2{hs[0], hs[1]}, f2{hs[2], hs[3]}};
     {
-      float h[kNSB];
-#pragma unroll
-      for (int i = 0; i < kNSB; ++i) h[i] = hs[i];
+      f2 h2[2] = {hs2[0], hs2[1]};
 #pragma unroll
       for (int g = 0; g < kGB; ++g) {
         const float dtu = dt[g] * uu[g];
 #pragma unroll
         for (int s = 0; s < kPB; ++s) {
-          const float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
-          const float dtus = s == 0 ? bcast4<0>(dtu) : s == 1 ? bcast4<1>(dtu) : s == 2 ? bcast4<2>(dtu) : bcast4<3>(dtu);
-          const float4 Bq = *reinterpret_cast<const float4*>(&sBC[(g * kPB + s) * 2 * kN + j * kNSB]);
-          const float Bv[kNSB] = {Bq.x, Bq.y, Bq.z, Bq.w};
+          float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
+          float dtus = s == 0 ? bcast4<0>(dtu) : s == 1 ? bcast4<1>(dtu) : s == 2 ? bcast4<2>(dtu) : bcast4<3>(dtu);
+          asm volatile("" : "+v"(dts), "+v"(dtus));
+          const f4 Bq = *reinterpret_cast<const f4*>(&sBC[(g * kPB + s) * 2 * kN + j * kNSB]);
 #pragma unroll
-          for (int i = 0; i < kNSB; ++i) {
-            h[i] = fmaf(__builtin_amdgcn_exp2f(dts * A2[i]), h[i], dtus * Bv[i]);
-            hh[g * kPB + s][i] = h[i];
+          for (int p = 0; p < 2; ++p) {
+            const f2 x = f2{dts, dts} * A2v[p];
+            const f2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+            const f2 bv = p ? f2{Bq[2], Bq[3]} : f2{Bq[0], Bq[1]};
+            h2[p] = __builtin_elementwise_fma(e, h2[p], f2{dtus, dtus} * bv);
+            hh[g * kPB + s][p] = h2[p];
           }
         }
       }
@@ -760,9 +782,9 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       float yp[kPB];
 #pragma unroll
       for (int s = 0; s < kPB; ++s) {
-        const float4 Cq = *reinterpret_cast<const float4*>(&sBC[(g * kPB + s) * 2 * kN + kN + j * kNSB]);
-        yp[s] = fmaf(Cq.x, hh[g * kPB + s][0], fmaf(Cq.y, hh[g * kPB + s][1],
-                fmaf(Cq.z, hh[g * kPB + s][2], Cq.w * hh[g * kPB + s][3])));
+        const f4 Cq = *reinterpret_cast<const f4*>(&sBC[(g * kPB + s) * 2 * kN + kN + j * kNSB]);
+        const f2 y2 = __builtin_elementwise_fma(f2{Cq[0], Cq[1]}, hh[g * kPB + s][0], f2{Cq[2], Cq[3]} * hh[g * kPB + s][1]);
+        yp[s] = y2[0] + y2[1];
       }
       const float y = fmaf(Dc, uu[g], group_reduce_scatter<kPB>(yp, j));  // pre-gate output, lane j's step
       float dy = go[g], dzv = 0.f;
@@ -777,31 +799,34 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       float ddt_p[kPB], du_p[kPB];
 #pragma unroll
       for (int s = kPB - 1; s >= 0; --s) {
-        float vals[8];  // [kind][i]: dB_i, dC_i of this step
-        const float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
-        const float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
-        const float dtus = s == 0 ? bcast4<0>(dtu_g) : s == 1 ? bcast4<1>(dtu_g) : s == 2 ? bcast4<2>(dtu_g) : bcast4<3>(dtu_g);
+        float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
+        float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
+        float dtus = s == 0 ? bcast4<0>(dtu_g) : s == 1 ? bcast4<1>(dtu_g) : s == 2 ? bcast4<2>(dtu_g) : bcast4<3>(dtu_g);
+        asm volatile("" : "+v"(dys), "+v"(dts), "+v"(dtus));
+        const f2 dys2 = {dys, dys}, dts2 = {dts, dts}, dtus2 = {dtus, dtus};
         const int tl = g * kPB + s;
-        const float4 Bq = *reinterpret_cast<const float4*>(&sBC[tl * 2 * kN + j * kNSB]);
-        const float4 Cq = *reinterpret_cast<const float4*>(&sBC[tl * 2 * kN + kN + j * kNSB]);
-        const float Bv[kNSB] = {Bq.x, Bq.y, Bq.z, Bq.w};
-        const float Cv[kNSB] = {Cq.x, Cq.y, Cq.z, Cq.w};
-        float ddtA = 0.f, dus = 0.f;
+        const f4 Bq = *reinterpret_cast<const f4*>(&sBC[tl * 2 * kN + j * kNSB]);
+        const f4 Cq = *reinterpret_cast<const f4*>(&sBC[tl * 2 * kN + kN + j * kNSB]);
+        f2 ddtA = {0.f, 0.f}, dus = {0.f, 0.f}, vB[2], vC[2];
 #pragma unroll
-        for (int i = 0; i < kNSB; ++i) {
-          const float dh = fmaf(dys, Cv[i], carry[i]);
-          const float hp = tl > 0 ? hh[tl > 0 ? tl - 1 : 0][i] : hs[i];
-          const float e = __builtin_amdgcn_exp2f(dts * A2[i]);
-          const float t1 = dh * e * hp;
-          ddtA = fmaf(An[i], t1, ddtA);
-          dus = fmaf(dh, Bv[i], dus);
-          dA_acc[i] = fmaf(t1, dts, dA_acc[i]);
-          vals[i] = dh * dtus;            // dB contribution (0 on lanes past `dim`)
-          vals[4 + i] = dys * hh[tl][i];  // dC contribution
-          carry[i] = e * dh;
+        for (int p = 0; p < 2; ++p) {
+          const f2 bv = p ? f2{Bq[2], Bq[3]} : f2{Bq[0], Bq[1]};
+          const f2 cv = p ? f2{Cq[2], Cq[3]} : f2{Cq[0], Cq[1]};
+          const f2 dh = __builtin_elementwise_fma(dys2, cv, carry2[p]);
+          const f2 hp = tl > 0 ? hh[tl > 0 ? tl - 1 : 0][p] : hs2[p];
+          const f2 x = dts2 * A2v[p];
+          const f2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+          const f2 t1 = dh * e * hp;
+          ddtA = __builtin_elementwise_fma(Anv[p], t1, ddtA);
+          dus = __builtin_elementwise_fma(dh, bv, dus);
+          dA2[p] = __builtin_elementwise_fma(t1, dts2, dA2[p]);
+          vB[p] = dh * dtus2;           // dB contribution (0 on lanes past `dim`)
+          vC[p] = dys2 * hh[tl][p];     // dC contribution
+          carry2[p] = e * dh;
         }
-        ddt_p[s] = ddtA;   // + u_s * dus_s, added after the reduce (u is per step)
-        du_p[s] = dus;
+        ddt_p[s] = ddtA[0] + ddtA[1];   // + u_s * dus_s, added after the reduce (u is per step)
+        du_p[s] = dus[0] + dus[1];
+        const float vals[8] = {vB[0][0], vB[0][1], vB[1][0], vB[1][1], vC[0][0], vC[0][1], vC[1][0], vC[1][1]};
         // sum the 8 values over the wave's 16 channels (lane bits 2..5):
         // bit5 <- kind (permlane32 swap), bit4 <- i>>1 (permlane16 swap),
         // bit3 <- i&1 (DPP), bit2 all-reduced; no selects in the swap stages
@@ -852,11 +877,11 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   if (cvalid) {
     float* pp = par + (((int64_t)b * K + kseg) * f.dim + c) * (kN + 2);
 #pragma unroll
-    for (int i = 0; i < kNSB; ++i) pp[j * kNSB + i] = dA_acc[i];
+    for (int i = 0; i < kNSB; ++i) pp[j * kNSB + i] = dA2[i >> 1][i & 1];
     if (j == 0) { pp[kN] = dD_acc; pp[kN + 1] = dbias_acc; }
     if (a.dh0 && kseg == 0) {
 #pragma unroll
-      for (int i = 0; i < kNSB; ++i) a.dh0[((int64_t)b * f.dim + c) * kN + j * kNSB + i] = carry[i];
+      for (int i = 0; i < kNSB; ++i) a.dh0[((int64_t)b * f.dim + c) * kN + j * kNSB + i] = carry2[i >> 1][i & 1];
     }
   }
 }
@@ -906,7 +931,7 @@ static int check_fwd(const MttsScanFwdArgs* a) {
   MTTS_CHECK(((uintptr_t)a->Bm % 16 == 0) && ((uintptr_t)a->Cm % 16 == 0) && (a->B_ls * esz) % 16 == 0 &&
                  (a->C_ls * esz) % 16 == 0 && (a->B_bs * esz) % 16 == 0 && (a->C_bs * esz) % 16 == 0,
              "scan: B/C rows must be 16-byte aligned");
-  if (a->ckpt) MTTS_CHECK(a->ckpt_chunk > 0 && a->ckpt_chunk % 4 == 0, "scan: ckpt_chunk %% 4 != 0");
+  if (a->ckpt) MTTS_CHECK(a->ckpt_chunk == kSub, "scan: ckpt_chunk must be %d", kSub);
   return MTTS_OK;
 }
 

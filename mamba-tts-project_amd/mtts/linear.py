@@ -71,12 +71,14 @@ def cast_weight(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return t
 
 
-def colsum(x2d: torch.Tensor) -> torch.Tensor:
-    """fp32 column sums of a (rows, cols) tensor with unit column stride."""
+def colsum(x2d: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """fp32 column sums of a (rows, cols) tensor with unit column stride
+    (into `out`, a contiguous fp32 vector, when given)."""
     if x2d.stride(-1) != 1:
         x2d = x2d.contiguous()
     rows, cols = x2d.shape
-    out = torch.empty(cols, device=x2d.device, dtype=torch.float32)
+    if out is None:
+        out = torch.empty(cols, device=x2d.device, dtype=torch.float32)
     rpg = max(rows, 1)
     wsz = L.lib().mtts_colsum_workspace(rows, cols, rpg)
     ws = torch.empty(wsz, device=x2d.device, dtype=torch.uint8) if wsz > 0 else None
@@ -85,17 +87,22 @@ def colsum(x2d: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4) -> torch.Tensor:
-    """dW = dy^T @ x in fp32; dy (M, n), x (M, k) with the same dtype."""
+def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4, out: torch.Tensor = None) -> torch.Tensor:
+    """dW = dy^T @ x in fp32; dy (M, n), x (M, k) with the same dtype.
+    `out` (n, k) fp32, possibly a row slice of a larger gradient, receives it."""
     M = dy.shape[0]
     if dy.dtype == torch.float32:
-        return dy.t() @ x
+        return torch.mm(dy.t(), x, out=out) if out is not None else dy.t() @ x
     if splits > 1 and M % splits == 0 and M >= 2048:
         m = M // splits
         part = torch.bmm(dy.reshape(splits, m, -1).transpose(1, 2), x.reshape(splits, m, -1),
                          out_dtype=torch.float32)
-        return part.sum(0)
-    return torch.mm(dy.t(), x, out_dtype=torch.float32)
+        return torch.sum(part, 0, out=out) if out is not None else part.sum(0)
+    r = torch.mm(dy.t(), x, out_dtype=torch.float32)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
 
 
 class LinearFn(torch.autograd.Function):

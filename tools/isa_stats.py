@@ -48,7 +48,7 @@ def main():
         blocks, cur, label = [], collections.Counter(), "entry"
         tot = collections.Counter()
         for line in body.splitlines():
-            l = line.strip()
+            l = line.split(";")[0].strip()
             if l.endswith(":") and not l.startswith(";"):
                 blocks.append((label, cur))
                 cur, label = collections.Counter(), l[:-1]
