@@ -169,11 +169,13 @@ __device__ __forceinline__ raw_t<T> ldr(const T* p) { return (raw_t<T>)*p; }
 // N consecutive elements as raw 32-bit words (one vector load), unpacked at use
 template <typename T, int N>
 struct RawVec {
-  static constexpr int W = N * (int)sizeof(T) / 4;
+  static constexpr int W = (N * (int)sizeof(T) + 3) / 4;
   static_assert(W == 1 || W == 2 || W == 4 || W == 8, "RawVec width");
   uint32_t w[W];
   __device__ __forceinline__ void load(const T* p) {
-    if constexpr (W == 1) {
+    if constexpr (N * sizeof(T) == 2) {
+      w[0] = (uint32_t)*p;  // one bf16
+    } else if constexpr (W == 1) {
       w[0] = *reinterpret_cast<const uint32_t*>(p);
     } else if constexpr (W == 2) {
       const uint2 v = *reinterpret_cast<const uint2*>(p);
@@ -187,7 +189,9 @@ struct RawVec {
     }
   }
   __device__ __forceinline__ void unpack(float (&o)[N]) const {
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (N * sizeof(T) == 2) {
+      o[0] = __uint_as_float(w[0] << 16);
+    } else if constexpr (sizeof(T) == 4) {
 #pragma unroll
       for (int i = 0; i < N; ++i) o[i] = __uint_as_float(w[i]);
     } else {
@@ -206,13 +210,17 @@ struct RawVec {
 // (fp32); u/delta/z of the next tile are prefetched into registers while the
 // current tile computes.
 enum { kFull = 0, kState = 1 };
-constexpr int kTileG = 8;   // P-step groups per tile
+constexpr int kTileG = 8;   // P-step groups per tile (carry kernel)
+constexpr int kTileGF = 4;  // forward: groups per tile (kRing register sets live)
+constexpr int kRing = 3;    // forward: register sets in the prefetch ring
+using TrueT = std::integral_constant<bool, true>;
+using FalseT = std::integral_constant<bool, false>;
 
 template <int P, typename Tio, typename Tbc, int MODE, bool SP>
 __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdArgs a, const int seg_len,
                                                              float* __restrict__ seg) {
   constexpr int NS = kN / P;
-  constexpr int G = kTileG;
+  constexpr int G = kTileGF;
   constexpr int TT = G * P;                       // timesteps per tile
   constexpr int VPT = TT * 2 * kN / kBlock;       // staged B/C values per thread (= P)
   __shared__ __attribute__((aligned(16))) float sBC[2][TT * 2 * kN];
@@ -271,38 +279,49 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
   const uint32_t lck = (uint32_t)(c * kN + j * NS);
 
   using R = raw_t<Tio>;
-  R cu[G], cd[G], cz[G], nu[G], nd[G], nz[G];
-  RawVec<Tbc, VPT> stv;
+  // one tile's inputs, raw; two sets (A/B) ping-pong so the loads for tile
+  // i+1 are in flight during tile i with no register copies between them
+  struct TileRegs {
+    R u[G], d[G], z[G];
+    RawVec<Tbc, VPT> st;
+  };
+  float diag_sink = 0.f;
   // TAIL: some timesteps of the tile are >= t_end -> clamp to the last valid one
-  auto load_regs = [&](auto tail, int t0, R (&uu)[G], R (&dd)[G], R (&zz)[G]) {
+  auto load_tile = [&](auto tail, int t0, TileRegs& X) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail)::value;
+    if constexpr (TAIL) {
+      X.st.load(st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN));
+    } else {
+      X.st.load(st0 + (int64_t)t0 * st_ls + lst);
+    }
+#ifdef MTTS_DIAG_NOMEM
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      X.u[g] = (R)(0x3f80u + (uint32_t)(t0 & 7) + g);
+      X.d[g] = (R)(0xbf00u + (uint32_t)g);
+      X.z[g] = (R)(0x3f00u + (uint32_t)g);
+    }
+    return;
+#endif
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int tg = t0 + g * P;
       if constexpr (TAIL) {
         const int ts = min(tg + j, L - 1);
-        uu[g] = ldr(u0 + (int64_t)ts * a.u_ls + c);
-        dd[g] = ldr(d0 + (int64_t)ts * a.delta_ls + c);
-        if constexpr (MODE == kFull) zz[g] = ldr(z0 + (int64_t)ts * z_ls + c);
+        X.u[g] = ldr(u0 + (int64_t)ts * a.u_ls + c);
+        X.d[g] = ldr(d0 + (int64_t)ts * a.delta_ls + c);
+        if constexpr (MODE == kFull) X.z[g] = ldr(z0 + (int64_t)ts * z_ls + c);
       } else {
-        uu[g] = ldr(u0 + (int64_t)tg * a.u_ls + lu);
-        dd[g] = ldr(d0 + (int64_t)tg * a.delta_ls + ld);
-        if constexpr (MODE == kFull) zz[g] = ldr(z0 + (int64_t)tg * z_ls + lz);
+        X.u[g] = ldr(u0 + (int64_t)tg * a.u_ls + lu);
+        X.d[g] = ldr(d0 + (int64_t)tg * a.delta_ls + ld);
+        if constexpr (MODE == kFull) X.z[g] = ldr(z0 + (int64_t)tg * z_ls + lz);
         static_assert(sizeof(lu) == 4, "32-bit lane offsets -> saddr loads");
       }
     }
   };
-  auto load_stage = [&](auto tail, int t0) {
-    constexpr bool TAIL = decltype(tail)::value;
-    if constexpr (TAIL) {
-      stv.load(st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN));
-    } else {
-      stv.load(st0 + (int64_t)t0 * st_ls + lst);
-    }
-  };
-  auto write_stage = [&](int buf) {
+  auto write_stage = [&](int buf, const TileRegs& X) __attribute__((always_inline)) {
     float v[VPT];
-    stv.unpack(v);
+    X.st.unpack(v);
     if constexpr (VPT == 4) {
       *reinterpret_cast<float4*>(&sBC[buf][e0]) = make_float4(v[0], v[1], v[2], v[3]);
     } else {
@@ -310,22 +329,34 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
       for (int q = 0; q < VPT; ++q) sBC[buf][e0 + q] = v[q];
     }
   };
-  auto compute_tile = [&](auto tail, int t0, int buf) {
+  auto compute_tile = [&](auto tail, int t0, int buf, const TileRegs& X) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail)::value;
     static_for<G>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
       const int tg = t0 + g * P;
-      // checkpoints every kSub steps; tiles start at multiples of kSub
-      if constexpr ((g * P) % kSub == 0) {
-        if (nck && (!TAIL || tg < t_end)) store_vec<NS>(ck0 + (int64_t)(tg / kSub) * a.dim * kN + lck, h);
+      // checkpoints every kSub steps (tg is wave-uniform: scalar test)
+      if constexpr ((TT % kSub) != 0 || (g * P) % kSub == 0) {
+        if (nck && (tg & (kSub - 1)) == 0 && (!TAIL || tg < t_end))
+          store_vec<NS>(ck0 + (int64_t)(tg / kSub) * a.dim * kN + lck, h);
       }
       const bool tv = !TAIL || (tg + j < t_end);
-      float dt = cvt_raw(cd[g]) + bias;
+      float dt = cvt_raw(X.d[g]) + bias;
       if constexpr (SP) dt = softplus_f(dt);
       if constexpr (TAIL) dt = tv ? dt : 0.f;  // padded steps are the identity map
-      const float ug = cvt_raw(cu[g]);
+      const float ug = cvt_raw(X.u[g]);
       const float dtu = dt * ug;
       if constexpr (MODE == kState) S += dt;
+#ifdef MTTS_DIAG_NOCOMPUTE
+      if constexpr (MODE == kFull) {
+        const float y = dtu + cvt_raw(X.z[g]);
+        if constexpr (TAIL) {
+          if (tv) stf(o0 + (int64_t)(tg + j) * a.out_ls + c, y);
+        } else {
+          stf(o0 + (int64_t)tg * a.out_ls + lo, y);
+        }
+      }
+      return;
+#endif
       float yp[P];
 #pragma unroll
       for (int s = 0; s < P; ++s) {
@@ -370,11 +401,15 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
       if constexpr (MODE == kFull) {
         float y = group_reduce_scatter<P>(yp, j);
         y = fmaf(Dc, ug, y);
-        if (has_z) y *= silu_f(cvt_raw(cz[g]));
+        if (has_z) y *= silu_f(cvt_raw(X.z[g]));
         if constexpr (TAIL) {
           if (tv) stf(o0 + (int64_t)(tg + j) * a.out_ls + c, y);
         } else {
+#ifdef MTTS_DIAG_NOMEM
+          diag_sink += y;
+#else
           stf(o0 + (int64_t)tg * a.out_ls + lo, y);
+#endif
         }
       }
       // materialise h here: otherwise (state-only mode) LLVM sinks every
@@ -385,39 +420,36 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
     });
   };
 
-  using TrueT = std::integral_constant<bool, true>;
-  using FalseT = std::integral_constant<bool, false>;
   const int nfull = (t_end - t_begin) / TT;
   const int ntiles = (t_end - t_begin + TT - 1) / TT;
-  if (nfull > 0) {
-    load_regs(FalseT{}, t_begin, cu, cd, cz);
-    load_stage(FalseT{}, t_begin);
-  } else {
-    load_regs(TrueT{}, t_begin, cu, cd, cz);
-    load_stage(TrueT{}, t_begin);
-  }
-  write_stage(0);
-  for (int it = 0; it < ntiles; ++it) {
-    const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);  // keep time indices in SGPRs
-    const int buf = it & 1;
-    __syncthreads();
-    if (it + 1 < ntiles) {
-      if (it + 1 < nfull) {
-        load_regs(FalseT{}, t0 + TT, nu, nd, nz);
-        load_stage(FalseT{}, t0 + TT);
-      } else {
-        load_regs(TrueT{}, t0 + TT, nu, nd, nz);
-        load_stage(TrueT{}, t0 + TT);
+  // ring of kRing register sets: tile it+kRing-1 is loading while tile it computes
+  // (prefetch distance kRing-1 tiles); ring slots are compile-time indices
+  constexpr int NR = P == 4 ? kRing : 2;  // P = 2 holds 8 states per lane: two sets fit
+  TileRegs ring[NR];
+  auto load_any = [&](int it, TileRegs& X) __attribute__((always_inline)) {
+    const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
+    if (it < nfull) load_tile(FalseT{}, t0, X);
+    else if (it < ntiles) load_tile(TrueT{}, t0, X);
+  };
+  static_for<NR - 1>([&](auto rc) { load_any(decltype(rc)::value, ring[decltype(rc)::value]); });
+  write_stage(0, ring[0]);
+  for (int it0 = 0; it0 < ntiles; it0 += NR) {
+    static_for<NR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      const int it = it0 + r;
+      if (it < ntiles) {
+        __syncthreads();
+        load_any(it + NR - 1, ring[(r + NR - 1) % NR]);
+        const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
+        if (it < nfull) compute_tile(FalseT{}, t0, it & 1, ring[r]);
+        else compute_tile(TrueT{}, t0, it & 1, ring[r]);
+        if (it + 1 < ntiles) write_stage((it + 1) & 1, ring[(r + 1) % NR]);
       }
-    }
-    if (it < nfull) compute_tile(FalseT{}, t0, buf);
-    else compute_tile(TrueT{}, t0, buf);
-    if (it + 1 < ntiles) {
-      write_stage(buf ^ 1);
-#pragma unroll
-      for (int g = 0; g < G; ++g) { cu[g] = nu[g]; cd[g] = nd[g]; cz[g] = nz[g]; }
-    }
+    });
   }
+#ifdef MTTS_DIAG_NOMEM
+  if (diag_sink == 12345.f) o0[c] = 0;
+#endif
   if constexpr (MODE == kFull) {
     if (k == K - 1 && a.last_state)
       store_vec<NS>(a.last_state + ((int64_t)b * a.dim + c) * kN + j * NS, h);
@@ -427,6 +459,237 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
 #pragma unroll
     for (int i = 0; i < NS; ++i) sp[j * NS + i] = h[i];
     if (j == 0) sp[kN] = S;
+  }
+}
+
+// ------------------------------------------------------------- forward, wide I/O
+// Same recurrence, lane mapping and L-segmentation as scan_fwd_kernel, but
+// u / delta / z tiles arrive as whole 16-byte chunks of timestep rows (the
+// block's CPB channels of one timestep are contiguous in the channel-last
+// layout) and go through LDS, and the outputs leave the same way.  The
+// per-lane 2-byte pattern of the narrow kernel issues 8x more memory
+// instructions than the bytes need and caps bf16 streaming at ~2.6 TB/s on
+// MI355X (memory-only timing build, tools/diag); 16-byte chunks do not.
+// Host-checked requirements: 16-byte aligned bases and strides of u, delta,
+// z, out and dim % (16 / sizeof(Tio)) == 0; otherwise the narrow kernel runs.
+constexpr bool wide_rows_ok(int P, int W, int pitch) {
+  for (int k1 = 0; k1 < P; ++k1)
+    for (int k2 = k1 + 1; k2 < P; ++k2) {
+      const int d = ((k2 - k1) * pitch) % 64;
+      if (d < W || 64 - d < W) return false;
+    }
+  return true;
+}
+// LDS row pitch (dwords) such that the P rows one wave reads in a group
+// (each W dwords wide) fall in disjoint banks; a multiple of 4 dwords.
+constexpr int wide_pitch_dw(int P, int rowdw, int W) {
+  for (int pad = 4; pad <= 64; pad += 4)
+    if (wide_rows_ok(P, W, rowdw + pad)) return rowdw + pad;
+  return rowdw + 4;
+}
+
+template <int P, typename Tio, typename Tbc, int MODE, bool SP>
+__global__ __launch_bounds__(kBlock, 4) void scan_fwd_wide_kernel(const MttsScanFwdArgs a, const int seg_len,
+                                                                  float* __restrict__ seg) {
+  constexpr int NS = kN / P;
+  constexpr int CPB = kBlock / P;           // channels per block
+  constexpr int ES = (int)sizeof(Tio);
+  constexpr int ROWB = CPB * ES;            // bytes of a block's timestep row
+  constexpr int TT = 4096 / ROWB;           // timesteps per tile (one 16-B chunk per thread per array)
+  constexpr int G = TT / P;                 // P-step groups per tile
+  constexpr int CPR = ROWB / 16;            // chunks per row
+  constexpr int EPC = 16 / ES;              // elements per chunk
+  constexpr int NA = MODE == kFull ? 3 : 2; // staged arrays: u, delta (, z)
+  constexpr int PIT = wide_pitch_dw(P, ROWB / 4, (64 / P) * ES / 4) * 4 / ES;  // row pitch (elements)
+  constexpr int VPT = TT * 2 * kN / kBlock;
+  static_assert(G >= 1 && TT % P == 0 && (TT * 2 * kN) % kBlock == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) Tio sX[2][NA][TT * PIT];
+  __shared__ __attribute__((aligned(16))) float sBC[2][TT * 2 * kN];
+
+  const int tid = threadIdx.x;
+  const int j = tid % P, cl = tid / P;
+  const int c0 = blockIdx.x * CPB;
+  const bool cvalid = c0 + cl < a.dim;
+  const int c = cvalid ? c0 + cl : a.dim - 1;
+  const int b = blockIdx.y;
+  const int k = blockIdx.z;
+  const int L = a.seqlen;
+  const int K = (L + seg_len - 1) / seg_len;
+  const int t_begin = k * seg_len;
+  const int t_end = min(L, t_begin + seg_len);
+  const bool has_z = MODE == kFull && a.z != nullptr;
+
+  // chunk this thread moves: row lrow, local channels [lcol, lcol + EPC)
+  const int lrow = tid / CPR, lcol = (tid % CPR) * EPC;
+  const bool lvalid = c0 + lcol < a.dim;  // whole chunk (dim % EPC == 0)
+  const Tio* __restrict__ gu = (const Tio*)a.u + (int64_t)b * a.u_bs + c0 + lcol;
+  const Tio* __restrict__ gd = (const Tio*)a.delta + (int64_t)b * a.delta_bs + c0 + lcol;
+  const Tio* __restrict__ gz = has_z ? (const Tio*)a.z + (int64_t)b * a.z_bs + c0 + lcol : gu;
+  const int64_t z_ls = has_z ? a.z_ls : a.u_ls;
+  Tio* __restrict__ go = (Tio*)a.out + (int64_t)b * a.out_bs + c0 + lcol;
+
+  // B/C staging slice (as in the narrow kernel)
+  const int e0 = tid * VPT;
+  const int st_s = e0 / (2 * kN), st_col = e0 % (2 * kN);
+  const Tbc* __restrict__ st0 = st_col < kN ? (const Tbc*)a.Bm + (int64_t)b * a.B_bs
+                                            : (const Tbc*)a.Cm + (int64_t)b * a.C_bs;
+  const int64_t st_ls = st_col < kN ? a.B_ls : a.C_ls;
+
+  float A2[NS], h[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) A2[i] = a.A[(int64_t)c * kN + j * NS + i] * kLog2e;
+  const float Dc = a.D ? a.D[c] : 0.f;
+  const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
+  float S = 0.f;
+  if constexpr (MODE == kFull) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) h[i] = a.h0 ? a.h0[((int64_t)b * a.dim + c) * kN + j * NS + i] : 0.f;
+    for (int kk = 0; kk < k; ++kk) {
+      const float* sp = seg + (((int64_t)b * K + kk) * a.dim + c) * (kN + 1);
+      const float Sk = sp[kN];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) h[i] = fmaf(__builtin_amdgcn_exp2f(A2[i] * Sk), h[i], sp[j * NS + i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) h[i] = 0.f;
+  }
+  const int nck = (MODE == kFull && a.ckpt) ? (L + kSub - 1) / kSub : 0;
+  float* __restrict__ ck0 = nck ? a.ckpt + (int64_t)b * nck * a.dim * kN : nullptr;
+  const uint32_t lck = (uint32_t)(c * kN + j * NS);
+
+  struct TileRegs {
+    uint4 x[NA];
+    RawVec<Tbc, VPT> st;
+  };
+  auto load_tile = [&](int t0, TileRegs& R) __attribute__((always_inline)) {
+    R.st.load(st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN));
+    const int t = t0 + lrow;
+    const bool ok = lvalid && t < t_end;
+    const int tc = ok ? t : t_begin;  // any in-range row; the value is discarded
+    R.x[0] = *reinterpret_cast<const uint4*>(gu + (int64_t)tc * a.u_ls);
+    R.x[1] = *reinterpret_cast<const uint4*>(gd + (int64_t)tc * a.delta_ls);
+    if constexpr (NA == 3) R.x[2] = *reinterpret_cast<const uint4*>(gz + (int64_t)tc * z_ls);
+    if (!ok) {
+#pragma unroll
+      for (int q = 0; q < NA; ++q) R.x[q] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto write_tile = [&](int buf, const TileRegs& R) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < NA; ++q) *reinterpret_cast<uint4*>(&sX[buf][q][lrow * PIT + lcol]) = R.x[q];
+    float v[VPT];
+    R.st.unpack(v);
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) sBC[buf][e0 + q] = v[q];
+  };
+  auto compute_tile = [&](auto tail, int t0, int buf) __attribute__((always_inline)) {
+    constexpr bool TAIL = decltype(tail)::value;
+    static_for<G>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      const int tg = t0 + g * P;
+      if constexpr ((TT % kSub) != 0 || (g * P) % kSub == 0) {
+        if (nck && cvalid && (tg & (kSub - 1)) == 0 && (!TAIL || tg < t_end))
+          store_vec<NS>(ck0 + (int64_t)(tg / kSub) * a.dim * kN + lck, h);
+      }
+      const int sx = (g * P + j) * PIT + cl;  // this lane's (step, channel) in the tile
+      const bool tv = !TAIL || (tg + j < t_end);
+      float dt = cvt_raw((raw_t<Tio>)sX[buf][1][sx]) + bias;
+      if constexpr (SP) dt = softplus_f(dt);
+      if constexpr (TAIL) dt = tv ? dt : 0.f;  // padded steps are the identity map
+      const float ug = cvt_raw((raw_t<Tio>)sX[buf][0][sx]);
+      const float dtu = dt * ug;
+      if constexpr (MODE == kState) S += dt;
+      float yp[P];
+#pragma unroll
+      for (int s = 0; s < P; ++s) {
+        float dts, dtus;
+        if constexpr (P == 2) {
+          dts = s == 0 ? group_bcast<2, 0>(dt) : group_bcast<2, 1>(dt);
+          dtus = s == 0 ? group_bcast<2, 0>(dtu) : group_bcast<2, 1>(dtu);
+        } else {
+          dts = s == 0 ? group_bcast<4, 0>(dt) : s == 1 ? group_bcast<4, 1>(dt)
+              : s == 2 ? group_bcast<4, 2>(dt) : group_bcast<4, 3>(dt);
+          dtus = s == 0 ? group_bcast<4, 0>(dtu) : s == 1 ? group_bcast<4, 1>(dtu)
+               : s == 2 ? group_bcast<4, 2>(dtu) : group_bcast<4, 3>(dtu);
+        }
+        asm volatile("" : "+v"(dts), "+v"(dtus));
+        const f2 dts2 = {dts, dts}, dtus2 = {dtus, dtus};
+        const float* bc = &sBC[buf][(g * P + s) * 2 * kN];
+        f2 y2 = {0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < NS / 4; ++q) {
+          const f4 vb = *reinterpret_cast<const f4*>(bc + j * NS + 4 * q);
+          f4 vc = {};
+          if constexpr (MODE == kFull) vc = *reinterpret_cast<const f4*>(bc + kN + j * NS + 4 * q);
+#pragma unroll
+          for (int p2 = 0; p2 < 2; ++p2) {
+            const int i = 4 * q + 2 * p2;
+            const f2 x = dts2 * f2{A2[i], A2[i + 1]};
+            const f2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+            const f2 bv = p2 ? f2{vb[2], vb[3]} : f2{vb[0], vb[1]};
+            const f2 hn = __builtin_elementwise_fma(e, f2{h[i], h[i + 1]}, dtus2 * bv);
+            h[i] = hn[0];
+            h[i + 1] = hn[1];
+            if constexpr (MODE == kFull) {
+              const f2 cv = p2 ? f2{vc[2], vc[3]} : f2{vc[0], vc[1]};
+              y2 = __builtin_elementwise_fma(cv, hn, y2);
+            }
+          }
+        }
+        yp[s] = y2[0] + y2[1];
+      }
+      if constexpr (MODE == kFull) {
+        float y = group_reduce_scatter<P>(yp, j);
+        y = fmaf(Dc, ug, y);
+        if (has_z) y *= silu_f(cvt_raw((raw_t<Tio>)sX[buf][2][sx]));
+        stf(&sX[buf][0][sx], y);  // the output replaces u in the tile image
+      }
+#ifndef MTTS_WIDE_FREE_SCHED
+#pragma unroll
+      for (int i = 0; i < NS; ++i) asm volatile("" : "+v"(h[i]));
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+    });
+  };
+  auto store_tile = [&](int t0, int buf) __attribute__((always_inline)) {
+    if constexpr (MODE == kFull) {
+      const int t = t0 + lrow;
+      if (lvalid && t < t_end)
+        *reinterpret_cast<uint4*>(go + (int64_t)t * a.out_ls) =
+            *reinterpret_cast<const uint4*>(&sX[buf][0][lrow * PIT + lcol]);
+    }
+  };
+
+  const int nfull = (t_end - t_begin) / TT;
+  const int ntiles = (t_end - t_begin + TT - 1) / TT;
+  TileRegs R;
+  load_tile(t_begin, R);
+  write_tile(0, R);
+  for (int it = 0; it < ntiles; ++it) {
+    const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
+    const int buf = it & 1;
+    __syncthreads();                                  // tile it in LDS; buffer buf^1 free
+    if (it + 1 < ntiles) load_tile(t0 + TT, R);       // in flight during the compute
+    if (it < nfull) compute_tile(FalseT{}, t0, buf);
+    else compute_tile(TrueT{}, t0, buf);
+    if (it + 1 < ntiles) write_tile(buf ^ 1, R);
+    if constexpr (MODE == kFull) {
+      __syncthreads();                                // outputs of tile it complete
+      store_tile(t0, buf);
+    }
+  }
+  if constexpr (MODE == kFull) {
+    if (k == K - 1 && a.last_state && cvalid)
+      store_vec<NS>(a.last_state + ((int64_t)b * a.dim + c) * kN + j * NS, h);
+  } else {
+    S = group_allreduce<P>(S);
+    if (cvalid) {
+      float* sp = seg + (((int64_t)b * K + k) * a.dim + c) * (kN + 1);
+#pragma unroll
+      for (int i = 0; i < NS; ++i) sp[j * NS + i] = h[i];
+      if (j == 0) sp[kN] = S;
+    }
   }
 }
 
@@ -980,10 +1243,33 @@ static FwdPlan plan_bwd(int batch, int dim, int seqlen) {
   return pl;
 }
 
+// 16-byte chunks of u / delta / z / out rows are addressable (wide kernel)
+static bool wide_io_ok(const MttsScanFwdArgs* a) {
+  if (getenv("MTTS_SCAN_NARROW")) return false;
+  const int es = a->dtype_io == MTTS_BF16 ? 2 : 4;
+  const int64_t epc = 16 / es;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (a->dim % epc) return false;
+  if (!al(a->u) || !al(a->delta) || !al(a->out) || (a->z && !al(a->z))) return false;
+  const int64_t st[] = {a->u_bs, a->u_ls, a->delta_bs, a->delta_ls, a->out_bs, a->out_ls,
+                        a->z ? a->z_bs : 0, a->z ? a->z_ls : 0};
+  for (int64_t v : st)
+    if (v % epc) return false;
+  return true;
+}
+
 template <int P, typename Tio, typename Tbc, bool SP>
 static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream_t st) {
   const int nbx = (a->dim + kBlock / P - 1) / (kBlock / P);
   float* seg = (float*)a->workspace;
+  if (wide_io_ok(a)) {
+    if (pl.K > 1)
+      hipLaunchKernelGGL((scan_fwd_wide_kernel<P, Tio, Tbc, kState, SP>), dim3(nbx, a->batch, pl.K - 1),
+                         dim3(kBlock), 0, st, *a, pl.seg_len, seg);
+    hipLaunchKernelGGL((scan_fwd_wide_kernel<P, Tio, Tbc, kFull, SP>), dim3(nbx, a->batch, pl.K), dim3(kBlock), 0,
+                       st, *a, pl.seg_len, seg);
+    return;
+  }
   if (pl.K > 1)
     hipLaunchKernelGGL((scan_fwd_kernel<P, Tio, Tbc, kState, SP>), dim3(nbx, a->batch, pl.K - 1), dim3(kBlock), 0,
                        st, *a, pl.seg_len, seg);

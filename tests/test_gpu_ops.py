@@ -34,13 +34,18 @@ def g32(a):
     return torch.from_numpy(np.asarray(a)).to(DEV, torch.float32)
 
 
-@pytest.fixture(params=["2", "4", "4:s3"])
+@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2"])
 def scan_p(request):
     """P (lanes per channel) and, with ':sK', a forced split of L into K
-    segments for both the forward and the backward (two-pass path)."""
-    keys = ("MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_BWD_SEGS")
+    segments for both the forward and the backward (two-pass path); 'n'
+    forces the narrow (per-lane element) forward kernel instead of the
+    16-byte-chunk one."""
+    keys = ("MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_BWD_SEGS", "MTTS_SCAN_NARROW")
     old = {k: os.environ.get(k) for k in keys}
     p, _, segs = request.param.partition(":s")
+    if p.endswith("n"):
+        p = p[:-1]
+        os.environ["MTTS_SCAN_NARROW"] = "1"
     os.environ["MTTS_SCAN_P"] = p
     if segs:
         os.environ["MTTS_SCAN_SEGS"] = segs
@@ -80,7 +85,8 @@ def test_scan_fwd_bwd_vs_golden(golden, name, scan_p):
         close(db, g["ddelta_bias"], name="ddelta_bias")
 
 
-@pytest.mark.parametrize("shape", [(1, 1, 1), (2, 3, 5), (3, 100, 37), (2, 70, 130), (1, 64, 1000)])
+@pytest.mark.parametrize("shape", [(1, 1, 1), (2, 3, 5), (3, 100, 37), (2, 70, 130), (1, 64, 1000), (2, 200, 77),
+                                   (1, 136, 300)])
 def test_scan_ragged_shapes_and_h0_split(shape, scan_p):
     """Ragged (B, D, L) incl. L=1, D not a multiple of 64, L not a multiple of
     16; and scanning [0,L1) then [L1,L) from h0=last_state equals one scan."""
