@@ -770,12 +770,21 @@ __device__ __forceinline__ void wave_reduce_scatter32(float (&v)[32], float& o0,
 // from zero carry-in at the segment end and record the carry leaving the
 // segment start, g_k = exp(dt_{t0} A) dh_{t0}, plus S_k = sum(dt).  The carry
 // entering segment k is then G_k = sum_{j>k} exp(A (S_{k+1}+..+S_{j-1})) g_j.
-template <typename Tio, typename Tbc, bool SP>
+template <typename Tio, typename Tbc, bool SP, bool WIDE>
 __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsScanBwdArgs a, const int seg_len,
                                                                    float* __restrict__ seg) {
   constexpr int G = kTileG;          // groups per tile
   constexpr int TT = G * kPB;        // 32 timesteps per tile
   __shared__ __attribute__((aligned(16))) float sC[2][TT * kN];
+  // WIDE staging of delta / dout / z tiles (16-byte row chunks through LDS)
+  constexpr int ES = (int)sizeof(Tio);
+  constexpr int ROWB = kChB * ES;
+  constexpr int CPR = ROWB / 16;
+  constexpr int EPC = 16 / ES;
+  constexpr int PIT = wide_pitch_dw(kPB, ROWB / 4, (64 / kPB) * ES / 4) * 4 / ES;
+  constexpr int NCH = 3 * TT * CPR / kBlock;
+  __shared__ __attribute__((aligned(16))) Tio sX[WIDE ? 2 : 1][3][WIDE ? TT * PIT : 1];
+  const int cl = threadIdx.x / kPB;
   const MttsScanFwdArgs& f = a.f;
   const int j = threadIdx.x % kPB;
   const int c_raw = blockIdx.x * kChB + threadIdx.x / kPB;
@@ -831,23 +840,77 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
     st.unpack(v);
     *reinterpret_cast<float2*>(&sC[buf][e0]) = make_float2(v[0], v[1]);
   };
+  // WIDE: this thread's chunks (array, row, column), loaded as 16-byte pieces
+  uint4 wx[WIDE ? NCH : 1];
+  const Tio* wsrc[WIDE ? NCH : 1];
+  int64_t wls[WIDE ? NCH : 1];
+  int wrow[WIDE ? NCH : 1], warr[WIDE ? NCH : 1], wcol[WIDE ? NCH : 1];
+  bool wok[WIDE ? NCH : 1];
+  if constexpr (WIDE) {
+    const int c0 = blockIdx.x * kChB;
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      const int idx = threadIdx.x + kBlock * q;
+      warr[q] = idx / (TT * CPR);
+      wrow[q] = (idx % (TT * CPR)) / CPR;
+      wcol[q] = (idx % CPR) * EPC;
+      wok[q] = c0 + wcol[q] < f.dim;
+      const int ar = warr[q];
+      wsrc[q] = (ar == 0 ? d0 : ar == 1 ? g0 : z0) + c0 + wcol[q];
+      wls[q] = ar == 0 ? f.delta_ls : ar == 1 ? a.dout_ls : z_ls;
+    }
+  }
+  auto load_w = [&](int t0) {
+    st.load(C0 + (int64_t)min(t0 + st_s, L - 1) * f.C_ls + st_n);
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      const int tr = t0 + wrow[q];
+      const bool ok = wok[q] && tr < t_end;
+      wx[q] = *reinterpret_cast<const uint4*>(wsrc[q] + (int64_t)(ok ? tr : t_begin) * wls[q]);
+      if (!ok) wx[q] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto write_w = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) *reinterpret_cast<uint4*>(&sX[buf][warr[q]][wrow[q] * PIT + wcol[q]]) = wx[q];
+    write_stage(buf);
+  };
   const int ntiles = (t_end - t_begin + TT - 1) / TT;
-  load(t_begin + (ntiles - 1) * TT, cx, cg, cz);
-  write_stage(0);
+  if constexpr (WIDE) {
+    load_w(t_begin + (ntiles - 1) * TT);
+    write_w(0);
+  } else {
+    load(t_begin + (ntiles - 1) * TT, cx, cg, cz);
+    write_stage(0);
+  }
   for (int q = 0; q < ntiles; ++q) {
     const int it = ntiles - 1 - q;
     const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
     const int buf = q & 1;
     __syncthreads();
-    if (it > 0) load(t0 - TT, nx, ng, nz);
+    if (it > 0) {
+      if constexpr (WIDE) load_w(t0 - TT);
+      else load(t0 - TT, nx, ng, nz);
+    }
     static_for<G>([&](auto gc) {
       constexpr int g = G - 1 - decltype(gc)::value;
       const bool tv = t0 + g * kPB + j < t_end;
-      float dt = cvt_raw(cx[g]) + bias;
+      R rx, rg, rz;
+      if constexpr (WIDE) {
+        const int sx = (g * kPB + j) * PIT + cl;
+        rx = (R)sX[buf][0][sx];
+        rg = (R)sX[buf][1][sx];
+        rz = (R)sX[buf][2][sx];
+      } else {
+        rx = cx[g];
+        rg = cg[g];
+        rz = cz[g];
+      }
+      float dt = cvt_raw(rx) + bias;
       if constexpr (SP) dt = softplus_f(dt);
       dt = tv ? dt : 0.f;
-      float dy = tv ? cvt_raw(cg[g]) : 0.f;
-      if (has_z) dy *= silu_f(cvt_raw(cz[g]));
+      float dy = tv ? cvt_raw(rg) : 0.f;
+      if (has_z) dy *= silu_f(cvt_raw(rz));
       S += dt;
 #pragma unroll
       for (int s = kPB - 1; s >= 0; --s) {
@@ -868,9 +931,13 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
       __builtin_amdgcn_sched_barrier(0);
     });
     if (it > 0) {
-      write_stage(buf ^ 1);
+      if constexpr (WIDE) {
+        write_w(buf ^ 1);
+      } else {
+        write_stage(buf ^ 1);
 #pragma unroll
-      for (int g = 0; g < G; ++g) { cx[g] = nx[g]; cg[g] = ng[g]; cz[g] = nz[g]; }
+        for (int g = 0; g < G; ++g) { cx[g] = nx[g]; cg[g] = ng[g]; cz[g] = nz[g]; }
+      }
     }
   }
   S = group_allreduce<kPB>(S);
@@ -882,7 +949,9 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   }
 }
 
-template <typename Tio, typename Tbc, bool SP>
+// WIDE: u / delta / z / dout chunks arrive as 16-byte row pieces through LDS
+// and du / ddelta / dz leave the same way (see scan_fwd_wide_kernel).
+template <typename Tio, typename Tbc, bool SP, bool WIDE>
 __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdArgs a, float* __restrict__ slab,
                                                              float* __restrict__ par, const int seg_len,
                                                              const float* __restrict__ seg) {
@@ -904,6 +973,16 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
 
   __shared__ __attribute__((aligned(16))) float red[kWaves][kSub * 2 * kN];  // per-wave dB/dC of one chunk
   __shared__ __attribute__((aligned(16))) float sBC[kSub * 2 * kN];          // B|C of the chunk, fp32
+  // WIDE staging: [buffer][u, delta, z, dout][kSub rows of the block's channels]
+  constexpr int ES = (int)sizeof(Tio);
+  constexpr int ROWB = kChB * ES;
+  constexpr int CPR = ROWB / 16;                  // 16-B chunks per row
+  constexpr int EPC = 16 / ES;
+  constexpr int PIT = wide_pitch_dw(kPB, ROWB / 4, (64 / kPB) * ES / 4) * 4 / ES;
+  constexpr int NIN = 4 * kSub * CPR / kBlock;    // input chunks per thread per chunk of steps
+  constexpr int NOUT = (3 * kSub * CPR + kBlock - 1) / kBlock;
+  __shared__ __attribute__((aligned(16))) Tio sIn[WIDE ? 2 : 1][4][WIDE ? kSub * PIT : 1];
+  const int cl = threadIdx.x / kPB;                // local channel
 
   // per-batch bases (uniform) + 32-bit per-lane offsets (lane j owns steps 4g+j)
   const Tio* __restrict__ u0 = (const Tio*)f.u + (int64_t)b * f.u_bs;
@@ -959,12 +1038,44 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   R n_u[kGB], n_x[kGB], n_z[kGB], n_g[kGB];
   RawVec<Tbc, 2> n_st;
   float n_hs[kNSB];
-  // steps >= L load a clamped index; their dy is zeroed at use
+  // WIDE: this thread's input / output chunks (array, row, column) are fixed
+  uint4 wx[WIDE ? NIN : 1];
+  const Tio* wsrc[WIDE ? NIN : 1];
+  int64_t wls[WIDE ? NIN : 1];
+  int wrow[WIDE ? NIN : 1], warr[WIDE ? NIN : 1], wcol[WIDE ? NIN : 1];
+  bool wok[WIDE ? NIN : 1];
+  if constexpr (WIDE) {
+    const int c0 = blockIdx.x * kChB;
+#pragma unroll
+    for (int q = 0; q < NIN; ++q) {
+      const int idx = threadIdx.x + kBlock * q;
+      warr[q] = idx / (kSub * CPR);
+      wrow[q] = (idx % (kSub * CPR)) / CPR;
+      wcol[q] = (idx % CPR) * EPC;
+      wok[q] = c0 + wcol[q] < f.dim;
+      const int ar = warr[q];
+      wsrc[q] = ar == 0 ? u0 : ar == 1 ? d0 : ar == 2 ? z0 : g0;
+      wsrc[q] += c0 + wcol[q];
+      wls[q] = ar == 0 ? f.u_ls : ar == 1 ? f.delta_ls : ar == 2 ? z_ls : a.dout_ls;
+    }
+  }
+  // steps >= L load a clamped index (narrow) or zeros (wide); their dy is zeroed at use
   auto prefetch = [&](int k) {
     const int t_start = __builtin_amdgcn_readfirstlane(k * kSub);
     const bool full = t_start + kSub <= L;
     const int t = full ? t_start + st_s : min(t_start + st_s, L - 1);
     n_st.load(st0 + (int64_t)t * st_ls + st_n);
+    load_vec<float, kNSB>(f.ckpt + (((int64_t)b * nck + k) * f.dim + c) * kN + j * kNSB, n_hs);
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int q = 0; q < NIN; ++q) {
+        const int tr = t_start + wrow[q];
+        const bool ok = wok[q] && tr < L;
+        wx[q] = *reinterpret_cast<const uint4*>(wsrc[q] + (int64_t)(ok ? tr : 0) * wls[q]);
+        if (!ok) wx[q] = make_uint4(0, 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int g = 0; g < kGB; ++g) {
       const int tg = t_start + g * kPB;
@@ -981,9 +1092,15 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
         n_g[g] = ldr(g0 + (int64_t)tc * a.dout_ls + c);
       }
     }
-    load_vec<float, kNSB>(f.ckpt + (((int64_t)b * nck + k) * f.dim + c) * kN + j * kNSB, n_hs);
   };
-  if (ck_end > ck_begin) prefetch(ck_end - 1);
+  auto write_in = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NIN; ++q) *reinterpret_cast<uint4*>(&sIn[buf][warr[q]][wrow[q] * PIT + wcol[q]]) = wx[q];
+  };
+  if (ck_end > ck_begin) {
+    prefetch(ck_end - 1);
+    if constexpr (WIDE) write_in((ck_end - 1) & 1);
+  }
 
   for (int k = ck_end - 1; k >= ck_begin; --k) {
     const int t_start = __builtin_amdgcn_readfirstlane(k * kSub);
@@ -994,13 +1111,26 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       *reinterpret_cast<float2*>(&sBC[e0]) = make_float2(v[0], v[1]);
     }
     float uu[kGB], xr[kGB], dt[kGB], zz[kGB], go[kGB], hs[kNSB];
+    const int buf = WIDE ? (k & 1) : 0;
+    if constexpr (WIDE) {
+      __syncthreads();  // staged inputs + B/C of this chunk visible
 #pragma unroll
-    for (int g = 0; g < kGB; ++g) {
-      uu[g] = cvt_raw(n_u[g]);
-      xr[g] = cvt_raw(n_x[g]) + bias;
-      zz[g] = cvt_raw(n_z[g]);
-      // padded steps (>= L) and lanes past `dim` contribute nothing
-      go[g] = (cvalid && (full || t_start + g * kPB + j < L)) ? cvt_raw(n_g[g]) : 0.f;
+      for (int g = 0; g < kGB; ++g) {
+        const int sx = (g * kPB + j) * PIT + cl;
+        uu[g] = cvt_raw((R)sIn[buf][0][sx]);
+        xr[g] = cvt_raw((R)sIn[buf][1][sx]) + bias;
+        zz[g] = cvt_raw((R)sIn[buf][2][sx]);
+        go[g] = (cvalid && (full || t_start + g * kPB + j < L)) ? cvt_raw((R)sIn[buf][3][sx]) : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < kGB; ++g) {
+        uu[g] = cvt_raw(n_u[g]);
+        xr[g] = cvt_raw(n_x[g]) + bias;
+        zz[g] = cvt_raw(n_z[g]);
+        // padded steps (>= L) and lanes past `dim` contribute nothing
+        go[g] = (cvalid && (full || t_start + g * kPB + j < L)) ? cvt_raw(n_g[g]) : 0.f;
+      }
     }
 #pragma unroll
     for (int i = 0; i < kNSB; ++i) hs[i] = n_hs[i];
@@ -1011,7 +1141,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       if constexpr (SP) d = softplus_f(d);
       dt[g] = (full || t_start + g * kPB + j < L) ? d : 0.f;
     }
-    __syncthreads();
+    if constexpr (!WIDE) __syncthreads();
 
     // ---- replay the chunk forward: h history in registers (state pairs, packed f32)
     f2 hh[kSub][2];
@@ -1113,6 +1243,13 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       float ddr = ddt_j;
       if constexpr (SP) ddr *= softplus_grad(xr[g]);
       if (tv) dbias_acc += ddr;
+      if constexpr (WIDE) {  // into the chunk image (inputs of this step already consumed)
+        const int sx = (g * kPB + j) * PIT + cl;
+        stf(&sIn[buf][0][sx], du_j);
+        stf(&sIn[buf][1][sx], ddr);
+        stf(&sIn[buf][2][sx], dzv);
+        continue;
+      }
       // lanes past `dim` computed zeros for channel dim-1: they must not store
       if (full && cvalid) {
         stf(du0 + (int64_t)tg * a.du_ls + odu, du_j);
@@ -1132,6 +1269,24 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       for (int w = 0; w < kWaves; ++w) sum += red[w][q];
       const int t = t_start + q / (2 * kN);
       if (t < L) slab[(((int64_t)b * nblk + blockIdx.x) * L + t) * (2 * kN) + (q % (2 * kN))] = sum;
+    }
+    if constexpr (WIDE) {
+      // du / ddelta / dz chunks of this chunk of steps -> global
+      const int c0 = blockIdx.x * kChB;
+#pragma unroll
+      for (int q = 0; q < NOUT; ++q) {
+        const int idx = threadIdx.x + kBlock * q;
+        if (idx < 3 * kSub * CPR) {
+          const int ar = idx / (kSub * CPR), row = (idx % (kSub * CPR)) / CPR, col = (idx % CPR) * EPC;
+          const int t = t_start + row;
+          if (c0 + col < f.dim && t < L && (ar != 2 || has_z)) {
+            Tio* dst = ar == 0 ? du0 + (int64_t)t * a.du_ls : ar == 1 ? dd0 + (int64_t)t * a.ddelta_ls
+                                                                      : dz0 + (int64_t)t * a.dz_ls;
+            *reinterpret_cast<uint4*>(dst + c0 + col) = *reinterpret_cast<const uint4*>(&sIn[buf][ar][row * PIT + col]);
+          }
+        }
+      }
+      if (k - 1 >= ck_begin) write_in((k - 1) & 1);
     }
   }
 
@@ -1326,24 +1481,58 @@ extern "C" int64_t mtts_selective_scan_bwd_workspace(int batch, int dim, int seq
   return (slab + par + segw) * 4 + 256;
 }
 
+// the backward's activations and gradients are all 16-byte addressable
+static bool wide_bwd_ok(const MttsScanBwdArgs* a) {
+  if (!wide_io_ok(&a->f)) return false;
+  const int64_t epc = a->f.dtype_io == MTTS_BF16 ? 8 : 4;
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al(a->dout) || !al(a->du) || !al(a->ddelta) || (a->dz && !al(a->dz))) return false;
+  const int64_t st[] = {a->dout_bs, a->dout_ls, a->du_bs, a->du_ls, a->ddelta_bs, a->ddelta_ls,
+                        a->dz ? a->dz_bs : 0, a->dz ? a->dz_ls : 0};
+  for (int64_t v : st)
+    if (v % epc) return false;
+  return true;
+}
+
 template <typename Tio, typename Tbc>
 static void launch_bwd(const MttsScanBwdArgs* a, const FwdPlan& pl, float* slab, float* par, float* segw,
                        hipStream_t st) {
   const int nblk = (a->f.dim + kChB - 1) / kChB;
+  const dim3 grid(nblk, a->f.batch, pl.K);
+  const bool wide = wide_bwd_ok(a);
   if (pl.K > 1) {
-    if (a->f.delta_softplus)
-      hipLaunchKernelGGL((scan_bwd_carry_kernel<Tio, Tbc, true>), dim3(nblk, a->f.batch, pl.K - 1), dim3(kBlock), 0,
-                         st, *a, pl.seg_len, segw);
-    else
-      hipLaunchKernelGGL((scan_bwd_carry_kernel<Tio, Tbc, false>), dim3(nblk, a->f.batch, pl.K - 1), dim3(kBlock), 0,
-                         st, *a, pl.seg_len, segw);
+    const dim3 cgrid(nblk, a->f.batch, pl.K - 1);
+    if (a->f.delta_softplus) {
+      if (wide)
+        hipLaunchKernelGGL((scan_bwd_carry_kernel<Tio, Tbc, true, true>), cgrid, dim3(kBlock), 0, st, *a, pl.seg_len,
+                           segw);
+      else
+        hipLaunchKernelGGL((scan_bwd_carry_kernel<Tio, Tbc, true, false>), cgrid, dim3(kBlock), 0, st, *a, pl.seg_len,
+                           segw);
+    } else {
+      if (wide)
+        hipLaunchKernelGGL((scan_bwd_carry_kernel<Tio, Tbc, false, true>), cgrid, dim3(kBlock), 0, st, *a, pl.seg_len,
+                           segw);
+      else
+        hipLaunchKernelGGL((scan_bwd_carry_kernel<Tio, Tbc, false, false>), cgrid, dim3(kBlock), 0, st, *a,
+                           pl.seg_len, segw);
+    }
   }
-  if (a->f.delta_softplus)
-    hipLaunchKernelGGL((scan_bwd_kernel<Tio, Tbc, true>), dim3(nblk, a->f.batch, pl.K), dim3(kBlock), 0, st, *a, slab,
-                       par, pl.seg_len, (const float*)segw);
-  else
-    hipLaunchKernelGGL((scan_bwd_kernel<Tio, Tbc, false>), dim3(nblk, a->f.batch, pl.K), dim3(kBlock), 0, st, *a,
-                       slab, par, pl.seg_len, (const float*)segw);
+  if (a->f.delta_softplus) {
+    if (wide)
+      hipLaunchKernelGGL((scan_bwd_kernel<Tio, Tbc, true, true>), grid, dim3(kBlock), 0, st, *a, slab, par, pl.seg_len,
+                         (const float*)segw);
+    else
+      hipLaunchKernelGGL((scan_bwd_kernel<Tio, Tbc, true, false>), grid, dim3(kBlock), 0, st, *a, slab, par,
+                         pl.seg_len, (const float*)segw);
+  } else {
+    if (wide)
+      hipLaunchKernelGGL((scan_bwd_kernel<Tio, Tbc, false, true>), grid, dim3(kBlock), 0, st, *a, slab, par,
+                         pl.seg_len, (const float*)segw);
+    else
+      hipLaunchKernelGGL((scan_bwd_kernel<Tio, Tbc, false, false>), grid, dim3(kBlock), 0, st, *a, slab, par,
+                         pl.seg_len, (const float*)segw);
+  }
 }
 
 extern "C" int mtts_selective_scan_bwd(const MttsScanBwdArgs* a, void* stream) {
