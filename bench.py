@@ -67,6 +67,7 @@ def make_batch(c, dev, seed):
 
 def train_bench(args, rank, world, dev):
     import mamba_decoder
+    from mtts.optim import clip_into_optimizer
     c = dict(C2)
     torch.manual_seed(0)
     model = mamba_decoder.MambaTTSDecoder(c["vocab"], d_model=c["d_model"], n_layers=c["n_layers"],
@@ -91,7 +92,7 @@ def train_bench(args, rank, world, dev):
         loss.backward()
         if dp is not None:
             dp.finish()
-        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        clip_into_optimizer(opt, params, 1.0)   # clip_grad_norm_(params, 1.0) applied inside the fused Adam pass
         opt.step()
         return loss
 

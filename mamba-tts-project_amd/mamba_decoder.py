@@ -29,6 +29,7 @@ from mtts.attention import CrossAttention
 from mtts import ops
 from mtts.linear import cast_scope, linear
 from mtts.decode import DecodeEngine
+from mtts.embed import embed_sum
 
 
 class MambaTTSDecoderLayer(nn.Module):
@@ -200,11 +201,11 @@ class MambaTTSDecoder(nn.Module):
         text_hidden = text_hidden.to(cd)
         text_hidden, text_mask = self._concat_ref(text_hidden, text_mask, ref_hidden, ref_mask, B, device)
 
-        tok = self.token_embed(audio_tokens)
-        qemb = self.quant_embed(quant_ids)
-        pos_ids = torch.arange(T, device=device)
-        pos = self.pos_embed(pos_ids)[None, :, :].expand(B, T, -1)
-        x = (tok + pos + qemb).to(cd)
+        # token + position + quantizer embeddings (:201-206), fused backward
+        if T > self.pos_embed.num_embeddings:
+            raise IndexError(f"sequence length {T} exceeds pos_embed max_len {self.pos_embed.num_embeddings}")
+        x = embed_sum(audio_tokens, quant_ids, self.token_embed.weight, self.quant_embed.weight,
+                      self.pos_embed.weight, cd)
 
         with cast_scope(self._gemm_weights(), cd):
             x, pending, _ = self._run_layers(x, text_hidden, z_style, text_mask, None)

@@ -79,7 +79,7 @@ class MambaInnerFn(torch.autograd.Function):
         dW_dt = wgrad(dd2, dt.reshape(-1, r))
         # x_proj: x_dbl = u @ W_x^T
         gx = dx_dbl.to(cd)
-        du = du + gx @ Wx
+        du.view(-1, di).addmm_(gx.view(-1, r + 2 * N), Wx)   # du += d(x_dbl) W_x, accumulated by the GEMM
         dW_x = wgrad(gx.reshape(-1, r + 2 * N), u.reshape(-1, di))
         _, dw, db = ops.conv_bwd(x, conv_w, conv_b, du, True, dx=dxz[..., :di])
         dA_log = (dA * A).to(A_log.dtype)
