@@ -43,7 +43,9 @@ def _worker(rank, world, port, bucket_mb, q):
         dp.zero_grad()
         m(x[rank * 6:(rank + 1) * 6]).square().mean().backward()
         dp.finish()
-    q.put((rank, {n: p.grad.clone() for n, p in m.named_parameters()}, len(dp.buckets)))
+    # numpy copies travel by value: a torch tensor would go through shared memory
+    # that can vanish when this process exits before the parent reads it
+    q.put((rank, {n: p.grad.detach().numpy().copy() for n, p in m.named_parameters()}, len(dp.buckets)))
     dist.destroy_process_group()
 
 
@@ -71,4 +73,4 @@ def test_grad_allreduce_gloo_world2(bucket_mb):
             assert nb > 1
         for n, p in m.named_parameters():
             ref = p.grad if p.grad is not None else torch.zeros_like(p)
-            torch.testing.assert_close(grads[n], ref, rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(grads[n]), ref, rtol=1e-5, atol=1e-6)
