@@ -729,10 +729,55 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_wide_kernel(const MttsScan
 //    stored right after the barrier that opens tile i+1, each chunk by the
 //    lane whose DMA refills it next (the store's read precedes that DMA).
 // 16-byte LDS-DMA: lane l's 16 bytes at g land at lds + 16*l (lds wave-uniform).
-// (Host pass: the target builtin would silently drop the kernel's host stub.)
+// Inline asm, not __builtin_amdgcn_global_load_lds: with the builtin hipcc puts
+// an s_waitcnt vmcnt(0) in front of the next LDS read it cannot prove disjoint
+// (any read of the other tile buffer), which serialises the prefetch with the
+// compute.  The asm is invisible to the compiler's wait insertion, so every
+// consumer of DMA'd bytes is preceded by an explicit wait_vmem() + barrier.
+// M0 holds the LDS base (one wait state before the DMA reads it).
 __device__ __forceinline__ void dma16(const void* g, void* lds) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+#endif
+}
+// W-dword global load into registers, invisible to the compiler's wait
+// insertion (so a later LDS-DMA can stay in flight past its consumer);
+// consume only after wait_vm<N>(regs) with the loads counted.
+template <int W, bool HALF = false>
+__device__ __forceinline__ void ldg_asm(uint32_t (&w)[W], const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (HALF) {
+    static_assert(W == 1, "half-dword load");
+    asm volatile("global_load_ushort %0, %1, off" : "=v"(w[0]) : "v"(p) : "memory");
+  } else if constexpr (W == 1) {
+    asm volatile("global_load_dword %0, %1, off" : "=v"(w[0]) : "v"(p) : "memory");
+  } else if constexpr (W == 2) {
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    u2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    w[0] = v[0]; w[1] = v[1];
+  } else {
+    static_assert(W == 4, "ldg_asm width");
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    u4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    w[0] = v[0]; w[1] = v[1]; w[2] = v[2]; w[3] = v[3];
+  }
+#endif
+}
+// s_waitcnt vmcnt(N) that also "redefines" the staged registers, so no use of
+// them can be scheduled above the wait.
+template <int N, int W>
+__device__ __forceinline__ void wait_vm(uint32_t (&w)[W]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(N == 0 || N == 2 || N == 3, "wait_vm count");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+#pragma unroll
+  for (int q = 0; q < W; ++q) asm volatile("" : "+v"(w[q]));
 #endif
 }
 __device__ __forceinline__ void wait_vmem() {
@@ -775,7 +820,7 @@ struct DmaTile {
   }
 };
 
-template <int P, typename Tio, typename Tbc, int MODE, bool SP>
+template <int P, typename Tio, typename Tbc, int MODE, bool SP, bool XL>
 __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFwdArgs a, const int seg_len,
                                                                 float* __restrict__ seg) {
   constexpr int NS = kN / P;
@@ -793,12 +838,18 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
   static_assert(G >= 1 && TT % P == 0 && (TT * 2 * kN) % kBlock == 0 && NS % 4 == 0, "tile shape");
   static_assert(TT * CPR == kBlock, "one chunk per thread per array");
   static_assert(DT::conflict_free(), "swizzle");
-  __shared__ __attribute__((aligned(16))) Tio sX[2][NA][IMG];
+  // tile buffers: 3 (DMA two tiles ahead) when they fit 4 blocks per CU, else 2
+  constexpr int NB = (3 * NA * IMG * ES + 2 * TT * 2 * kN * 4 + (XL ? 4096 : 0)) <= 40960 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) Tio sX[NB][NA][IMG];
   __shared__ __attribute__((aligned(16))) float sBC[2][TT * 2 * kN];
+  // per-wave (delta, delta*u) exchange: the lane that formed step s of a
+  // group writes its pair, every lane of the channel reads all P pairs
+  __shared__ __attribute__((aligned(16))) float sS[XL ? kBlock / 64 : 1][2][64 / P][P][2];
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int j = tid % P, cl = tid / P;
+  const int cw = (tid & 63) / P;                  // channel within the wave
   const int c0 = blockIdx.x * CPB;
   const bool cvalid = c0 + cl < a.dim;
   const int c = cvalid ? c0 + cl : a.dim - 1;
@@ -860,9 +911,14 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
   float* __restrict__ ck0 = nck ? a.ckpt + (int64_t)b * nck * a.dim * kN : nullptr;
   const uint32_t lck = (uint32_t)(c * kN + j * NS);
 
-  RawVec<Tbc, VPT> stg;
-  auto issue_tile = [&](int t0, int buf) __attribute__((always_inline)) {
-    stg.load(st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN));
+  constexpr int SW = RawVec<Tbc, VPT>::W;     // staging dwords per thread
+  constexpr bool SHALF = VPT * (int)sizeof(Tbc) == 2;  // a single bf16
+  static_assert(SHALF || VPT * (int)sizeof(Tbc) == 4 * SW, "B/C staging is whole dwords");
+  uint32_t stg[SW];
+  auto load_bc = [&](int t0) __attribute__((always_inline)) {
+    ldg_asm<SW, SHALF>(stg, st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN));
+  };
+  auto dma_tile = [&](int t0, int buf) __attribute__((always_inline)) {
     const int t = t0 + lrow;
     const int tc = t < t_end ? t : t_begin;        // rows past the segment: any in-range row (masked)
     auto lds = [&](int q) { return (void*)&sX[buf][q][wave * 64 * EPC]; };
@@ -875,7 +931,15 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
   };
   auto stage_bc = [&](int buf) __attribute__((always_inline)) {
     float v[VPT];
-    stg.unpack(v);
+    if constexpr (sizeof(Tbc) == 4) {
+#pragma unroll
+      for (int q = 0; q < VPT; ++q) v[q] = __uint_as_float(stg[q]);
+    } else if constexpr (SHALF) {
+      v[0] = __uint_as_float(stg[0] << 16);
+    } else {
+#pragma unroll
+      for (int q = 0; q < SW; ++q) unpack_bf2(stg[q], v[2 * q], v[2 * q + 1]);
+    }
     if constexpr (VPT == 4) {
       *reinterpret_cast<float4*>(&sBC[buf][e0]) = make_float4(v[0], v[1], v[2], v[3]);
     } else if constexpr (VPT == 2) {
@@ -918,13 +982,18 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
     }
   };
 
-  auto compute_tile = [&](auto tail, int t0, int buf) __attribute__((always_inline)) {
+  auto compute_tile = [&](auto tail, int t0, int buf, int bb) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail)::value;
 #ifdef MTTS_DIAG_NOCOMPUTE
     return;
 #endif
+    // publish a group's (delta, delta*u) pairs (XL) for the lanes of the channel
+    auto put = [&](int pb, const Scal& v) __attribute__((always_inline)) {
+      if constexpr (XL) *reinterpret_cast<float2*>(&sS[wave][pb][cw][j][0]) = make_float2(v.dt, v.dtu);
+    };
     Scal cur;
     scalar(tail, t0, buf, 0, cur);
+    put(0, cur);
     static_for<G>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
       const int tg = t0 + g * P;
@@ -936,25 +1005,35 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
           store_vec<NS>(ck0 + (int64_t)(tg / kSub) * a.dim * kN + lck, hv);
         }
       }
-      // (1) this group's B / C rows, issued first
+      // (2) first: delta / delta*u of the group's P steps to every lane of the channel:
+      // XL from the LDS exchange (published one group ahead), else DPP broadcasts
+      float dts[P], dtus[P];
+      if constexpr (XL) {
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < P / 2; ++q) {
+          const f4 v = *reinterpret_cast<const f4*>(&sS[wave][g & 1][cw][2 * q][0]);
+          dts[2 * q] = v[0]; dtus[2 * q] = v[1]; dts[2 * q + 1] = v[2]; dtus[2 * q + 1] = v[3];
+        }
+      } else {
+        static_for<P>([&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          dts[s] = MTTS_DIAG_NODPP ? cur.dt : group_bcast<P, s>(cur.dt);
+          dtus[s] = MTTS_DIAG_NODPP ? cur.dtu + s : group_bcast<P, s>(cur.dtu);
+          asm volatile("" : "+v"(dts[s]), "+v"(dtus[s]));
+        });
+      }
+      // (1) this group's B / C rows (their latency hides under the exponentials)
       f4 Bq[P][NS / 4], Cq[P][NS / 4];
 #pragma unroll
       for (int s = 0; s < P; ++s) {
-        const float* bc = &sBC[buf][(g * P + s) * 2 * kN + j * NS];
+        const float* bc = &sBC[bb][(g * P + s) * 2 * kN + j * NS];
 #pragma unroll
         for (int q = 0; q < NS / 4; ++q) {
           Bq[s][q] = *reinterpret_cast<const f4*>(bc + 4 * q);
           if constexpr (MODE == kFull) Cq[s][q] = *reinterpret_cast<const f4*>(bc + kN + 4 * q);
         }
       }
-      // (2) delta / delta*u of the group's P steps to every lane of the channel
-      float dts[P], dtus[P];
-      static_for<P>([&](auto sc) {
-        constexpr int s = decltype(sc)::value;
-        dts[s] = MTTS_DIAG_NODPP ? cur.dt : group_bcast<P, s>(cur.dt);
-        dtus[s] = MTTS_DIAG_NODPP ? cur.dtu + s : group_bcast<P, s>(cur.dtu);
-        asm volatile("" : "+v"(dts[s]), "+v"(dtus[s]));
-      });
       // (3) all exponentials of the group (independent of the recurrence)
       f2 e[P][NP2];
 #pragma unroll
@@ -964,9 +1043,14 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
           const f2 x = f2{dts[s], dts[s]} * A2[p];
           e[s][p] = MTTS_DIAG_NOEXP ? x : f2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
         }
-      // (4) next group's scalar work, off the chain
+      // (4) next group's scalar work, off the chain (XL: kept behind the
+      // exponentials so its LDS reads do not wait on this group's B/C reads)
+      if constexpr (XL) __builtin_amdgcn_sched_barrier(0);
       Scal nxt;
-      if constexpr (g + 1 < G) scalar(tail, t0, buf, g + 1, nxt);
+      if constexpr (g + 1 < G) {
+        scalar(tail, t0, buf, g + 1, nxt);
+        put((g + 1) & 1, nxt);
+      }
       // (5) recurrence + outputs
       float yp[P];
 #pragma unroll
@@ -1001,24 +1085,38 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
 
   const int nfull = (t_end - t_begin) / TT;
   const int ntiles = (t_end - t_begin + TT - 1) / TT;
-  issue_tile(t_begin, 0);
+  // VMEM order per iteration: [stores of tile it-1] [B/C regs of tile it+1]
+  // [DMA of tile it+NB-1]; the end-of-iteration wait leaves only that DMA in
+  // flight, so tile it+1 (DMA'd an iteration earlier when NB = 3) is complete.
+  load_bc(t_begin);
+  dma_tile(t_begin, 0);
+  wait_vm<0>(stg);
   stage_bc(0);
-  wait_vmem();  // this wave's DMA chunks are in LDS
+  if constexpr (NB == 3)
+    if (ntiles > 1) dma_tile(t_begin + TT, 1);
+  int buf = 0, prev = NB - 1;
   for (int it = 0; it < ntiles; ++it) {
     const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
-    const int buf = it & 1;
     __syncthreads();  // tile it in LDS (every wave's DMA drained); outputs of tile it-1 complete
     if constexpr (MODE == kFull)
-      if (it > 0) store_tile(t0 - TT, buf ^ 1);     // read before this lane's DMA below refills the chunk
-    if (it + 1 < ntiles) issue_tile(t0 + TT, buf ^ 1);
-    if (it < nfull) compute_tile(FalseT{}, t0, buf);
-    else compute_tile(TrueT{}, t0, buf);
-    if (it + 1 < ntiles) stage_bc(buf ^ 1);
-    wait_vmem();
+      if (it > 0) store_tile(t0 - TT, prev);        // read before this lane's DMA below refills the chunk
+    const bool more = it + 1 < ntiles;
+    const bool ahead = it + NB - 1 < ntiles;
+    if (more) load_bc(t0 + TT);
+    if (ahead) dma_tile(t0 + (NB - 1) * TT, prev);  // buffer (it + NB - 1) % NB == (it - 1) % NB
+    if (it < nfull) compute_tile(FalseT{}, t0, buf, it & 1);
+    else compute_tile(TrueT{}, t0, buf, it & 1);
+    if (more) {
+      if (NB == 3 && ahead) wait_vm<NA>(stg);
+      else wait_vm<0>(stg);
+      stage_bc((it + 1) & 1);
+    }
+    prev = buf;
+    buf = buf + 1 == NB ? 0 : buf + 1;
   }
   if constexpr (MODE == kFull) {
     __syncthreads();
-    store_tile(t_begin + (ntiles - 1) * TT, (ntiles - 1) & 1);
+    store_tile(t_begin + (ntiles - 1) * TT, prev);
     if (k == K - 1 && a.last_state && cvalid) {
       float hv[NS];
 #pragma unroll
@@ -1761,10 +1859,18 @@ static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream
   const int nbx = (a->dim + kBlock / P - 1) / (kBlock / P);
   float* seg = (float*)a->workspace;
   if (wide_io_ok(a) && !getenv("MTTS_SCAN_FWD_V1")) {
-    if (pl.K > 1)
-      hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kState, SP>), dim3(nbx, a->batch, pl.K - 1),
+    if (getenv("MTTS_SCAN_XDPP")) {
+      if (pl.K > 1)
+        hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kState, SP, false>), dim3(nbx, a->batch, pl.K - 1),
+                           dim3(kBlock), 0, st, *a, pl.seg_len, seg);
+      hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kFull, SP, false>), dim3(nbx, a->batch, pl.K),
                          dim3(kBlock), 0, st, *a, pl.seg_len, seg);
-    hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kFull, SP>), dim3(nbx, a->batch, pl.K), dim3(kBlock), 0,
+      return;
+    }
+    if (pl.K > 1)
+      hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kState, SP, true>), dim3(nbx, a->batch, pl.K - 1),
+                         dim3(kBlock), 0, st, *a, pl.seg_len, seg);
+    hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kFull, SP, true>), dim3(nbx, a->batch, pl.K), dim3(kBlock), 0,
                        st, *a, pl.seg_len, seg);
     return;
   }

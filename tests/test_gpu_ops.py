@@ -34,19 +34,24 @@ def g32(a):
     return torch.from_numpy(np.asarray(a)).to(DEV, torch.float32)
 
 
-@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2", "4v1", "2v1:s2"])
+@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2", "4v1", "2v1:s2", "4d", "2d:s2"])
 def scan_p(request):
     """P (lanes per channel) and, with ':sK', a forced split of L into K
     segments for both the forward and the backward (two-pass path); 'n'
     forces the narrow (per-lane element) forward kernel instead of the
     16-byte-chunk one; 'v1' the register-staged wide forward kernel instead of
-    the LDS-DMA one."""
-    keys = ("MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_BWD_SEGS", "MTTS_SCAN_NARROW", "MTTS_SCAN_FWD_V1")
+    the LDS-DMA one; 'd' the LDS-DMA kernel with DPP broadcasts instead of
+    the LDS (delta, delta*u) exchange."""
+    keys = ("MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_BWD_SEGS", "MTTS_SCAN_NARROW", "MTTS_SCAN_FWD_V1",
+            "MTTS_SCAN_XDPP")
     old = {k: os.environ.get(k) for k in keys}
     p, _, segs = request.param.partition(":s")
     if p.endswith("v1"):
         p = p[:-2]
         os.environ["MTTS_SCAN_FWD_V1"] = "1"
+    if p.endswith("d"):
+        p = p[:-1]
+        os.environ["MTTS_SCAN_XDPP"] = "1"
     if p.endswith("n"):
         p = p[:-1]
         os.environ["MTTS_SCAN_NARROW"] = "1"
