@@ -11,12 +11,16 @@ all-reduce of the gradients.
 
 Also reported on rank 0 (same JSON line):
   roofline      selective_scan fwd at the north-star shape (B=32, L=8192,
-                d_inner=2048, N=16, bf16 I/O), HIP-event timed, HBM-bound
-  scan_fp32     the same at fp32 I/O
+                d_inner=2048, N=16) with fp32 I/O -- the reference's own
+                precision (train.py runs mamba-ssm in fp32) -- HIP-event
+                timed on the launch stream, HBM-bound
+  roofline_bf16 the same with bf16 I/O (VALU-bound: DESIGN.md section 3)
   step_mfma     the step's algorithmic FLOPs / step time vs dense bf16 peak
   decode        decode_step p50/p90 latency (C4, B=32, 12L)
   cpu_baseline  the pure-PyTorch oracle (oracle/mamba_ref.py) fwd+bwd of the
                 same 12L model on a bounded sample, host cores
+  cpu_baseline_scan  the oracle's selective_scan_ref on a bounded slice of
+                the north-star scan (one batch row: B=1, L=8192), host cores
 """
 from __future__ import annotations
 
@@ -119,7 +123,7 @@ def train_bench(args, rank, world, dev):
     return c, ms, tokens_per_s, float(loss.item())
 
 
-def scan_roofline(dtype, B=32, L=8192, D=2048, iters=10):
+def scan_roofline(dtype, B=32, L=8192, D=2048, iters=20):
     """selective_scan fwd at the north-star shape; returns (ms, bytes, GB/s)."""
     from mtts import ops
     dev = "cuda"
@@ -136,7 +140,7 @@ def scan_roofline(dtype, B=32, L=8192, D=2048, iters=10):
     bias = dt0 + torch.log(-torch.expm1(-dt0))
     out = torch.empty_like(u)
     run = lambda: ops.scan_fwd(u, delta, A, Bm, Cm, Dp, z, bias, True, out=out)  # noqa: E731
-    for _ in range(2):
+    for _ in range(3):
         run()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -189,6 +193,29 @@ def decode_bench(steps, B=32):
     lat = sorted(lat[min(100, steps // 4):])
     return {"B": B, "steps": steps, "p50_ms": lat[len(lat) // 2], "p90_ms": lat[int(len(lat) * 0.9)],
             "mode": m.decode_mode, "layers": c["n_layers"], "d_model": c["d_model"], "T_text": c["T_text"]}
+
+
+def cpu_baseline_scan(L=8192, D=2048):
+    """oracle selective_scan_ref (pure PyTorch, fp32, CPU) on a bounded slice
+    of the north-star scan (one of its 32 batch rows: B=1, L=8192,
+    d_inner=2048, N=16), softplus + z
+    gate; reported in the roofline's unit (algorithmic bytes / s, fp32 I/O)."""
+    from oracle import mamba_ref as R
+    torch.set_num_threads(min(os.cpu_count() or 1, 64))
+    g = torch.Generator().manual_seed(0)
+    N = 16
+    u, z = torch.randn(1, D, L, generator=g), torch.randn(1, D, L, generator=g)
+    delta = torch.randn(1, D, L, generator=g) * 0.1
+    Bm, Cm = torch.randn(1, N, L, generator=g), torch.randn(1, N, L, generator=g)
+    A = -torch.arange(1, N + 1, dtype=torch.float32).repeat(D, 1)
+    bias = torch.full((D,), -4.0)
+    t0 = time.perf_counter()
+    R.selective_scan_ref(u, delta, A, Bm, Cm, torch.ones(D), z, bias, True)
+    dt = time.perf_counter() - t0
+    nbytes = 4 * D * L * 4 + 2 * N * L * 4 + (D * N + 2 * D) * 4
+    return {"value": nbytes / dt / 1e9, "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/mamba_ref.py selective_scan_ref, B=1 L={L} d_inner={D} N=16 fp32, {dt:.1f}s "
+                      f"({D * L / dt / 1e6:.2f} M (b,d,l)/s)"}
 
 
 def cpu_baseline(budget_s=20.0):
@@ -257,22 +284,26 @@ def main():
     rec["step_mfma"] = {"bound": "mfma", "achieved": fl / (ms * 1e-3) / 1e12, "peak": BF16_PEAK / 1e12,
                         "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / BF16_PEAK, "flops_per_step": fl}
     if rank == 0 and not args.skip_extras:
-        sms, sb, sbw = scan_roofline(torch.bfloat16)
-        log(f"[bench] scan bf16 north-star {sms:.3f} ms {sbw / 1e9:.0f} GB/s")
-        rec["roofline"] = {"kernel": "selective_scan_fwd (north-star B=32 L=8192 d_inner=2048 N=16, bf16 I/O)",
-                           "bound": "hbm", "achieved": sbw / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                           "frac": sbw / HBM_PEAK, "traffic": pmc_traffic("bf16"), "ms": sms, "algorithmic_bytes": sb,
-                           "traffic_source": "profiles/r01_scan_pmc_summary.json (2*FETCH_SIZE+WRITE_SIZE)"}
         fms, fb, fbw = scan_roofline(torch.float32)
         log(f"[bench] scan fp32 north-star {fms:.3f} ms {fbw / 1e9:.0f} GB/s")
-        rec["scan_fp32"] = {"bound": "hbm", "achieved": fbw / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                            "frac": fbw / HBM_PEAK, "ms": fms, "algorithmic_bytes": fb, "traffic": pmc_traffic("fp32")}
+        rec["roofline"] = {"kernel": "selective_scan_fwd (north-star B=32 L=8192 d_inner=2048 N=16, fp32 I/O = the "
+                                     "reference's precision, f32 math)",
+                           "bound": "hbm", "achieved": fbw / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                           "frac": fbw / HBM_PEAK, "traffic": pmc_traffic("fp32"), "ms": fms, "algorithmic_bytes": fb,
+                           "traffic_source": "profiles/r01_scan_pmc_summary.json (2*FETCH_SIZE+WRITE_SIZE)"}
+        sms, sb, sbw = scan_roofline(torch.bfloat16)
+        log(f"[bench] scan bf16 north-star {sms:.3f} ms {sbw / 1e9:.0f} GB/s")
+        rec["roofline_bf16"] = {"bound": "hbm (VALU-limited, DESIGN.md section 3)", "achieved": sbw / 1e9,
+                                "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": sbw / HBM_PEAK, "ms": sms,
+                                "algorithmic_bytes": sb, "traffic": pmc_traffic("bf16")}
         if args.decode_steps > 0:
             rec["decode"] = decode_bench(args.decode_steps)
             log(f"[bench] decode {rec['decode']}")
         if args.cpu_budget > 0:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_budget)
             log(f"[bench] cpu {rec['cpu_baseline']}")
+            rec["cpu_baseline_scan"] = cpu_baseline_scan()
+            log(f"[bench] cpu scan {rec['cpu_baseline_scan']}")
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
