@@ -17,6 +17,8 @@ Also reported on rank 0 (same JSON line):
   roofline_bf16 the same with bf16 I/O (VALU-bound: DESIGN.md section 3)
   step_mfma     the step's algorithmic FLOPs / step time vs dense bf16 peak
   decode        decode_step p50/p90 latency (C4, B=32, 12L)
+  style         style pipeline: HIP length regulator
+                roofline, StyleConditioningPipeline eval / train times
   cpu_baseline  the pure-PyTorch oracle (oracle/mamba_ref.py) fwd+bwd of the
                 same 12L model on a bounded sample, host cores
   cpu_baseline_scan  the oracle's selective_scan_ref on a bounded slice of
@@ -195,6 +197,60 @@ def decode_bench(steps, B=32):
             "mode": m.decode_mode, "layers": c["n_layers"], "d_model": c["d_model"], "T_text": c["T_text"]}
 
 
+def style_bench(B=8, T_text=128, d_model=1024, d_style=256, iters=20):
+    """the style pipeline (style_cross_attention.py) at a
+    C5-like shape, bf16: the HIP length regulator alone (HBM roofline: it
+    moves out + in rows once) and the whole StyleConditioningPipeline, eval
+    forward (single-key attention shortcut) and train fwd+bwd."""
+    import style_cross_attention as sca
+    from mtts import ops
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(3)
+    text = torch.randn(B, T_text, d_model, device=dev, generator=g).to(torch.bfloat16)
+    style = torch.randn(B, d_style, device=dev, generator=g).to(torch.bfloat16)
+    dur = torch.randint(2, 15, (B, T_text), device=dev, generator=g).float()   # ~8 frames / phoneme
+    max_len = int(ops.length_regulate_lengths(dur).max().item())
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters
+
+    # the regulator kernel alone: 10 launches captured in a hipGraph, so the
+    # per-launch time is GPU time, not Python/ctypes launch overhead
+    with torch.no_grad():
+        ops.LengthRegulateFn.apply(text, dur, max_len)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(10):
+                ops.LengthRegulateFn.apply(text, dur, max_len)
+    reg_ms = timed(graph.replay) / 10
+    reg_bytes = B * max_len * d_model * 2 + B * T_text * d_model * 2
+    pipe = sca.StyleConditioningPipeline(d_style=d_style, d_model=d_model, num_heads=8, dropout=0.1).to(dev)
+    pipe = pipe.to(torch.bfloat16)
+    pipe.eval()
+    with torch.no_grad():
+        eval_ms = timed(lambda: pipe(text, style, dur, max_frame_len=max_len))
+    pipe.train()
+    textg = text.detach().requires_grad_(True)
+
+    def train_step():
+        frames, _, _, _ = pipe(textg, style, dur, max_frame_len=max_len)
+        frames.float().square().mean().backward()
+    train_ms = timed(train_step)
+    return {"B": B, "T_text": T_text, "T_frame": max_len, "d_model": d_model, "dtype": "bf16",
+            "regulator": {"ms": reg_ms, "bound": "hbm", "achieved": reg_bytes / reg_ms / 1e6, "peak": HBM_PEAK / 1e9,
+                          "unit": "GB/s", "frac": reg_bytes / (reg_ms * 1e-3) / HBM_PEAK},
+            "pipeline_eval_ms": eval_ms, "pipeline_train_fwd_bwd_ms": train_ms}
+
+
 def cpu_baseline_scan(L=8192, D=2048):
     """oracle selective_scan_ref (pure PyTorch, fp32, CPU) on a bounded slice
     of the north-star scan (one of its 32 batch rows: B=1, L=8192,
@@ -296,6 +352,8 @@ def main():
         rec["roofline_bf16"] = {"bound": "hbm (VALU-limited, DESIGN.md section 3)", "achieved": sbw / 1e9,
                                 "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": sbw / HBM_PEAK, "ms": sms,
                                 "algorithmic_bytes": sb, "traffic": pmc_traffic("bf16")}
+        rec["style"] = style_bench()
+        log(f"[bench] style {rec['style']}")
         if args.decode_steps > 0:
             rec["decode"] = decode_bench(args.decode_steps)
             log(f"[bench] decode {rec['decode']}")

@@ -293,6 +293,29 @@ typedef struct {
 int64_t mtts_attention_bwd_workspace(int batch, int heads, int head_dim, int q_len, int kv_len, int dtype);
 int mtts_attention_bwd(const MttsAttnBwdArgs* a, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Length regulator (phoneme -> frame expansion).  Replaces the Python loop of
+ * style_cross_attention.py:156-198 (LengthRegulator.forward: round, clamp
+ * >= 0, repeat rows, one .item() per (b, phoneme)) and its autograd.
+ *   dur[b,t]   = max(round_half_even(durations[b,t]), 0)
+ *   lengths[b] = sum_t dur[b,t]                       (int64, pre-truncation)
+ *   out[b,f,:] = hidden[b, t(f), :] for f < min(lengths[b], max_len), else 0
+ * with t(f) the phoneme whose interval [end_{t-1}, end_t) of running duration
+ * sums holds f.  The backward writes every row of dhidden:
+ *   dhidden[b,t,:] = sum_{f in [end_{t-1}, min(end_t, max_len))} dout[b,f,:]
+ * (fp32 accumulation, fixed order).  durations: fp32 (B, T) with batch stride
+ * dur_bs; hidden/out/dout/dhidden: (B, rows, D) with unit element stride,
+ * dtype MTTS_F32 / MTTS_BF16.  T <= 4096.
+ * ------------------------------------------------------------------------ */
+int mtts_length_regulate_lengths(const float* durations, int64_t dur_bs, int batch, int T, int64_t* lengths,
+                                 void* stream);
+int mtts_length_regulate_fwd(const void* hidden, int dtype, int batch, int T, int D, int64_t h_bs, int64_t h_ls,
+                             const float* durations, int64_t dur_bs, int max_len, void* out, int64_t o_bs,
+                             int64_t o_ls, void* stream);
+int mtts_length_regulate_bwd(const void* dout, int dtype, int batch, int T, int D, int64_t do_bs, int64_t do_ls,
+                             const float* durations, int64_t dur_bs, int max_len, void* dhidden, int64_t dh_bs,
+                             int64_t dh_ls, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

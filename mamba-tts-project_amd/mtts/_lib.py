@@ -115,6 +115,9 @@ _SIGS = {
     "mtts_attention_fwd": ([C.POINTER(AttnFwdArgs), vp], i32),
     "mtts_attention_bwd_workspace": ([i32, i32, i32, i32, i32, i32], i64),
     "mtts_attention_bwd": ([C.POINTER(AttnBwdArgs), vp], i32),
+    "mtts_length_regulate_lengths": ([vp, i64, i32, i32, vp, vp], i32),
+    "mtts_length_regulate_fwd": ([vp, i32, i32, i32, i32, i64, i64, vp, i64, i32, vp, i64, i64, vp], i32),
+    "mtts_length_regulate_bwd": ([vp, i32, i32, i32, i32, i64, i64, vp, i64, i32, vp, i64, i64, vp], i32),
 }
 
 _lib = None

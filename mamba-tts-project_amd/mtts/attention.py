@@ -90,6 +90,8 @@ class CrossAttention(nn.Module):
         d, H = self.embed_dim, self.num_heads
         W, b = self.in_proj_weight, self.in_proj_bias
         p_drop = self.dropout if self.training else 0.0
+        if key.shape[1] == 1 and key_padding_mask is None and p_drop == 0.0:
+            return self._single_key(query, key, value), None
         if key is value:
             q, kv = InProjFn.apply(query, key.to(cd), W, b)
             o = attn_kernels.attention_kv(q, kv, H, key_padding_mask, p_drop)
@@ -100,3 +102,22 @@ class CrossAttention(nn.Module):
             o = attn_kernels.attention(q, k, v, H, key_padding_mask, p_drop)
         out = linear(o, self.out_proj.weight, self.out_proj.bias)
         return out, None
+
+    def _single_key(self, query, key, value):
+        """One unmasked key (the style token of style_cross_attention.py:125-131,
+        270-276) and no attention dropout: softmax over a single logit is
+        exactly 1, so every query row's attention output is the value
+        projection of that key, out_proj(v) -- independent of q and k.  Only the
+        value projection and out_proj run, on B rows instead of B*Tq.  torch's
+        MHA gives the q/k in-projection rows exactly zero gradient here
+        (dS = P*(dP - rowsum(P*dP)) = 0 for one key); LinearFn's row slice
+        reproduces that for the weights, and the zero-weighted key term keeps a
+        (zero) gradient flowing to `key` so optimizer state and weight decay of
+        the key path behave as with torch MHA."""
+        cd = query.dtype
+        d = self.embed_dim
+        B, Tq = query.shape[0], query.shape[1]
+        v = linear(value.to(cd), self.in_proj_weight, self.in_proj_bias, rows=(2 * d, 3 * d))   # (B, 1, d)
+        o = linear(v, self.out_proj.weight, self.out_proj.bias)
+        o = o + 0.0 * key.to(cd).sum(dim=-1, keepdim=True)
+        return o.expand(B, Tq, d).contiguous()

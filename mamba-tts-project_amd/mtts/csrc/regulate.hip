@@ -1,0 +1,219 @@
+// Length regulator (phoneme -> frame expansion) for the style pipeline,
+// replacing the reference's per-(b, phoneme) Python loop with one .item()
+// each (style_cross_attention.py:156-198, LengthRegulator.forward):
+//   dur[b,t]   = max(round_half_even(durations[b,t]), 0)
+//   lengths[b] = sum_t dur[b,t]
+//   out[b,f,:] = hidden[b, t(f), :] for f < min(lengths[b], max_len), else 0,
+// t(f) = the phoneme whose cumulative-duration interval [end_{t-1}, end_t)
+// holds f.  The backward is the matching segment sum: dhidden[b,t,:] =
+// sum over f in [end_{t-1}, min(end_t, max_len)) of dout[b,f,:] (fixed order,
+// deterministic).  Every block re-derives the running sums of its batch row
+// in LDS (T <= 4096 phonemes), so there is no host round trip and no
+// intermediate index tensor; rows move as 16-byte vectors.
+#include "common.h"
+
+namespace mtts {
+
+constexpr int kRegMaxT = 4096;
+constexpr int kRegBlock = 256;
+
+// ends[t] = sum_{s <= t} dur[s] (int64) for one batch row, whole block.
+__device__ void dur_scan(const float* __restrict__ dur, int T, long long* ends, long long* part) {
+  const int i = threadIdx.x;
+  const int per = (T + kRegBlock - 1) / kRegBlock;
+  const int t0 = min(T, i * per), t1 = min(T, t0 + per);
+  long long s = 0;
+  for (int t = t0; t < t1; ++t) {
+    const float r = fmaxf(rintf(dur[t]), 0.f);   // torch.round (half to even), clamp(min=0)
+    s += (long long)r;
+    ends[t] = s;
+  }
+  part[i] = s;
+  __syncthreads();
+  for (int off = 1; off < kRegBlock; off <<= 1) {
+    const long long v = i >= off ? part[i - off] : 0;
+    __syncthreads();
+    part[i] += v;
+    __syncthreads();
+  }
+  const long long base = i > 0 ? part[i - 1] : 0;
+  for (int t = t0; t < t1; ++t) ends[t] += base;
+  __syncthreads();
+}
+
+template <typename T, int EV>
+struct alignas(EV == 1 ? sizeof(T) : 16) Vec {
+  T v[EV];
+};
+
+__global__ __launch_bounds__(kRegBlock) void reg_lengths_kernel(const float* __restrict__ dur, int64_t dur_bs, int T,
+                                                                int64_t* __restrict__ lengths) {
+  __shared__ long long ends[kRegMaxT];
+  __shared__ long long part[kRegBlock];
+  const int b = blockIdx.x;
+  dur_scan(dur + b * dur_bs, T, ends, part);
+  if (threadIdx.x == 0) lengths[b] = T > 0 ? ends[T - 1] : 0;
+}
+
+// one wave per output frame (fpb frames per block)
+template <typename T, int EV>
+__global__ __launch_bounds__(kRegBlock) void reg_fwd_kernel(const T* __restrict__ h, int64_t h_bs, int64_t h_ls,
+                                                            const float* __restrict__ dur, int64_t dur_bs, int nT,
+                                                            int D, int max_len, T* __restrict__ out, int64_t o_bs,
+                                                            int64_t o_ls, int fpb) {
+  __shared__ long long ends[kRegMaxT];
+  __shared__ long long part[kRegBlock];
+  const int b = blockIdx.y;
+  dur_scan(dur + b * dur_bs, nT, ends, part);
+  const long long len = nT > 0 ? ends[nT - 1] : 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nv = D / EV;
+  using V = Vec<T, EV>;
+  const int f0 = blockIdx.x * fpb;
+  const int f1 = min(max_len, f0 + fpb);
+  for (int f = f0 + w; f < f1; f += kRegBlock / 64) {
+    V* __restrict__ dst = reinterpret_cast<V*>(out + b * o_bs + (int64_t)f * o_ls);
+    if (f < len) {
+      int lo = 0, hi = nT;  // first t with ends[t] > f
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ends[mid] <= f) lo = mid + 1;
+        else hi = mid;
+      }
+      const V* __restrict__ src = reinterpret_cast<const V*>(h + b * h_bs + (int64_t)lo * h_ls);
+      for (int c = lane; c < nv; c += 64) dst[c] = src[c];
+    } else {
+      V z;
+      for (int e = 0; e < EV; ++e) reinterpret_cast<T*>(&z)[e] = T(0);
+      for (int c = lane; c < nv; c += 64) dst[c] = z;
+    }
+  }
+}
+
+// one wave per phoneme (ppb phonemes per block); fp32 accumulation
+template <typename T, int EV>
+__global__ __launch_bounds__(kRegBlock) void reg_bwd_kernel(const T* __restrict__ dout, int64_t do_bs, int64_t do_ls,
+                                                            const float* __restrict__ dur, int64_t dur_bs, int nT,
+                                                            int D, int max_len, T* __restrict__ dh, int64_t dh_bs,
+                                                            int64_t dh_ls, int ppb) {
+  __shared__ long long ends[kRegMaxT];
+  __shared__ long long part[kRegBlock];
+  const int b = blockIdx.y;
+  dur_scan(dur + b * dur_bs, nT, ends, part);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nv = D / EV;
+  using V = Vec<T, EV>;
+  const int t0 = blockIdx.x * ppb;
+  const int t1 = min(nT, t0 + ppb);
+  for (int t = t0 + w; t < t1; t += kRegBlock / 64) {
+    const long long s = t > 0 ? ends[t - 1] : 0;
+    const long long e = min(ends[t], (long long)max_len);
+    V* __restrict__ dst = reinterpret_cast<V*>(dh + b * dh_bs + (int64_t)t * dh_ls);
+    for (int c = lane; c < nv; c += 64) {
+      float acc[EV];
+#pragma unroll
+      for (int q = 0; q < EV; ++q) acc[q] = 0.f;
+      for (long long f = s; f < e; ++f) {
+        const V v = reinterpret_cast<const V*>(dout + b * do_bs + f * do_ls)[c];
+#pragma unroll
+        for (int q = 0; q < EV; ++q) acc[q] += ldf(&v.v[q]);
+      }
+      V o;
+#pragma unroll
+      for (int q = 0; q < EV; ++q) stf(&o.v[q], acc[q]);
+      dst[c] = o;
+    }
+  }
+}
+
+static bool vec_ok(int es, int D, std::initializer_list<const void*> ptrs, std::initializer_list<int64_t> strides) {
+  const int ev = 16 / es;
+  if (D % ev) return false;
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % 16) return false;
+  for (int64_t s : strides)
+    if (s % ev) return false;
+  return true;
+}
+
+}  // namespace mtts
+
+using namespace mtts;
+
+extern "C" int mtts_length_regulate_lengths(const float* durations, int64_t dur_bs, int batch, int T,
+                                            int64_t* lengths, void* stream) {
+  MTTS_CHECK(lengths && batch >= 0 && T >= 0 && (T == 0 || durations), "length_regulate: bad args");
+  MTTS_CHECK(T <= kRegMaxT, "length_regulate: T=%d phonemes > %d", T, kRegMaxT);
+  if (batch == 0) return MTTS_OK;
+  hipLaunchKernelGGL(reg_lengths_kernel, dim3(batch), dim3(kRegBlock), 0, (hipStream_t)stream, durations, dur_bs, T,
+                     lengths);
+  MTTS_LAUNCH_CHECK("length_regulate_lengths");
+  return MTTS_OK;
+}
+
+extern "C" int mtts_length_regulate_fwd(const void* hidden, int dtype, int batch, int T, int D, int64_t h_bs,
+                                        int64_t h_ls, const float* durations, int64_t dur_bs, int max_len, void* out,
+                                        int64_t o_bs, int64_t o_ls, void* stream) {
+  MTTS_CHECK(batch >= 0 && T >= 0 && D > 0 && max_len >= 0, "length_regulate: bad args");
+  MTTS_CHECK(out || batch == 0 || max_len == 0, "length_regulate: null output");
+  MTTS_CHECK(T == 0 || (hidden && durations), "length_regulate: null input");
+  MTTS_CHECK(T <= kRegMaxT, "length_regulate: T=%d phonemes > %d", T, kRegMaxT);
+  MTTS_CHECK(dtype == MTTS_F32 || dtype == MTTS_BF16, "length_regulate: bad dtype");
+  if (batch == 0 || max_len == 0) return MTTS_OK;
+  const int fpb = 16;  // 4 frames per wave: >= 256 blocks already at B=4, 1000 frames
+  dim3 grid((max_len + fpb - 1) / fpb, batch);
+  hipStream_t st = (hipStream_t)stream;
+  const int es = dtype == MTTS_F32 ? 4 : 2;
+  const bool v = vec_ok(es, D, {hidden, out}, {h_bs, h_ls, o_bs, o_ls});
+  if (dtype == MTTS_F32) {
+    if (v)
+      hipLaunchKernelGGL((reg_fwd_kernel<float, 4>), grid, dim3(kRegBlock), 0, st, (const float*)hidden, h_bs, h_ls,
+                         durations, dur_bs, T, D, max_len, (float*)out, o_bs, o_ls, fpb);
+    else
+      hipLaunchKernelGGL((reg_fwd_kernel<float, 1>), grid, dim3(kRegBlock), 0, st, (const float*)hidden, h_bs, h_ls,
+                         durations, dur_bs, T, D, max_len, (float*)out, o_bs, o_ls, fpb);
+  } else {
+    if (v)
+      hipLaunchKernelGGL((reg_fwd_kernel<bf16_t, 8>), grid, dim3(kRegBlock), 0, st, (const bf16_t*)hidden, h_bs,
+                         h_ls, durations, dur_bs, T, D, max_len, (bf16_t*)out, o_bs, o_ls, fpb);
+    else
+      hipLaunchKernelGGL((reg_fwd_kernel<bf16_t, 1>), grid, dim3(kRegBlock), 0, st, (const bf16_t*)hidden, h_bs,
+                         h_ls, durations, dur_bs, T, D, max_len, (bf16_t*)out, o_bs, o_ls, fpb);
+  }
+  MTTS_LAUNCH_CHECK("length_regulate_fwd");
+  return MTTS_OK;
+}
+
+extern "C" int mtts_length_regulate_bwd(const void* dout, int dtype, int batch, int T, int D, int64_t do_bs,
+                                        int64_t do_ls, const float* durations, int64_t dur_bs, int max_len,
+                                        void* dhidden, int64_t dh_bs, int64_t dh_ls, void* stream) {
+  MTTS_CHECK(batch >= 0 && T >= 0 && D > 0 && max_len >= 0, "length_regulate_bwd: bad args");
+  MTTS_CHECK(dhidden || batch == 0 || T == 0, "length_regulate_bwd: null output");
+  MTTS_CHECK(T == 0 || durations, "length_regulate_bwd: null durations");
+  MTTS_CHECK(max_len == 0 || dout, "length_regulate_bwd: null dout");
+  MTTS_CHECK(T <= kRegMaxT, "length_regulate_bwd: T=%d phonemes > %d", T, kRegMaxT);
+  MTTS_CHECK(dtype == MTTS_F32 || dtype == MTTS_BF16, "length_regulate_bwd: bad dtype");
+  if (batch == 0 || T == 0) return MTTS_OK;
+  const int ppb = 16;
+  dim3 grid((T + ppb - 1) / ppb, batch);
+  hipStream_t st = (hipStream_t)stream;
+  const int es = dtype == MTTS_F32 ? 4 : 2;
+  const bool v = vec_ok(es, D, {dout ? dout : dhidden, dhidden}, {do_bs, do_ls, dh_bs, dh_ls});
+  if (dtype == MTTS_F32) {
+    if (v)
+      hipLaunchKernelGGL((reg_bwd_kernel<float, 4>), grid, dim3(kRegBlock), 0, st, (const float*)dout, do_bs, do_ls,
+                         durations, dur_bs, T, D, max_len, (float*)dhidden, dh_bs, dh_ls, ppb);
+    else
+      hipLaunchKernelGGL((reg_bwd_kernel<float, 1>), grid, dim3(kRegBlock), 0, st, (const float*)dout, do_bs, do_ls,
+                         durations, dur_bs, T, D, max_len, (float*)dhidden, dh_bs, dh_ls, ppb);
+  } else {
+    if (v)
+      hipLaunchKernelGGL((reg_bwd_kernel<bf16_t, 8>), grid, dim3(kRegBlock), 0, st, (const bf16_t*)dout, do_bs,
+                         do_ls, durations, dur_bs, T, D, max_len, (bf16_t*)dhidden, dh_bs, dh_ls, ppb);
+    else
+      hipLaunchKernelGGL((reg_bwd_kernel<bf16_t, 1>), grid, dim3(kRegBlock), 0, st, (const bf16_t*)dout, do_bs,
+                         do_ls, durations, dur_bs, T, D, max_len, (bf16_t*)dhidden, dh_bs, dh_ls, ppb);
+  }
+  MTTS_LAUNCH_CHECK("length_regulate_bwd");
+  return MTTS_OK;
+}

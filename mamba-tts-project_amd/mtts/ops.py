@@ -417,3 +417,63 @@ class LayerNormFn(torch.autograd.Function):
 def layer_norm(x, w, b, eps=1e-5, res=None, gamma=None, beta=None, rows_per_group=1):
     """Returns (y, x_sum) with x_sum = x + res (an empty tensor when res is None)."""
     return LayerNormFn.apply(x, res, w, b, gamma, beta, eps, rows_per_group)
+
+
+# ---------------------------------------------------------------------------
+# length regulator (style_cross_attention.py:156-198)
+# ---------------------------------------------------------------------------
+
+def _dur_f32(durations):
+    d = durations.detach()
+    if d.dtype != torch.float32:
+        d = d.to(torch.float32)
+    return d if d.stride(-1) == 1 else d.contiguous()
+
+
+def length_regulate_lengths(durations):
+    """lengths[b] = sum_t max(round(durations[b,t]), 0) as int64, on device."""
+    _check_cuda(durations)
+    d = _dur_f32(durations)
+    B, T = d.shape
+    out = torch.empty(B, device=d.device, dtype=torch.int64)
+    L.call_raw("mtts_length_regulate_lengths", d.data_ptr(), d.stride(0), B, T, out.data_ptr())
+    return out
+
+
+class LengthRegulateFn(torch.autograd.Function):
+    """out = hidden rows repeated by rounded, clamped durations, zero-padded
+    to max_len; backward = per-phoneme segment sums of dout."""
+
+    @staticmethod
+    def forward(ctx, hidden, durations, max_len):
+        _check_cuda(hidden, durations)
+        h = hidden if hidden.stride(-1) == 1 else hidden.contiguous()
+        d = _dur_f32(durations)
+        B, T, D = h.shape
+        out = torch.empty(B, max_len, D, device=h.device, dtype=h.dtype)
+        L.call_raw("mtts_length_regulate_fwd", h.data_ptr(), L.dtype_code(h), B, T, D, h.stride(0), h.stride(1),
+                   d.data_ptr(), d.stride(0), max_len, out.data_ptr(), out.stride(0), out.stride(1))
+        ctx.save_for_backward(d)
+        ctx.meta = (T, max_len)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (d,) = ctx.saved_tensors
+        T, max_len = ctx.meta
+        g = dout if dout.stride(-1) == 1 else dout.contiguous()
+        B, _, D = g.shape
+        dh = torch.empty(B, T, D, device=g.device, dtype=g.dtype)
+        L.call_raw("mtts_length_regulate_bwd", g.data_ptr(), L.dtype_code(g), B, T, D, g.stride(0), g.stride(1),
+                   d.data_ptr(), d.stride(0), max_len, dh.data_ptr(), dh.stride(0), dh.stride(1))
+        return dh, None, None
+
+
+def length_regulate(hidden, durations, max_len=None):
+    """(expanded (B, max_len, D), lengths (B,) int64).  With max_len None the
+    output is as long as the longest row (one device->host read, as in the
+    reference's output_lengths.max().item())."""
+    lengths = length_regulate_lengths(durations)
+    if max_len is None:
+        max_len = int(lengths.max().item()) if lengths.numel() > 0 else 0
+    return LengthRegulateFn.apply(hidden, durations, int(max_len)), lengths

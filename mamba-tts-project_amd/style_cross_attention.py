@@ -9,9 +9,10 @@ Implements:
 4. Length Regulator (phoneme-level → frame-level)          (reference :144-212)
 
 Arithmetic runs on libmtts kernels: fused residual-add + LayerNorm, the HIP
-attention core, and a host-sync-free LengthRegulator gather (the reference
-loops over (b, phoneme) with one .item() each, :185-196); only the output
-length needs one device->host read when max_len is None, as in the reference.
+attention core, and the HIP length regulator (mtts_length_regulate_*: the
+reference loops over (b, phoneme) with one .item() each, :185-196); only the
+output length needs one device->host read when max_len is None, as in the
+reference.
 """
 
 import torch
@@ -93,19 +94,10 @@ class LengthRegulator(nn.Module):
         super().__init__()
 
     def forward(self, hidden, durations, max_len=None):
-        B, T, D = hidden.shape
-        durations = torch.clamp(torch.round(durations), min=0).long()
-        output_lengths = durations.sum(dim=1)
-        if max_len is None:
-            max_len = int(output_lengths.max().item()) if B > 0 else 0
-        ends = torch.cumsum(durations, dim=1)                                   # (B, T)
-        pos = torch.arange(max_len, device=hidden.device)[None].expand(B, -1).contiguous()
-        idx = torch.searchsorted(ends, pos, right=True)                          # phoneme of each frame
-        valid = pos < output_lengths[:, None]
-        idx = idx.clamp(max=max(T - 1, 0))
-        expanded = torch.gather(hidden, 1, idx[..., None].expand(B, max_len, D))
-        expanded = expanded * valid[..., None].to(hidden.dtype)
-        return expanded, output_lengths
+        """hidden (B, T_text, d), durations (B, T_text) -> (expanded (B, T_frame, d),
+        output_lengths (B,)), reference :156-198; one HIP kernel for the lengths
+        and one for the gather (mtts_length_regulate_*)."""
+        return ops.length_regulate(hidden, durations, max_len)
 
     def forward_with_target(self, hidden, target_durations):
         return self.forward(hidden, target_durations)

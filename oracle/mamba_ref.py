@@ -158,6 +158,25 @@ def mha_ref(q_in, kv_in, in_w, in_b, out_w, out_b, n_heads, key_padding_mask=Non
     return o @ out_w.T + out_b
 
 
+def length_regulator_ref(hidden, durations, max_len=None):
+    """Restates style_cross_attention.py:156-198 (LengthRegulator.forward):
+    durations rounded half-to-even (torch.round) and clamped >= 0; row b of
+    the output repeats hidden[b, t] dur[b, t] times, in order, truncated to
+    max_len and zero-padded; lengths are the untruncated sums (int64)."""
+    Bsz, T, D = hidden.shape
+    dur = torch.clamp(torch.round(durations), min=0).long()
+    lengths = dur.sum(dim=1)
+    if max_len is None:
+        max_len = int(lengths.max().item()) if Bsz > 0 else 0
+    rows = []
+    for b in range(Bsz):
+        idx = [t for t in range(T) for _ in range(int(dur[b, t]))][:max_len]
+        r = hidden[b, idx] if idx else hidden.new_zeros(0, D)
+        rows.append(torch.cat([r, hidden.new_zeros(max_len - len(idx), D)], 0))
+    out = torch.stack(rows) if rows else hidden.new_zeros(0, max_len, D)
+    return out, lengths
+
+
 # --------------------------------------------------------------------------
 # Module-level restatements (state_dict keys identical to the reference)
 # --------------------------------------------------------------------------

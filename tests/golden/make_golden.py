@@ -286,9 +286,37 @@ def gen_style(msca, seed=4):
     save("style.npz", **arrays)
 
 
+def gen_regulator(msca, seed=7):
+    """Reference LengthRegulator (style_cross_attention.py:156-198) alone:
+    half-integer durations (round half to even), negatives (clamp), an
+    all-zero row, max_len None / shorter / longer than the longest row; the
+    hidden gradient of sum(expanded * w) through the reference loop."""
+    g = torch.Generator().manual_seed(seed)
+    reg = msca.LengthRegulator()
+    B, Tt, D = 4, 9, 24
+    hidden = rnd(g, B, Tt, D)
+    dur = torch.randint(0, 6, (B, Tt), generator=g).double()
+    dur[0, :4] = torch.tensor([0.5, 1.5, 2.5, 3.5], dtype=torch.float64)
+    dur[1, 2], dur[1, 5] = -2.0, 0.49
+    dur[2] = 0.0
+    dur[3, 0] = 4.6
+    arrays = dict(hidden=f32(hidden), durations=f32(dur))
+    for tag, ml in (("none", None), ("short", 6), ("long", 40)):
+        h = hidden.clone().requires_grad_(True)
+        out, lengths = reg(h, dur, max_len=ml)
+        w = rnd(g, *out.shape)
+        (out * w).sum().backward()
+        arrays.update({f"{tag}/out": f32(out.detach()), f"{tag}/lengths": lengths.numpy(), f"{tag}/w": f32(w),
+                       f"{tag}/dhidden": f32(h.grad)})
+    save("regulator.npz", **arrays)
+
+
 def main():
     torch.set_num_threads(8)
     mdec, msca = import_reference()
+    if sys.argv[1:] == ["regulator"]:
+        gen_regulator(msca)
+        return
     gen_scan("scan_full.npz", 2, 64, 256)
     gen_scan("scan_plain.npz", 1, 32, 512, use_z=False, use_D=False, use_bias=False, softplus=False, seed=5)
     gen_scan("scan_short.npz", 3, 16, 3, seed=6)
@@ -296,6 +324,7 @@ def main():
     gen_state_update()
     gen_decoder(mdec)
     gen_style(msca)
+    gen_regulator(msca)
 
 
 if __name__ == "__main__":
