@@ -316,6 +316,29 @@ int mtts_length_regulate_bwd(const void* dout, int dtype, int batch, int T, int 
                              const float* durations, int64_t dur_bs, int max_len, void* dhidden, int64_t dh_bs,
                              int64_t dh_ls, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Compute-dtype weight copies for the decoder's GEMMs, one launch per step:
+ * for every descriptor, the contiguous fp32 master src (rows x cols) is
+ * rounded (RNE) to bf16 into dst (rows x cols, contiguous) and, when dstT is
+ * not NULL, into dstT = src^T (cols x rows, contiguous).  Stands in for the
+ * per-parameter `.to(bfloat16)` casts an autocast region would make of the
+ * reference's fp32 nn.Linear / nn.MultiheadAttention weights
+ * (mamba_decoder.py:26-48, mamba_ssm Mamba projections); dstT feeds the
+ * data-gradient GEMMs.  `descs` is a DEVICE array of n descriptors sorted
+ * by tile0, where tile0 is the running sum of mtts_cast_tiles(rows, cols)
+ * of the descriptors before it; total_tiles is the sum over all.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  const float* src;
+  void* dst;
+  void* dstT;       /* may be NULL */
+  int rows, cols;
+  int64_t tile0;
+} MttsCastDesc;
+
+int64_t mtts_cast_tiles(int rows, int cols);
+int mtts_cast_bf16_multi(const MttsCastDesc* descs, int n, int64_t total_tiles, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

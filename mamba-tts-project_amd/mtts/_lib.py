@@ -95,6 +95,10 @@ class AttnBwdArgs(C.Structure):
                 ("dv", vp), ("dv_bs", i64), ("dv_ls", i64), ("workspace", vp)]
 
 
+class CastDesc(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("dstT", vp), ("rows", i32), ("cols", i32), ("tile0", i64)]
+
+
 _SIGS = {
     "mtts_abi_version": ([], i32),
     "mtts_last_error": ([], C.c_char_p),
@@ -115,6 +119,8 @@ _SIGS = {
     "mtts_attention_fwd": ([C.POINTER(AttnFwdArgs), vp], i32),
     "mtts_attention_bwd_workspace": ([i32, i32, i32, i32, i32, i32], i64),
     "mtts_attention_bwd": ([C.POINTER(AttnBwdArgs), vp], i32),
+    "mtts_cast_tiles": ([i32, i32], i64),
+    "mtts_cast_bf16_multi": ([vp, i32, i64, vp], i32),
     "mtts_length_regulate_lengths": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_length_regulate_fwd": ([vp, i32, i32, i32, i32, i64, i64, vp, i64, i32, vp, i64, i64, vp], i32),
     "mtts_length_regulate_bwd": ([vp, i32, i32, i32, i32, i64, i64, vp, i64, i32, vp, i64, i64, vp], i32),

@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import attn_kernels
-from .linear import cast_scope, cast_weight, colsum, linear, wgrad
+from .linear import _want_t, cast_scope, cast_weight, cast_weight_t, colsum, linear, wgrad
 
 
 class InProjFn(torch.autograd.Function):
@@ -36,6 +36,7 @@ class InProjFn(torch.autograd.Function):
         q = torch.addmm(bc[:d], x2, Wc[:d].t())
         kv = torch.addmm(bc[d:], k2, Wc[d:].t())
         ctx.save_for_backward(x2, k2, Wc)
+        ctx.weight = weight
         ctx.meta = (query.shape, key.shape, weight.dtype, bias.dtype)
         return q.view(*query.shape[:-1], d), kv.view(*key.shape[:-1], 2 * d)
 
@@ -46,8 +47,13 @@ class InProjFn(torch.autograd.Function):
         d = x2.shape[1]
         dq2 = dq.reshape(-1, d).to(Wc.dtype)
         dkv2 = dkv.reshape(-1, 2 * d).to(Wc.dtype)
-        dquery = (dq2 @ Wc[:d]).view(qshape) if ctx.needs_input_grad[0] else None
-        dkey = (dkv2 @ Wc[d:]).view(kshape) if ctx.needs_input_grad[1] else None
+        if Wc.dtype == torch.bfloat16 and _want_t(ctx.weight):
+            Wt = cast_weight_t(ctx.weight, Wc.dtype)       # (d, 3d): dgrads as dy @ (W^T)^T
+            dquery = (dq2 @ Wt[:, :d].t()).view(qshape) if ctx.needs_input_grad[0] else None
+            dkey = (dkv2 @ Wt[:, d:].t()).view(kshape) if ctx.needs_input_grad[1] else None
+        else:
+            dquery = (dq2 @ Wc[:d]).view(qshape) if ctx.needs_input_grad[0] else None
+            dkey = (dkv2 @ Wc[d:]).view(kshape) if ctx.needs_input_grad[1] else None
         dW = db = None
         if ctx.needs_input_grad[2]:
             dW = torch.empty(3 * d, d, device=x2.device, dtype=torch.float32)

@@ -1814,7 +1814,10 @@ static FwdPlan plan_fwd(int batch, int dim, int seqlen) {
   FwdPlan pl;
   pl.P = pick_p(batch, dim);
   const int64_t lanes = (int64_t)batch * dim * pl.P;
-  int K = (int)((262144 + lanes - 1) / lanes);  // >= 4 waves per SIMD on 1024 SIMDs
+  // >= 1 wave per SIMD on 1024 SIMDs: the LDS-DMA forward keeps its memory
+  // pipeline full at one wave per SIMD, so extra state passes only cost
+  // (C2, B*D = 16384: one pass 0.181 ms vs K = 4 0.195 ms, tools/scan_segs.py)
+  int K = (int)((65536 + lanes - 1) / lanes);
   K = std::max(1, std::min(K, seqlen / 128));
   if (const char* e = getenv("MTTS_SCAN_SEGS")) K = std::max(1, atoi(e));
   int seg = (seqlen + K - 1) / K;

@@ -11,11 +11,13 @@ tools/bench_gemm.py).  Two things are done differently from nn.Linear:
 * bias gradients are a HIP column sum (mtts_colsum) with fp32 accumulation.
 
 Weights are fp32 masters.  Their compute-dtype copies are refreshed once per
-top-level forward (`cast_scope`): the decoder casts every GEMM weight with
-one multi-tensor copy into persistent buffers, nested module calls reuse
-them, and the backward uses the copies saved by the forward.  (Version
-counters are not used: fused optimizers update parameters without bumping
-them.)
+top-level forward (`cast_scope`): the decoder casts every GEMM weight in ONE
+HIP launch (mtts_cast_bf16_multi) into persistent buffers, writing for the
+large 2-D weights a transposed bf16 copy W^T as well; nested module calls
+reuse them.  The forward runs x @ W^T on W (hipBLASLt "NT"), the data
+gradient dy @ W on W^T (again "NT": 1.1-1.4 PF/s on these shapes vs
+0.9-1.2 for the "NN" form, tools/bench_gemm.py).  (Version counters are not
+used: fused optimizers update parameters without bumping them.)
 """
 from __future__ import annotations
 
@@ -26,15 +28,62 @@ import torch
 from . import _lib as L
 
 _scope = {"token": 0, "depth": 0}
+_cast_plans = {}
+TRANSPOSE_MIN = 512   # weights with both dims >= this also get a W^T copy
+
+
+def _want_t(p):
+    return p.dim() == 2 and min(p.shape) >= TRANSPOSE_MIN
+
+
+def _cast_multi_bf16(params):
+    """One mtts_cast_bf16_multi launch: W -> bf16 W (and W^T) for all params."""
+    key = tuple((p.data_ptr(), tuple(p.shape)) for p in params)
+    plan = _cast_plans.get(key)
+    if plan is None:
+        descs = (L.CastDesc * len(params))()
+        bufs = []
+        tile0 = 0
+        for i, p in enumerate(params):
+            ent = getattr(p, "_mtts_cast", None)
+            buf = ent[1] if (ent is not None and ent[1].dtype == torch.bfloat16 and ent[1].shape == p.shape) else \
+                torch.empty(p.shape, device=p.device, dtype=torch.bfloat16)
+            bt = None
+            if _want_t(p):
+                ent = getattr(p, "_mtts_castT", None)
+                tshape = (p.shape[1], p.shape[0])
+                bt = ent[1] if (ent is not None and ent[1].shape == tshape) else \
+                    torch.empty(tshape, device=p.device, dtype=torch.bfloat16)
+            rows, cols = (p.shape[0], p.shape[1]) if p.dim() == 2 else (1, p.numel())
+            descs[i].src, descs[i].dst, descs[i].dstT = p.data_ptr(), buf.data_ptr(), L.ptr(bt)
+            descs[i].rows, descs[i].cols, descs[i].tile0 = rows, cols, tile0
+            tile0 += L.lib().mtts_cast_tiles(rows, cols)
+            bufs.append((buf, bt))
+        raw = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(params[0].device)
+        plan = (raw, bufs, tile0)
+        _cast_plans[key] = plan
+    raw, bufs, total = plan
+    L.call_raw("mtts_cast_bf16_multi", raw.data_ptr(), len(params), total)
+    tok = _scope["token"]
+    for p, (b, bt) in zip(params, bufs):
+        p._mtts_cast = (tok, b)
+        if bt is not None:
+            p._mtts_castT = (tok, bt)
 
 
 @contextlib.contextmanager
 def cast_scope(params=None, dtype=None):
     """Open a weight-cast scope; the outermost scope invalidates all cached
-    casts and (optionally) pre-casts `params` to `dtype` in one foreach copy."""
+    casts and (optionally) pre-casts `params` to `dtype` (bf16: one HIP
+    launch, with W^T copies; otherwise one foreach copy)."""
     if _scope["depth"] == 0:
         _scope["token"] += 1
-        if params is not None and dtype is not None:
+        fast = (params is not None and dtype == torch.bfloat16 and len(params) > 0 and
+                all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.dim() in (1, 2)
+                    for p in params))
+        if fast:
+            _cast_multi_bf16(list(params))
+        elif params is not None and dtype is not None:
             src = [p for p in params if p.dtype != dtype and p.is_cuda]
             dst = []
             for p in src:
@@ -68,6 +117,17 @@ def cast_weight(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     else:
         t = w.detach().to(dtype)
     w._mtts_cast = (_scope["token"], t)
+    return t
+
+
+def cast_weight_t(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Contiguous compute-dtype W^T (cols x rows) for the current cast scope
+    (made by the scope's multi-tensor cast, else transposed here)."""
+    ent = getattr(w, "_mtts_castT", None)
+    if ent is not None and ent[0] == _scope["token"] and ent[1].dtype == dtype:
+        return ent[1]
+    t = cast_weight(w, dtype).t().contiguous()
+    w._mtts_castT = (_scope["token"], t)
     return t
 
 
@@ -124,6 +184,7 @@ class LinearFn(torch.autograd.Function):
         else:
             y = x2 @ w.t()
         ctx.save_for_backward(x2, w)
+        ctx.weight = weight
         ctx.meta = (x.shape, weight.shape, weight.dtype, None if bias is None else bias.dtype, r0, r1)
         return y.view(*x.shape[:-1], w.shape[0])
 
@@ -134,7 +195,15 @@ class LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if dy2.dtype != w.dtype:
             dy2 = dy2.to(w.dtype)
-        dx = (dy2 @ w).view(xshape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if w.dtype == torch.bfloat16 and _want_t(ctx.weight):
+                wt = cast_weight_t(ctx.weight, w.dtype)        # (k, n): dy @ (W^T)^T, the fast operand layout
+                if r0 is not None:
+                    wt = wt[:, r0:r1]
+                dx = (dy2 @ wt.t()).view(xshape)
+            else:
+                dx = (dy2 @ w).view(xshape)
         dW = db = None
         if ctx.needs_input_grad[1]:
             g = wgrad(dy2, x2).to(wdt)

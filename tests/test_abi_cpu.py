@@ -34,7 +34,7 @@ STRUCTS = {
     "MttsScanFwdArgs": "ScanFwdArgs", "MttsScanBwdArgs": "ScanBwdArgs", "MttsConvFwdArgs": "ConvFwdArgs",
     "MttsConvBwdArgs": "ConvBwdArgs", "MttsConvUpdateArgs": "ConvUpdateArgs",
     "MttsStateUpdateArgs": "StateUpdateArgs", "MttsLNArgs": "LNArgs", "MttsLNBwdArgs": "LNBwdArgs",
-    "MttsAttnFwdArgs": "AttnFwdArgs", "MttsAttnBwdArgs": "AttnBwdArgs",
+    "MttsAttnFwdArgs": "AttnFwdArgs", "MttsAttnBwdArgs": "AttnBwdArgs", "MttsCastDesc": "CastDesc",
 }
 
 

@@ -306,3 +306,25 @@ def test_linear_fn_grads(dtype):
     close(x.grad.float(), xr.grad, rtol=tol, name="dx")
     close(w.grad, wr.grad, rtol=tol, name="dw")
     close(b.grad, br.grad, rtol=tol, name="db")
+
+
+@pytest.mark.parametrize("shapes", [[(4096, 1024), (10, 1024), (96, 2048), (3000,), (2048, 64), (1024, 1024)],
+                                    [(130, 70), (64, 64), (5,), (513, 520)]])
+def test_cast_bf16_multi(shapes):
+    """mtts_cast_bf16_multi (one launch over a parameter list) == torch's RNE
+    .to(bfloat16) and its transpose, exact, for full / ragged tiles and 1-D."""
+    from mtts import _lib as L
+    from mtts.linear import _cast_multi_bf16, _want_t, TRANSPOSE_MIN
+    torch.manual_seed(0)
+    ps = [torch.randn(*s, device=DEV) * 3 for s in shapes]
+    _cast_multi_bf16(ps)
+    for p in ps:
+        ref = p.to(torch.bfloat16)
+        assert torch.equal(p._mtts_cast[1], ref)
+        if _want_t(p):
+            assert torch.equal(p._mtts_castT[1], ref.t().contiguous())
+        elif p.dim() == 2 and min(p.shape) < TRANSPOSE_MIN:
+            assert getattr(p, "_mtts_castT", None) is None
+    ps[0].add_(1.0)                # a later step re-casts the same buffers in place
+    _cast_multi_bf16(ps)
+    assert torch.equal(ps[0]._mtts_cast[1], ps[0].to(torch.bfloat16))
