@@ -339,6 +339,34 @@ typedef struct {
 int64_t mtts_cast_tiles(int rows, int cols);
 int mtts_cast_bf16_multi(const MttsCastDesc* descs, int n, int64_t total_tiles, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Fused gradient clipping + Adam over a parameter list (train.py:232-235:
+ * torch.nn.utils.clip_grad_norm_(params, max_norm) then torch.optim.Adam
+ * .step(), default Adam: L2 weight_decay, no amsgrad).  With max_norm > 0
+ * the update uses g * min(1, max_norm / (||g||_2 + 1e-6)) (gradients are not
+ * rewritten); max_norm <= 0 disables clipping.  `tensors` is a DEVICE array
+ * of n fp32 tensors (p, g, exp_avg, exp_avg_sq: numel each), sorted by
+ * chunk0 = running sum of mtts_adam_chunks(numel).  step_counter (device
+ * int32) holds the steps taken; the call increments it and derives the bias
+ * corrections from it on the device (graph-replayable).  norm_out (device,
+ * 4 floats) receives {total grad norm, clip coefficient, lr/(1-b1^t),
+ * sqrt(1-b2^t)}.  Deterministic.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t n;
+  int64_t chunk0;
+} MttsAdamTensor;
+
+int64_t mtts_adam_chunks(int64_t numel);
+int64_t mtts_adam_workspace(int64_t total_chunks);
+int mtts_clip_adam(const MttsAdamTensor* tensors, int ntensors, int64_t total_chunks, int* step_counter, float lr,
+                   float beta1, float beta2, float eps, float weight_decay, float max_norm, void* workspace,
+                   float* norm_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,6 +99,10 @@ class CastDesc(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("dstT", vp), ("rows", i32), ("cols", i32), ("tile0", i64)]
 
 
+class AdamTensor(C.Structure):
+    _fields_ = [("p", vp), ("g", vp), ("m", vp), ("v", vp), ("n", i64), ("chunk0", i64)]
+
+
 _SIGS = {
     "mtts_abi_version": ([], i32),
     "mtts_last_error": ([], C.c_char_p),
@@ -119,6 +123,9 @@ _SIGS = {
     "mtts_attention_fwd": ([C.POINTER(AttnFwdArgs), vp], i32),
     "mtts_attention_bwd_workspace": ([i32, i32, i32, i32, i32, i32], i64),
     "mtts_attention_bwd": ([C.POINTER(AttnBwdArgs), vp], i32),
+    "mtts_adam_chunks": ([i64], i64),
+    "mtts_adam_workspace": ([i64], i64),
+    "mtts_clip_adam": ([vp, i32, i64, vp, f32, f32, f32, f32, f32, f32, vp, vp, vp], i32),
     "mtts_cast_tiles": ([i32, i32], i64),
     "mtts_cast_bf16_multi": ([vp, i32, i64, vp], i32),
     "mtts_length_regulate_lengths": ([vp, i64, i32, i32, vp, vp], i32),
