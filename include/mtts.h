@@ -367,6 +367,22 @@ int mtts_clip_adam(const MttsAdamTensor* tensors, int ntensors, int64_t total_ch
                    float beta1, float beta2, float eps, float weight_decay, float max_norm, void* workspace,
                    float* norm_out, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Embedding sum of the decoder prologue (mamba_decoder.py:167-171:
+ * token_embed(tokens) + pos_embed(arange(T)) + quant_embed(quant_ids)) and of
+ * the reference-voice path (train.py:115-131 embed_codec_tokens: positions
+ * arange(T_ref).repeat(Q), quantizers arange(Q).repeat_interleave(T_ref)):
+ *   out[b,l,:] = tok_w[tokens[b,l]] + q_w[quant_ids[l]] + pos_w[pos_ids[l]]
+ * tokens int64 (B, L) with batch stride tok_bs; quant_ids / pos_ids int32
+ * (L) shared by the batch; tables fp32 contiguous (rows x d), d % 4 == 0;
+ * out (B, L, d) contiguous rows, batch stride out_bs, dtype MTTS_F32/BF16.
+ * A token outside [0, vocab) sets *err_flag = 1 (device int32, caller
+ * zeroed) and leaves its row unwritten (nn.Embedding raises).
+ * ------------------------------------------------------------------------ */
+int mtts_embed_sum(const int64_t* tokens, int64_t tok_bs, const int* quant_ids, const int* pos_ids,
+                   const float* tok_w, const float* q_w, const float* pos_w, int batch, int L, int d, int vocab,
+                   void* out, int dtype, int64_t out_bs, int* err_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -184,11 +184,10 @@ class MambaTTSDecoder(nn.Module):
         if audio_tokens.dim() == 3:
             B, Q, T = audio_tokens.shape
             audio_tokens = audio_tokens.reshape(B, Q * T)
-            quant_ids = torch.arange(Q, device=audio_tokens.device).repeat_interleave(T)
-            quant_ids = quant_ids.unsqueeze(0).expand(B, -1)
+            quant_ids = torch.arange(Q, device=audio_tokens.device).repeat_interleave(T)   # per position
         elif audio_tokens.dim() == 2:
             B, T = audio_tokens.shape
-            quant_ids = torch.zeros_like(audio_tokens)
+            quant_ids = torch.zeros(T, device=audio_tokens.device, dtype=torch.long)
         else:
             raise ValueError("audio_tokens must be (B, T) or (B, Q, T)")
         device = audio_tokens.device
@@ -202,8 +201,9 @@ class MambaTTSDecoder(nn.Module):
         text_hidden, text_mask = self._concat_ref(text_hidden, text_mask, ref_hidden, ref_mask, B, device)
 
         # token + position + quantizer embeddings (:201-206), fused backward
-        if T > self.pos_embed.num_embeddings:
-            raise IndexError(f"sequence length {T} exceeds pos_embed max_len {self.pos_embed.num_embeddings}")
+        if audio_tokens.shape[1] > self.pos_embed.num_embeddings:
+            raise IndexError(f"sequence length {audio_tokens.shape[1]} exceeds pos_embed max_len "
+                             f"{self.pos_embed.num_embeddings}")
         x = embed_sum(audio_tokens, quant_ids, self.token_embed.weight, self.quant_embed.weight,
                       self.pos_embed.weight, cd)
 

@@ -126,6 +126,7 @@ _SIGS = {
     "mtts_adam_chunks": ([i64], i64),
     "mtts_adam_workspace": ([i64], i64),
     "mtts_clip_adam": ([vp, i32, i64, vp, f32, f32, f32, f32, f32, f32, vp, vp, vp], i32),
+    "mtts_embed_sum": ([vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, i32, i64, vp, vp], i32),
     "mtts_cast_tiles": ([i32, i32], i64),
     "mtts_cast_bf16_multi": ([vp, i32, i64, vp], i32),
     "mtts_length_regulate_lengths": ([vp, i64, i32, i32, vp, vp], i32),

@@ -217,3 +217,68 @@ extern "C" int mtts_length_regulate_bwd(const void* dout, int dtype, int batch, 
   MTTS_LAUNCH_CHECK("length_regulate_bwd");
   return MTTS_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Embedding sum (mamba_decoder.py:167-171 prologue, train.py:115-131
+// embed_codec_tokens):  out[b,l,:] = tok_w[tok[b,l]] + q_w[qid[l]] + pos_w[pid[l]]
+// fp32 tables (the master parameters), int64 token ids, int32 per-position
+// quantizer / position ids shared by the batch; one wave per output row,
+// float4 table reads, fp32 sum, out in f32 or bf16.
+namespace mtts {
+
+template <typename T>
+__global__ __launch_bounds__(256) void embed_sum_kernel(const int64_t* __restrict__ tok, int64_t tok_bs,
+                                                        const int* __restrict__ qid, const int* __restrict__ pid,
+                                                        const float* __restrict__ tw, const float* __restrict__ qw,
+                                                        const float* __restrict__ pw, int L, int d, int V, int rpb,
+                                                        T* __restrict__ out, int64_t o_bs, int* __restrict__ err) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l0 = blockIdx.x * rpb;
+  for (int l = l0 + w; l < min(L, l0 + rpb); l += 4) {
+    const int64_t t = tok[b * tok_bs + l];
+    if (t < 0 || t >= V) {
+      if (lane == 0) err[0] = 1;  // nn.Embedding would raise; the host checks the flag
+      continue;
+    }
+    const float4* __restrict__ a = reinterpret_cast<const float4*>(tw + t * d);
+    const float4* __restrict__ q = reinterpret_cast<const float4*>(qw + (int64_t)qid[l] * d);
+    const float4* __restrict__ p = reinterpret_cast<const float4*>(pw + (int64_t)pid[l] * d);
+    T* __restrict__ o = out + b * o_bs + (int64_t)l * d;
+    for (int c = lane; c < d / 4; c += 64) {
+      const float4 x = a[c], y = q[c], z = p[c];
+      const float s0 = (x.x + z.x) + y.x, s1 = (x.y + z.y) + y.y, s2 = (x.z + z.z) + y.z, s3 = (x.w + z.w) + y.w;
+      if constexpr (sizeof(T) == 4) {
+        reinterpret_cast<float4*>(o)[c] = make_float4(s0, s1, s2, s3);
+      } else {
+        reinterpret_cast<uint2*>(o)[c] =
+            make_uint2((uint32_t)f2bf(s0) | ((uint32_t)f2bf(s1) << 16), (uint32_t)f2bf(s2) | ((uint32_t)f2bf(s3) << 16));
+      }
+    }
+  }
+}
+
+}  // namespace mtts
+
+extern "C" int mtts_embed_sum(const int64_t* tokens, int64_t tok_bs, const int* quant_ids, const int* pos_ids,
+                              const float* tok_w, const float* q_w, const float* pos_w, int batch, int L, int d,
+                              int vocab, void* out, int dtype, int64_t out_bs, int* err_flag, void* stream) {
+  MTTS_CHECK(batch >= 0 && L >= 0 && d > 0 && vocab > 0, "embed_sum: bad args");
+  MTTS_CHECK(d % 4 == 0, "embed_sum: d_model %% 4 != 0");
+  MTTS_CHECK(dtype == MTTS_F32 || dtype == MTTS_BF16, "embed_sum: bad dtype");
+  if (batch == 0 || L == 0) return MTTS_OK;
+  MTTS_CHECK(tokens && quant_ids && pos_ids && tok_w && q_w && pos_w && out && err_flag, "embed_sum: null pointer");
+  MTTS_CHECK(((uintptr_t)tok_w | (uintptr_t)q_w | (uintptr_t)pos_w | (uintptr_t)out) % 16 == 0,
+             "embed_sum: tables/out must be 16-byte aligned");
+  const int rpb = 16;
+  dim3 grid((L + rpb - 1) / rpb, batch);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MTTS_F32)
+    hipLaunchKernelGGL(embed_sum_kernel<float>, grid, dim3(256), 0, st, tokens, tok_bs, quant_ids, pos_ids, tok_w, q_w,
+                       pos_w, L, d, vocab, rpb, (float*)out, out_bs, err_flag);
+  else
+    hipLaunchKernelGGL(embed_sum_kernel<bf16_t>, grid, dim3(256), 0, st, tokens, tok_bs, quant_ids, pos_ids, tok_w,
+                       q_w, pos_w, L, d, vocab, rpb, (bf16_t*)out, out_bs, err_flag);
+  MTTS_LAUNCH_CHECK("embed_sum");
+  return MTTS_OK;
+}

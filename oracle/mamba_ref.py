@@ -158,6 +158,24 @@ def mha_ref(q_in, kv_in, in_w, in_b, out_w, out_b, n_heads, key_padding_mask=Non
     return o @ out_w.T + out_b
 
 
+def embed_codec_tokens_ref(tokens_3d, tok_w, pos_w, q_w):
+    """Restates train.py:115-131 (embed_codec_tokens): flatten (B, Q, T) ids
+    quantizer-major; ref = tok_w[ids] + pos_w[arange(T).repeat(Q)] +
+    q_w[arange(Q).repeat_interleave(T)]; mask True where the id is 0."""
+    B, Q, T = tokens_3d.shape
+    flat = tokens_3d.reshape(B, Q * T)
+    quant_ids = torch.arange(Q).repeat_interleave(T).unsqueeze(0).expand(B, -1)
+    pos_ids = torch.arange(T).repeat(Q)
+    ref = F.embedding(flat, tok_w) + F.embedding(pos_ids, pos_w)[None].expand(B, -1, -1) + F.embedding(quant_ids, q_w)
+    return ref, (tokens_3d == 0).reshape(B, Q * T)
+
+
+def codec_ce_loss_ref(logits, targets, pad_id=0):
+    """Restates train.py:31-42: CE over (B*T, V), ignore_index=pad_id, no shift."""
+    B, T, V = logits.shape
+    return F.cross_entropy(logits.reshape(B * T, V), targets.reshape(B * T), ignore_index=pad_id)
+
+
 def length_regulator_ref(hidden, durations, max_len=None):
     """Restates style_cross_attention.py:156-198 (LengthRegulator.forward):
     durations rounded half-to-even (torch.round) and clamped >= 0; row b of
