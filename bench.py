@@ -17,6 +17,9 @@ Also reported on rank 0 (same JSON line):
   roofline_bf16 the same with bf16 I/O (VALU-bound: DESIGN.md section 3)
   step_mfma     the step's algorithmic FLOPs / step time vs dense bf16 peak
   decode        decode_step p50/p90 latency (C4, B=32, 12L)
+  c5_decoder    the decoder step at train.py's shape:
+                T_audio = 5x1024 flattened codec streams, voice prompt as
+                5120 reference keys (T_kv = 5248), tokens/s and TFLOP/s
   style         style pipeline: HIP length regulator
                 roofline, StyleConditioningPipeline eval / train times
   cpu_baseline  the pure-PyTorch oracle (oracle/mamba_ref.py) fwd+bwd of the
@@ -278,6 +281,57 @@ def style_bench(B=8, T_text=128, d_model=1024, d_style=256, iters=20):
             "pipeline_eval_ms": eval_ms, "pipeline_train_fwd_bwd_ms": train_ms}
 
 
+def c5_decoder_bench(B=4, Q=5, T_frames=1024, T_text=128, steps=3):
+    """SURVEY §8f row 3 / configs[4]'s decoder: the train.py shape -- 5 FACodec
+    streams of 1024 frames flattened to T_audio = 5120, the voice prompt
+    embedded as reference (embed_codec_tokens, 5120 keys) in front of the
+    text (T_kv = 5248), codec_ce_loss, fused clip + Adam; 12L d=1024 bf16."""
+    import mamba_decoder
+    import codec_tokens as ct
+    from mtts.optim import FusedClipAdam
+    dev = "cuda"
+    torch.manual_seed(0)
+    m = mamba_decoder.MambaTTSDecoder(10, d_model=1024, n_layers=12, n_heads=8, d_ff=2048, d_style=256,
+                                      num_quantizers=Q).to(dev)
+    m.compute_dtype = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(5)
+    codec = torch.randint(0, 10, (B, T_frames, Q), device=dev, generator=g)
+    voice = torch.randint(0, 10, (B, T_frames, Q), device=dev, generator=g)
+    text = torch.randn(B, T_text, 1024, device=dev, generator=g)
+    z = torch.randn(B, 256, device=dev, generator=g)
+    tmask = torch.ones(B, T_text, dtype=torch.bool, device=dev)
+    audio, _, _ = ct.flatten_codec_tokens(codec)
+    _, v3, _ = ct.flatten_codec_tokens(voice)
+    params = list(m.parameters())
+    opt = FusedClipAdam(params, lr=1e-4, max_grad_norm=1.0)
+
+    def step():
+        ref, vmask = ct.embed_codec_tokens(v3, m)
+        logits = m(audio, text, z, text_mask=tmask, ref_hidden=ref, ref_mask=vmask)
+        loss = ct.codec_ce_loss(logits, audio)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    T = Q * T_frames
+    T_kv = Q * T_frames + T_text
+    c = dict(C2, B=B, T=T, T_text=T_kv)
+    fl = flops_per_step(c)
+    attn_fl = 3 * 12 * 4 * B * T * T_kv * 1024
+    del m, opt
+    torch.cuda.empty_cache()
+    return {"B": B, "T_audio": T, "T_kv": T_kv, "ms_per_step": ms, "tokens_per_s": B * T / ms * 1e3,
+            "tflops": fl / ms / 1e9, "attention_share_of_flops": attn_fl / fl, "loss": float(loss.item())}
+
+
 def cpu_baseline_scan(L=8192, D=2048):
     """oracle selective_scan_ref (pure PyTorch, fp32, CPU) on a bounded slice
     of the north-star scan (one of its 32 batch rows: B=1, L=8192,
@@ -382,6 +436,8 @@ def main():
         rec["roofline_bf16"] = {"bound": "hbm (VALU-limited, DESIGN.md section 3)", "achieved": sbw / 1e9,
                                 "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": sbw / HBM_PEAK, "ms": sms,
                                 "algorithmic_bytes": sb, "traffic": pmc_traffic("bf16")}
+        rec["c5_decoder"] = c5_decoder_bench()
+        log(f"[bench] c5 decoder {rec['c5_decoder']}")
         rec["style"] = style_bench()
         log(f"[bench] style {rec['style']}")
         if args.decode_steps > 0:

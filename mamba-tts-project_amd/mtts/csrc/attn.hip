@@ -254,8 +254,18 @@ struct BwdParams {
   MttsAttnBwdArgs a;
   int nchunk, qchunk;  // query chunks (grid.x) and queries per chunk (multiple of 32)
   float* part;         // nchunk > 1: fp32 dK|dV partials [nchunk][B][Tk][2*H*hd]
-  float* dq_acc;       // > 1 key group: fp32 dq accumulator [B][Tq][H*hd]
+  float* dq_acc;       // > 1 key group (mode 0): fp32 dq accumulator [B][Tq][H*hd]
+  float* delta;        // modes 1/2: -rowsum(dO * O) per (b, h, query) [B][H][Tq]
 };
+
+// Backward modes.  0: short key side (C2, <= one key group): workgroup =
+// (query chunk, head, batch), dK/dV of all keys + dQ.  Long key side (the
+// train.py shape, 5k reference keys) splits the work in two launches:
+// 2 (first): workgroup = one 32-query slice; loops over all key groups with
+//    dQ in registers (no global accumulator); writes -delta per query;
+// 1: workgroup = one key group; sweeps all queries with dK/dV in registers
+//    (complete: no partials, no reduce pass); delta from mode 2.
+constexpr int kBwdShort = 0, kBwdKV = 1, kBwdQ = 2;
 
 template <typename T, int HD>
 struct BwdCfg {
@@ -267,7 +277,7 @@ struct BwdCfg {
   static constexpr int ND = (HD + 31) / 32;
 };
 
-template <typename T, int HD>
+template <typename T, int HD, int MODE>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
   using C = BwdCfg<T, HD>;
   constexpr bool BF = C::BF;
@@ -290,13 +300,19 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
   const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;  // tr_read addressing
   const int b = blockIdx.z, hh = blockIdx.y, chunk = blockIdx.x;
   const int d = f.heads * HD;
-  const int qbeg = chunk * p.qchunk, qend = min(f.q_len, qbeg + p.qchunk);
+  const int qbeg = MODE == kBwdKV ? 0 : MODE == kBwdQ ? 32 * chunk : chunk * p.qchunk;
+  const int qend = MODE == kBwdKV ? f.q_len : min(f.q_len, MODE == kBwdQ ? qbeg + 32 : qbeg + p.qchunk);
   const float c = f.scale * kLog2e;
   const float inv_scale = 1.f / f.scale;
   const uint8_t* mb = f.key_padding_mask ? f.key_padding_mask + b * f.mask_bs : nullptr;
   const int nkg = (f.kv_len + KG - 1) / KG;
+  float* const dbuf = p.delta ? p.delta + ((int64_t)b * f.heads + hh) * f.q_len : nullptr;
+  constexpr int NQT = (ND + NW - 1) / NW;   // mode 2: dQ tiles per wave, held across key groups
+  f32x16 QA[NQT];
+#pragma unroll
+  for (int t = 0; t < NQT; ++t) QA[t] = f32x16{};
 
-  for (int kg = 0; kg < nkg; ++kg) {
+  for (int kg = MODE == kBwdKV ? chunk : 0; kg < (MODE == kBwdKV ? chunk + 1 : nkg); ++kg) {
     const int kg0 = kg * KG;
     __syncthreads();
     {
@@ -330,7 +346,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
     for (int q0 = qbeg; q0 < qend; q0 += 32) {
       __syncthreads();
       // ---- stage Q, dO images; delta = rowsum(dO * O); -lse/scale
-      {
+      // (mode 2: its single slice once, kept across key groups)
+      if (MODE != kBwdQ || kg == 0) {
         const T* qb = (const T*)f.q + b * f.q_bs + hh * HD;
         const T* ob = (const T*)f.out + b * f.o_bs + hh * HD;
         const T* gb = (const T*)a.dout + b * a.do_bs + hh * HD;
@@ -341,7 +358,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
           if (qi < qend) {
             qv = *(const f32x4*)(qb + qi * f.q_ls + cc);
             gv = *(const f32x4*)(gb + qi * a.do_ls + cc);
-            ov = *(const f32x4*)(ob + qi * f.o_ls + cc);
+            if constexpr (MODE != kBwdKV) ov = *(const f32x4*)(ob + qi * f.o_ls + cc);
           }
           *(f32x4*)(sQ + row * P + cc) = qv;
           *(f32x4*)(sO + row * P + cc) = gv;
@@ -355,7 +372,15 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
             for (int e = 0; e < 4; ++e) dl += gv[e] * ov[e];
           }
           dl = group_sum<HD / CH>(dl);
-          if (i % (HD / CH) == 0) sD[row] = -dl;
+          if constexpr (MODE != kBwdKV) {
+            if (i % (HD / CH) == 0) {
+              sD[row] = -dl;
+              if (MODE == kBwdQ && qi < qend) dbuf[qi] = -dl;
+            }
+          }
+        }
+        if constexpr (MODE == kBwdKV) {
+          if (tid < 32) sD[tid] = q0 + tid < qend ? dbuf[q0 + tid] : 0.f;
         }
         if (tid < 32) {
           const int qi = q0 + tid;
@@ -404,6 +429,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
       if constexpr (BF) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
+          if constexpr (MODE == kBwdQ) break;
           const s16x8 pa = pack8(S, s), da = pack8(D, s);
 #pragma unroll
           for (int dt = 0; dt < ND; ++dt) {
@@ -425,6 +451,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
       } else {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
+          if constexpr (MODE == kBwdQ) break;
           const int row = acc_row(i, h);
           const float* po = (const float*)sO + row * P + r;
           const float* pq = (const float*)sQ + row * P + r;
@@ -439,10 +466,11 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
           *(f32x4*)((float*)sS + key * PS + 8 * g4 + 4 * h) =
               f32x4{D[4 * g4], D[4 * g4 + 1], D[4 * g4 + 2], D[4 * g4 + 3]};
       }
+      if constexpr (MODE == kBwdKV) continue;   // dQ comes from the mode-2 launch
       __syncthreads();
       // ---- dQ[q][dims of tile dt] = scale * dS K over the group's keys
       for (int dt = wave; dt < ND; dt += NW) {
-        f32x16 Q = {};
+        f32x16 Q = MODE == kBwdQ ? QA[(dt - wave) / NW] : f32x16{};
         if constexpr (BF) {
 #pragma unroll
           for (int s = 0; s < KG / 16; ++s) {
@@ -456,6 +484,10 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
             const int kk = KG / 2 * h + s;
             Q = mfma_f32(((const float*)sS)[kk * PS + r], ((const float*)sK)[kk * P + dt * 32 + r], Q);
           }
+        }
+        if constexpr (MODE == kBwdQ) {
+          QA[(dt - wave) / NW] = Q;                // summed over all key groups, written after
+          continue;
         }
         const int dim = dt * 32 + r;
         if (dim < HD) {
@@ -479,6 +511,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
       }
     }
     // ---- dK (scaled), dV of this wave's 32 keys: rows = keys (registers), cols = dims (lanes)
+    if constexpr (MODE == kBwdQ) continue;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt) {
       const int dim = dt * 32 + r;
@@ -488,7 +521,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
         const int kk = kg0 + wave * 32 + acc_row(i, h);
         if (kk >= f.kv_len) continue;
         const float vk = dK[dt][i] * f.scale, vv = dV[dt][i];
-        if (p.nchunk > 1) {
+        if (MODE == kBwdShort && p.nchunk > 1) {
           float* pr = p.part + (((int64_t)chunk * f.batch + b) * f.kv_len + kk) * (2 * d) + hh * HD + dim;
           pr[0] = vk;
           pr[d] = vv;
@@ -496,6 +529,19 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
           mtts::stf((T*)a.dk + b * a.dk_bs + (int64_t)kk * a.dk_ls + hh * HD + dim, vk);
           mtts::stf((T*)a.dv + b * a.dv_bs + (int64_t)kk * a.dv_ls + hh * HD + dim, vv);
         }
+      }
+    }
+  }
+  if constexpr (MODE == kBwdQ) {
+#pragma unroll
+    for (int t = 0; t < NQT; ++t) {
+      const int dt = wave + t * NW;
+      const int dim = dt * 32 + r;
+      if (dt >= ND || dim >= HD) continue;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = qbeg + acc_row(i, h);
+        if (qi < qend) mtts::stf((T*)a.dq + b * a.dq_bs + (int64_t)qi * a.dq_ls + hh * HD + dim, QA[t][i] * f.scale);
       }
     }
   }
@@ -560,7 +606,8 @@ void dispatch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
 
 struct BwdPlan {
   int nchunk, qchunk, kg;
-  int64_t part_bytes, dq_bytes;
+  bool split;                  // long key side: modes 2 + 1
+  int64_t part_bytes, dq_bytes, delta_bytes;
 };
 
 BwdPlan plan_bwd(int batch, int heads, int head_dim, int q_len, int kv_len, int dtype) {
@@ -576,26 +623,38 @@ BwdPlan plan_bwd(int batch, int heads, int head_dim, int q_len, int kv_len, int 
   pl.nchunk = (q_len + pl.qchunk - 1) / pl.qchunk;
   if (pl.nchunk < 1) pl.nchunk = 1;
   const int64_t d = (int64_t)heads * head_dim;
+  pl.split = kv_len > pl.kg && !getenv("MTTS_ATTN_BWD_FUSED");
+  if (pl.split) {
+    pl.delta_bytes = ((int64_t)batch * heads * q_len * 4 + 255) / 256 * 256;
+    return pl;
+  }
   pl.part_bytes = pl.nchunk > 1 ? (int64_t)pl.nchunk * batch * kv_len * 2 * d * 4 : 0;
   pl.dq_bytes = kv_len > pl.kg ? (int64_t)batch * q_len * d * 4 : 0;
   return pl;
 }
 
 template <typename T, int HD>
-void launch_bwd(const BwdParams& p, hipStream_t st) {
-  dim3 grid(p.nchunk, p.a.f.heads, p.a.f.batch);
-  attn_bwd_kernel<T, HD><<<grid, BwdCfg<T, HD>::NW * 64, 0, st>>>(p);
+void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
+  constexpr int NT = BwdCfg<T, HD>::NW * 64;
+  const MttsAttnFwdArgs& f = p.a.f;
+  if (split) {
+    constexpr int KG = BwdCfg<T, HD>::KG;
+    attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
+    attn_bwd_kernel<T, HD, kBwdKV><<<dim3((f.kv_len + KG - 1) / KG, f.heads, f.batch), NT, 0, st>>>(p);
+    return;
+  }
+  attn_bwd_kernel<T, HD, kBwdShort><<<dim3(p.nchunk, f.heads, f.batch), NT, 0, st>>>(p);
 }
 
 template <typename T>
-void dispatch_bwd(const BwdParams& p, hipStream_t st) {
+void dispatch_bwd(const BwdParams& p, bool split, hipStream_t st) {
   switch (p.a.f.head_dim) {
-    case 16: launch_bwd<T, 16>(p, st); break;
-    case 32: launch_bwd<T, 32>(p, st); break;
-    case 64: launch_bwd<T, 64>(p, st); break;
-    default: launch_bwd<T, 128>(p, st); break;
+    case 16: launch_bwd<T, 16>(p, split, st); break;
+    case 32: launch_bwd<T, 32>(p, split, st); break;
+    case 64: launch_bwd<T, 64>(p, split, st); break;
+    default: launch_bwd<T, 128>(p, split, st); break;
   }
-  if (p.nchunk > 1) {
+  if (!split && p.nchunk > 1) {
     const int64_t n = (int64_t)p.a.f.batch * p.a.f.kv_len * 2 * p.a.f.heads * p.a.f.head_dim;
     int blocks = (int)((n + 255) / 256);
     if (blocks > 4096) blocks = 4096;
@@ -621,7 +680,7 @@ extern "C" int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream) {
 
 extern "C" int64_t mtts_attention_bwd_workspace(int batch, int heads, int head_dim, int q_len, int kv_len, int dtype) {
   const BwdPlan pl = plan_bwd(batch, heads, head_dim, q_len, kv_len, dtype);
-  return pl.part_bytes + pl.dq_bytes + 256;
+  return pl.part_bytes + pl.dq_bytes + pl.delta_bytes + 256;
 }
 
 extern "C" int mtts_attention_bwd(const MttsAttnBwdArgs* a, void* stream) {
@@ -650,17 +709,19 @@ extern "C" int mtts_attention_bwd(const MttsAttnBwdArgs* a, void* stream) {
     return MTTS_OK;
   }
   const BwdPlan pl = plan_bwd(f.batch, f.heads, f.head_dim, f.q_len, f.kv_len, f.dtype);
-  MTTS_CHECK(a->workspace || (pl.part_bytes + pl.dq_bytes) == 0, "attention_bwd: workspace required");
+  MTTS_CHECK(a->workspace || (pl.part_bytes + pl.dq_bytes + pl.delta_bytes) == 0,
+             "attention_bwd: workspace required");
   BwdParams p;
   p.a = *a;
   p.nchunk = pl.nchunk;
   p.qchunk = pl.qchunk;
   p.part = pl.part_bytes ? (float*)a->workspace : nullptr;
   p.dq_acc = pl.dq_bytes ? (float*)((char*)a->workspace + pl.part_bytes) : nullptr;
+  p.delta = pl.delta_bytes ? (float*)((char*)a->workspace + pl.part_bytes + pl.dq_bytes) : nullptr;
   if (f.dtype == MTTS_BF16)
-    dispatch_bwd<bf16_t>(p, st);
+    dispatch_bwd<bf16_t>(p, pl.split, st);
   else
-    dispatch_bwd<float>(p, st);
+    dispatch_bwd<float>(p, pl.split, st);
   MTTS_LAUNCH_CHECK("attention_bwd");
   return MTTS_OK;
 }
