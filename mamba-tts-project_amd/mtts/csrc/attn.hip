@@ -547,6 +547,149 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
   }
 }
 
+// Long key side, bf16, dQ pass (replaces mode 2 for hd 64 / 128): a
+// workgroup owns 128 queries, one 32-query slice per WAVE (so every staged
+// key group feeds 4x the MFMAs of mode 2's key-split waves).  Q and dO stay
+// in registers as MFMA A fragments for the whole sweep; per key group of 128
+// (K / V images in LDS, shared by the waves) and per 32-key tile:
+//   S = Q K^T - lse/scale, dP = dO V^T - delta  (query rows, key on the lane)
+//   P = exp2(c S) (masked keys 0), dS = P dP -> the wave's own dS^T image ->
+//   dQ += dS K  (transposed LDS reads of dS^T and K), in registers.
+// delta = rowsum(dO * O) is computed once per query and written for the
+// dK/dV pass (mode 1).
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
+  constexpr int KG = 128, P = HD + 8, PS = 32;
+  constexpr int NQ = HD / 16, ND = HD / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t sK[KG * P + 32];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[KG * P + 32];
+  __shared__ __attribute__((aligned(16))) bf16_t sS[4][32 * PS + 32];
+  __shared__ float sLq[4][32], sDq[4][32];
+  __shared__ uint32_t sMask[KG / 32];
+  const MttsAttnBwdArgs& a = p.a;
+  const MttsAttnFwdArgs& f = a.f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int b = blockIdx.z, hh = blockIdx.y;
+  const int q0 = blockIdx.x * 128 + wave * 32;           // this wave's queries
+  const float c = f.scale * kLog2e, inv_scale = 1.f / f.scale;
+  const uint8_t* mb = f.key_padding_mask ? f.key_padding_mask + b * f.mask_bs : nullptr;
+  const bf16_t* qb = (const bf16_t*)f.q + b * f.q_bs + hh * HD;
+  const bf16_t* gb = (const bf16_t*)a.dout + b * a.do_bs + hh * HD;
+  const bf16_t* ob = (const bf16_t*)f.out + b * f.o_bs + hh * HD;
+  // ---- A fragments of Q / dO (query row r, dims 16s + 8h .. +7), delta, -lse/scale
+  const int qi = q0 + r;
+  const bool qv = qi < f.q_len;
+  s16x8 Qf[NQ], Gf[NQ];
+  float dl = 0.f;
+#pragma unroll
+  for (int s = 0; s < NQ; ++s) {
+    Qf[s] = qv ? *(const s16x8*)(qb + (int64_t)qi * f.q_ls + 16 * s + 8 * h) : s16x8{};
+    Gf[s] = qv ? *(const s16x8*)(gb + (int64_t)qi * a.do_ls + 16 * s + 8 * h) : s16x8{};
+    const s16x8 o8 = qv ? *(const s16x8*)(ob + (int64_t)qi * f.o_ls + 16 * s + 8 * h) : s16x8{};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += mtts::bf2f((bf16_t)Gf[s][e]) * mtts::bf2f((bf16_t)o8[e]);
+  }
+  dl += __shfl_xor(dl, 32);
+  if (h == 0) {
+    float L = 0.f;
+    if (qv) {
+      L = -f.lse[((int64_t)b * f.heads + hh) * f.q_len + qi] * inv_scale;
+      p.delta[((int64_t)b * f.heads + hh) * f.q_len + qi] = -dl;
+    }
+    sLq[wave][r] = L;
+    sDq[wave][r] = qv ? -dl : 0.f;
+  }
+  __syncthreads();
+  float Lr[16], Dr[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    Lr[i] = sLq[wave][acc_row(i, h)];
+    Dr[i] = sDq[wave][acc_row(i, h)];
+  }
+  f32x16 QA[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) QA[dt] = f32x16{};
+  const int nkg = (f.kv_len + KG - 1) / KG;
+  const bf16_t* kb = (const bf16_t*)f.k + b * f.k_bs + hh * HD;
+  const bf16_t* vb = (const bf16_t*)f.v + b * f.v_bs + hh * HD;
+  bf16_t* sSw = sS[wave];
+  for (int kg = 0; kg < nkg; ++kg) {
+    const int kg0 = kg * KG;
+    __syncthreads();  // previous key group's images consumed
+    for (int i = tid; i < KG * HD / 8; i += 256) {
+      const int row = i / (HD / 8), cc = (i % (HD / 8)) * 8;
+      const int key = kg0 + row;
+      f32x4 kv = {}, vv = {};
+      if (key < f.kv_len) {
+        kv = *(const f32x4*)(kb + (int64_t)key * f.k_ls + cc);
+        vv = *(const f32x4*)(vb + (int64_t)key * f.v_ls + cc);
+      }
+      *(f32x4*)(sK + row * P + cc) = kv;
+      *(f32x4*)(sV + row * P + cc) = vv;
+    }
+    if (wave < KG / 64) {
+      const int key = kg0 + 64 * wave + lane;
+      const bool ok = key < f.kv_len && !(mb && mb[key]);
+      const uint64_t bal = __ballot(ok);
+      if (lane == 0) {
+        sMask[2 * wave] = (uint32_t)bal;
+        sMask[2 * wave + 1] = (uint32_t)(bal >> 32);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < KG / 32; ++kt) {
+      f32x16 S, D;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        S[i] = Lr[i];
+        D[i] = Dr[i];
+      }
+      const bf16_t* kr = sK + (kt * 32 + r) * P + 8 * h;
+      const bf16_t* vr = sV + (kt * 32 + r) * P + 8 * h;
+#pragma unroll
+      for (int s = 0; s < NQ; ++s) {
+        S = mfma_bf16(Qf[s], *(const s16x8*)(kr + 16 * s), S);
+        D = mfma_bf16(Gf[s], *(const s16x8*)(vr + 16 * s), D);
+      }
+      const bool kvalid = (sMask[kt] >> r) & 1u;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        s16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          const float pv = kvalid ? exp2_raw(c * S[i]) : 0.f;
+          v[e] = bfbits(pv * D[i]);                    // dS (unscaled), bf16
+        }
+        *(s16x4*)(sSw + r * PS + 8 * g4 + 4 * h) = v;  // dS^T [key][query]
+      }
+      // dQ[q][dims] += dS[q][32 keys of tile kt] K[keys][dims]
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16_t* ps = sSw + (16 * s + 8 * h + qq) * PS + 16 * g + 4 * pp;
+        const s16x8 A = cat(tr_read(ps), tr_read(ps + 4 * PS));
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          const bf16_t* pk = sK + (kt * 32 + 16 * s + 8 * h + qq) * P + dt * 32 + 16 * g + 4 * pp;
+          QA[dt] = mfma_bf16(A, cat(tr_read(pk), tr_read(pk + 4 * P)), QA[dt]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qo = q0 + acc_row(i, h);
+      if (qo < f.q_len)
+        mtts::stf((bf16_t*)a.dq + b * a.dq_bs + (int64_t)qo * a.dq_ls + hh * HD + dt * 32 + r, QA[dt][i] * f.scale);
+    }
+  }
+}
+
 // sum of the query-chunk partials -> dk, dv (fixed order)
 template <typename T>
 __global__ __launch_bounds__(256) void attn_bwd_reduce_kernel(BwdParams p) {
@@ -639,7 +782,14 @@ void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
   const MttsAttnFwdArgs& f = p.a.f;
   if (split) {
     constexpr int KG = BwdCfg<T, HD>::KG;
-    attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
+    if constexpr (std::is_same<T, bf16_t>::value && (HD == 64 || HD == 128)) {
+      if (!getenv("MTTS_ATTN_DQ_V1"))
+        attn_bwd_dq_kernel<HD><<<dim3((f.q_len + 127) / 128, f.heads, f.batch), 256, 0, st>>>(p);
+      else
+        attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
+    } else {
+      attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
+    }
     attn_bwd_kernel<T, HD, kBwdKV><<<dim3((f.kv_len + KG - 1) / KG, f.heads, f.batch), NT, 0, st>>>(p);
     return;
   }

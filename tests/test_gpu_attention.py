@@ -161,15 +161,20 @@ def test_north_star_shape_bf16():
     close(dkv[:2], rkv, 3e-2)
 
 
-@pytest.mark.parametrize("split", [True, False])
+@pytest.mark.parametrize("path", ["split", "split_dq_v1", "fused"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("case", [(1, 100, 1100, 2, 128), (2, 64, 777, 4, 64), (2, 33, 129, 2, 32)])
-def test_backward_long_key_side(case, dtype, split, monkeypatch):
+@pytest.mark.parametrize("case", [(1, 100, 1100, 2, 128), (2, 64, 777, 4, 64), (2, 33, 129, 2, 32),
+                                  (1, 300, 260, 2, 128)])
+def test_backward_long_key_side(case, dtype, path, monkeypatch):
     """Key side longer than one key group (the train.py shape: 5k reference
-    keys): the split backward (per-query-slice dQ launch + per-key-group
-    dK/dV launch) and the fused chunked one (MTTS_ATTN_BWD_FUSED) both match."""
-    if not split:
+    keys): the split backward (dQ launch -- wave-per-query-slice kernel for
+    bf16 hd 64/128, or the key-split mode-2 kernel (MTTS_ATTN_DQ_V1) -- then
+    the per-key-group dK/dV launch) and the fused chunked one
+    (MTTS_ATTN_BWD_FUSED) all match."""
+    if path == "fused":
         monkeypatch.setenv("MTTS_ATTN_BWD_FUSED", "1")
+    if path == "split_dq_v1":
+        monkeypatch.setenv("MTTS_ATTN_DQ_V1", "1")
     B, T, S, H, hd = case
     q, kv, kpm = make(B, T, S, H, hd, dtype, seed=5)
     o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
