@@ -113,8 +113,17 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_kernel(const MttsLNArgs 
 
 // Each block handles RB consecutive rows (all in one FiLM group); partials
 // per block: dw, db (cols each) and dgamma, dbeta (cols each).
+// 8 waves per block for rows of <= 16 elements per lane (2 per SIMD at one
+// block per CU; wider rows keep 4 waves to stay in registers) and the next
+// row's x / dy loads issued before the current row's math: the 4-wave,
+// load-then-compute form ran at ~55 % of HBM (one 16-B load pair in flight
+// per wave).
+template <int VEC, int NV>
+constexpr int ln_bwd_waves() { return VEC * NV <= 16 ? 8 : 4; }
 template <typename T, typename TG, int VEC, int NV>
-__global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const MttsLNBwdArgs a, int RB, float* __restrict__ part) {
+__global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(const MttsLNBwdArgs a, int RB,
+                                                                  float* __restrict__ part) {
+  constexpr int kLnBwdWaves = ln_bwd_waves<VEC, NV>();
   const MttsLNArgs& f = a.f;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -138,18 +147,35 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const MttsLNBwdAr
   }
   const T* xsrc = (const T*)((f.res && f.x_sum) ? f.x_sum : f.x);
   const int64_t xrs = (f.res && f.x_sum) ? f.xsum_rs : f.x_rs;
-  for (int r = wave; r < RB; r += kLnWaves) {
+  const int rend = min(RB, f.rows - row0);
+  float nxv[NV][VEC], ndy[NV][VEC];
+  auto load_row = [&](int rr) __attribute__((always_inline)) {
+    const int row = row0 + rr;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c0 = (k * 64 + lane) * VEC;
+      ld_vec<T, VEC>(xsrc + (int64_t)row * xrs + c0, nxv[k]);
+      ld_vec<T, VEC>((const T*)a.dy + (int64_t)row * a.dy_rs + c0, ndy[k]);
+    }
+  };
+  if (wave < rend) load_row(wave);
+  for (int r = wave; r < rend; r += kLnBwdWaves) {
     const int row = row0 + r;
-    if (row >= f.rows) break;
     const float mean = f.mean[row], rstd = f.rstd[row];
+    float cxv[NV][VEC], cdy[NV][VEC];
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) { cxv[k][q] = nxv[k][q]; cdy[k][q] = ndy[k][q]; }
+    if (r + kLnBwdWaves < rend) load_row(r + kLnBwdWaves);
     float xh[NV][VEC], dxh[NV][VEC];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c0 = (k * 64 + lane) * VEC;
       float xv[VEC], dy[VEC];
-      ld_vec<T, VEC>(xsrc + (int64_t)row * xrs + c0, xv);
-      ld_vec<T, VEC>((const T*)a.dy + (int64_t)row * a.dy_rs + c0, dy);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) { xv[q] = cxv[k][q]; dy[q] = cdy[k][q]; }
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
         const float h = (xv[q] - mean) * rstd;
@@ -183,8 +209,8 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const MttsLNBwdAr
       st_vec<T, VEC>((T*)a.dx + (int64_t)row * a.dx_rs + c0, o);
     }
   }
-  // block partials: reduce the 4 waves through LDS, then one write per column
-  extern __shared__ float sm[];  // [kLnWaves][cols]
+  // block partials: reduce the waves through LDS, then one write per column
+  extern __shared__ float sm[];  // [kLnBwdWaves][cols]
   const int nk = film ? 4 : 2;
   for (int which = 0; which < nk; ++which) {
 #pragma unroll
@@ -197,10 +223,10 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const MttsLNBwdAr
       }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < n; c += 64 * kLnWaves) {
+    for (int c = threadIdx.x; c < n; c += 64 * kLnBwdWaves) {
       float s = 0.f;
 #pragma unroll
-      for (int w = 0; w < kLnWaves; ++w) s += sm[w * n + c];
+      for (int w = 0; w < kLnBwdWaves; ++w) s += sm[w * n + c];
       part[((int64_t)which * gridDim.x + blockIdx.x) * n + c] = s;
     }
     __syncthreads();
@@ -222,8 +248,9 @@ static void launch_fwd(const MttsLNArgs* a, hipStream_t st) {
 template <typename T, typename TG, int VEC, int NV>
 static void launch_bwd(const MttsLNBwdArgs* a, int rb, float* part, hipStream_t st) {
   const int nblk = (a->f.rows + rb - 1) / rb;
-  hipLaunchKernelGGL((ln_bwd_kernel<T, TG, VEC, NV>), dim3(nblk), dim3(64 * kLnWaves),
-                     kLnWaves * a->f.cols * sizeof(float), st, *a, rb, part);
+  constexpr int W = ln_bwd_waves<VEC, NV>();
+  hipLaunchKernelGGL((ln_bwd_kernel<T, TG, VEC, NV>), dim3(nblk), dim3(64 * W), W * a->f.cols * sizeof(float), st, *a,
+                     rb, part);
 }
 
 // dispatch on (dtype, gamma dtype, cols)
