@@ -145,16 +145,28 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(const MttsConvBwdArgs a, 
   // g beyond L is zero; dx[t-3] needs g[t-3 .. t]
   const int tlast = min(t0 + kTT + 3, L + 3);
   const int town = min(t0 + kTT, L);
-  for (int t = t0; t < tlast; ++t) {
-    float x3[CPT], go[CPT], g[CPT];
-    const bool in = t < L;
-    if (in) {
-      load_x<T, CPT>(f, b, c0, t, x3);
-      ldv<T, CPT>(dout + (int64_t)t * a.dout_ls, go);
+  // x / dout of step t+2 and t+1 are in flight while step t computes
+  float px[2][CPT], pg[2][CPT];
+  auto fetch = [&](int t, float (&xx)[CPT], float (&gg)[CPT]) __attribute__((always_inline)) {
+    if (t < L && t < tlast) {
+      load_x<T, CPT>(f, b, c0, t, xx);
+      ldv<T, CPT>(dout + (int64_t)t * a.dout_ls, gg);
     } else {
 #pragma unroll
-      for (int q = 0; q < CPT; ++q) { x3[q] = 0.f; go[q] = 0.f; }
+      for (int q = 0; q < CPT; ++q) { xx[q] = 0.f; gg[q] = 0.f; }
     }
+  };
+  fetch(t0, px[0], pg[0]);
+  fetch(t0 + 1, px[1], pg[1]);
+#pragma unroll 2
+  for (int t = t0; t < tlast; ++t) {
+    float x3[CPT], go[CPT], g[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      x3[q] = px[0][q]; go[q] = pg[0][q];
+      px[0][q] = px[1][q]; pg[0][q] = pg[1][q];
+    }
+    fetch(t + 2, px[1], pg[1]);
     const bool own = t < town;
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
