@@ -402,8 +402,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # MTTS_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the
+        # data-parallel path on one card (ranks share it); the product path is
+        # "nccl" (RCCL over xGMI), one rank per GPU
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("MTTS_DIST_BACKEND", "nccl"))
     dev = torch.device("cuda", local)
     from mtts import _lib
     _lib.lib()
