@@ -20,6 +20,7 @@ Also reported on rank 0 (same JSON line):
   c5_decoder    the decoder step at train.py's shape:
                 T_audio = 5x1024 flattened codec streams, voice prompt as
                 5120 reference keys (T_kv = 5248), tokens/s and TFLOP/s
+  text_encoder  TextEncoder + DurationPredictor fwd+bwd
   style         style pipeline: HIP length regulator
                 roofline, StyleConditioningPipeline eval / train times
   cpu_baseline  the pure-PyTorch oracle (oracle/mamba_ref.py) fwd+bwd of the
@@ -332,6 +333,37 @@ def c5_decoder_bench(B=4, Q=5, T_frames=1024, T_text=128, steps=3):
             "tflops": fl / ms / 1e9, "attention_share_of_flops": attn_fl / fl, "loss": float(loss.item())}
 
 
+def text_bench(B=8, T_text=128, d_model=512, iters=10):
+    """TextEncoder (4 FFT blocks, 2 heads of 64, conv FFN
+    k=9 to 1024) + DurationPredictor at train.py's width (d_model 512), fp32
+    as the reference, fwd + bwd of encoder output and duration loss."""
+    import text_encoder as te
+    dev = "cuda"
+    torch.manual_seed(0)
+    enc = te.TextEncoder(79, d_model=d_model).to(dev).train()
+    dur = te.DurationPredictor(d_model=d_model).to(dev).train()
+    g = torch.Generator(device=dev).manual_seed(9)
+    ids = torch.randint(1, 79, (B, T_text), device=dev, generator=g)
+    lens = torch.randint(T_text // 2, T_text + 1, (B,), device=dev, generator=g)
+    mask = torch.arange(T_text, device=dev)[None] >= lens[:, None]
+    ids = ids.masked_fill(mask, 0)
+    target = torch.randint(1, 10, (B, T_text), device=dev, generator=g).float()
+
+    def step():
+        h = enc(ids, mask=mask)
+        loss = dur.compute_loss(dur(h, mask=mask), target, mask=mask) + h.square().mean()
+        loss.backward()
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        step()
+    torch.cuda.synchronize()
+    return {"B": B, "T_text": T_text, "d_model": d_model, "dtype": "fp32",
+            "fwd_bwd_ms": (time.perf_counter() - t0) / iters * 1e3}
+
+
 def cpu_baseline_scan(L=8192, D=2048):
     """oracle selective_scan_ref (pure PyTorch, fp32, CPU) on a bounded slice
     of the north-star scan (one of its 32 batch rows: B=1, L=8192,
@@ -442,6 +474,8 @@ def main():
                                 "algorithmic_bytes": sb, "traffic": pmc_traffic("bf16")}
         rec["c5_decoder"] = c5_decoder_bench()
         log(f"[bench] c5 decoder {rec['c5_decoder']}")
+        rec["text_encoder"] = text_bench()
+        log(f"[bench] text encoder {rec['text_encoder']}")
         rec["style"] = style_bench()
         log(f"[bench] style {rec['style']}")
         if args.decode_steps > 0:

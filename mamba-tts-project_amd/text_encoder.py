@@ -1,0 +1,299 @@
+"""Text encoder and duration predictor — MI355X-native drop-in for the
+reference's text_encoder.py: same class names,
+constructor arguments, forward signatures and state_dict keys.
+
+The reference builds these from the un-vendored FastSpeech2 repository
+(text_encoder.py:16-18 import ``lib.FastSpeech2``; setup.sh clones
+ming024/FastSpeech2, unpinned), which is absent here, so its published
+architecture is restated:
+
+* ``get_sinusoid_encoding_table`` (FastSpeech2 transformer/Models.py): angle
+  pos / 10000^(2*(i//2)/d), sin on even and cos on odd columns, the
+  padding_idx row zeroed;
+* ``FFTBlock`` (transformer/Layers.py): self-attention, masked_fill(pad, 0),
+  position-wise conv FFN, masked_fill(pad, 0);
+* ``MultiHeadAttention`` (transformer/SubLayers.py): w_qs / w_ks / w_vs
+  (d_model -> n_head*d_k), softmax(q k^T / sqrt(d_k), keys masked -inf), fc
+  back to d_model, dropout, LayerNorm(out + residual);
+* ``PositionwiseFeedForward``: Conv1d(d, d_inner, k0, pad (k0-1)/2) -> ReLU ->
+  Conv1d(d_inner, d, k1) -> dropout -> LayerNorm(out + residual);
+* ``VariancePredictor`` (model/modules.py): [Conv(k, pad (k-1)/2) -> ReLU ->
+  LayerNorm -> Dropout] x 2 -> Linear(filter, 1) -> squeeze -> masked_fill.
+
+Arithmetic: the attention core is the HIP MFMA attention (mtts_attention_*,
+key_padding_mask = the pad mask, True = pad, as the reference's
+slf_attn_mask); LayerNorm(x + residual) is the fused HIP LayerNorm; the
+projections and the convolutions are GEMMs (convolutions as one GEMM over a
+strided unfold of the time axis: weight (O, C, K) -> (O, C*K)) on hipBLASLt.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mtts import attn_kernels, ops
+from mtts.linear import linear
+
+
+def get_sinusoid_encoding_table(n_position, d_hid, padding_idx=None):
+    """Sinusoid position table (FastSpeech2 transformer/Models.py)."""
+    pos = np.arange(n_position, dtype=np.float64)[:, None]
+    i = np.arange(d_hid)[None, :]
+    table = pos / np.power(10000, 2 * (i // 2) / d_hid)
+    table[:, 0::2] = np.sin(table[:, 0::2])
+    table[:, 1::2] = np.cos(table[:, 1::2])
+    if padding_idx is not None:
+        table[padding_idx] = 0.0
+    return torch.FloatTensor(table)
+
+
+def _ln(mod, x, res=None):
+    y, _ = ops.layer_norm(x, mod.weight, mod.bias, mod.eps, res=res)
+    return y
+
+
+def conv1d_same(x, weight, bias, padding):
+    """Conv1d over the time axis of channel-last x (B, T, C) with weight
+    (O, C, K), as one GEMM: y[b, t] = W(O, C*K) . unfold(x)[b, t] + bias."""
+    O, C, K = weight.shape
+    if K == 1 and padding == 0:
+        return linear(x, weight.reshape(O, C), bias)
+    B, T, _ = x.shape
+    xp = F.pad(x, (0, 0, padding, padding))
+    Tout = T + 2 * padding - K + 1
+    cols = xp.unfold(1, K, 1).reshape(B * Tout, C * K)       # [c, k] order = weight's
+    return linear(cols, weight.reshape(O, C * K), bias).view(B, Tout, O)
+
+
+class Conv(nn.Module):
+    """FastSpeech2 model/modules.py Conv: Conv1d on (B, T, C) inputs."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=1, stride=1, padding=0, dilation=1, bias=True,
+                 w_init="linear"):
+        super().__init__()
+        if stride != 1 or dilation != 1:
+            raise ValueError("Conv: stride / dilation 1 only (the text encoder's use)")
+        self.conv = nn.Conv1d(in_channels, out_channels, kernel_size=kernel_size, padding=padding, bias=bias)
+
+    def forward(self, x):
+        return conv1d_same(x, self.conv.weight, self.conv.bias, self.conv.padding[0])
+
+
+class MultiHeadAttention(nn.Module):
+    def __init__(self, n_head, d_model, d_k, d_v, dropout=0.1):
+        super().__init__()
+        if d_k != d_v:
+            raise ValueError("MultiHeadAttention: d_k == d_v only (the text encoder's use)")
+        self.n_head, self.d_k, self.d_v = n_head, d_k, d_v
+        self.w_qs = nn.Linear(d_model, n_head * d_k)
+        self.w_ks = nn.Linear(d_model, n_head * d_k)
+        self.w_vs = nn.Linear(d_model, n_head * d_v)
+        self.layer_norm = nn.LayerNorm(d_model)
+        self.fc = nn.Linear(n_head * d_v, d_model)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, q, k, v, mask=None):
+        """q/k/v (B, L, d_model); mask (B, L_k) bool, True = pad key.
+        Returns (output, None): attention weights are not materialised."""
+        residual = q
+        qh = linear(q, self.w_qs.weight, self.w_qs.bias)
+        kh = linear(k, self.w_ks.weight, self.w_ks.bias)
+        vh = linear(v, self.w_vs.weight, self.w_vs.bias)
+        # temperature sqrt(d_k) = the kernel's 1/sqrt(head_dim) scale
+        o = attn_kernels.attention(qh, kh, vh, self.n_head, key_padding_mask=mask)
+        o = self.dropout(linear(o, self.fc.weight, self.fc.bias))
+        return _ln(self.layer_norm, o, res=residual), None
+
+
+class PositionwiseFeedForward(nn.Module):
+    def __init__(self, d_in, d_hid, kernel_size, dropout=0.1):
+        super().__init__()
+        self.w_1 = nn.Conv1d(d_in, d_hid, kernel_size=kernel_size[0], padding=(kernel_size[0] - 1) // 2)
+        self.w_2 = nn.Conv1d(d_hid, d_in, kernel_size=kernel_size[1], padding=(kernel_size[1] - 1) // 2)
+        self.layer_norm = nn.LayerNorm(d_in)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x):
+        h = F.relu(conv1d_same(x, self.w_1.weight, self.w_1.bias, self.w_1.padding[0]))
+        out = self.dropout(conv1d_same(h, self.w_2.weight, self.w_2.bias, self.w_2.padding[0]))
+        return _ln(self.layer_norm, out, res=x)
+
+
+class FFTBlock(nn.Module):
+    def __init__(self, d_model, n_head, d_k, d_v, d_inner, kernel_size, dropout=0.1):
+        super().__init__()
+        self.slf_attn = MultiHeadAttention(n_head, d_model, d_k, d_v, dropout=dropout)
+        self.pos_ffn = PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout=dropout)
+
+    def forward(self, enc_input, mask=None, slf_attn_mask=None):
+        keypad = mask                      # slf_attn_mask = mask expanded over queries: the key pad mask
+        enc_output, attn = self.slf_attn(enc_input, enc_input, enc_input, mask=keypad)
+        enc_output = enc_output.masked_fill(mask.unsqueeze(-1), 0)
+        enc_output = self.pos_ffn(enc_output)
+        enc_output = enc_output.masked_fill(mask.unsqueeze(-1), 0)
+        return enc_output, attn
+
+
+class TextEncoder(nn.Module):
+    """Reference text_encoder.py:21-128 (FastSpeech2 Encoder over phonemes)."""
+
+    def __init__(self, vocab_size, d_model=256, n_layers=4, n_head=2, d_k=64, d_v=64, d_inner=1024,
+                 kernel_size=(9, 1), dropout=0.1, max_seq_len=3000, padding_idx=0):
+        super().__init__()
+        n_position = max_seq_len + 1
+        self.max_seq_len = max_seq_len
+        self.d_model = d_model
+        self.padding_idx = padding_idx
+        self.phoneme_emb = nn.Embedding(vocab_size, d_model, padding_idx=padding_idx)
+        self.position_enc = nn.Parameter(get_sinusoid_encoding_table(n_position, d_model, padding_idx).unsqueeze(0),
+                                         requires_grad=False)
+        self.layer_stack = nn.ModuleList([FFTBlock(d_model, n_head, d_k, d_v, d_inner, kernel_size, dropout=dropout)
+                                          for _ in range(n_layers)])
+
+    def forward(self, phoneme_ids, mask=None, return_attns=False):
+        """phoneme_ids (B, L); mask (B, L) bool, True = pad.  -> (B, L, d_model)
+        [, list of None per layer when return_attns: weights not materialised].
+        mask None means no padding (the reference's FFTBlock would fail on it)."""
+        B, L = phoneme_ids.shape
+        if mask is None:
+            mask = torch.zeros(B, L, dtype=torch.bool, device=phoneme_ids.device)
+        emb = F.embedding(phoneme_ids, self.phoneme_emb.weight, padding_idx=self.padding_idx)
+        if not self.training and L > self.max_seq_len:
+            pos = get_sinusoid_encoding_table(L, self.d_model)[:L].to(emb.device, emb.dtype)
+        else:
+            pos = self.position_enc[0, :L].to(emb.dtype)
+        x = emb + pos[None]
+        attns = []
+        for layer in self.layer_stack:
+            x, a = layer(x, mask=mask, slf_attn_mask=None)
+            if return_attns:
+                attns.append(a)
+        return (x, attns) if return_attns else x
+
+
+class VariancePredictor(nn.Module):
+    """FastSpeech2 model/modules.py VariancePredictor (state_dict keys kept)."""
+
+    def __init__(self, model_config):
+        super().__init__()
+        from collections import OrderedDict
+        self.input_size = model_config["transformer"]["encoder_hidden"]
+        self.filter_size = model_config["variance_predictor"]["filter_size"]
+        self.kernel = model_config["variance_predictor"]["kernel_size"]
+        self.conv_output_size = self.filter_size
+        self.dropout = model_config["variance_predictor"]["dropout"]
+        self.conv_layer = nn.Sequential(OrderedDict([
+            ("conv1d_1", Conv(self.input_size, self.filter_size, kernel_size=self.kernel,
+                              padding=(self.kernel - 1) // 2)),
+            ("relu_1", nn.ReLU()),
+            ("layer_norm_1", nn.LayerNorm(self.filter_size)),
+            ("dropout_1", nn.Dropout(self.dropout)),
+            ("conv1d_2", Conv(self.filter_size, self.filter_size, kernel_size=self.kernel, padding=1)),
+            ("relu_2", nn.ReLU()),
+            ("layer_norm_2", nn.LayerNorm(self.filter_size)),
+            ("dropout_2", nn.Dropout(self.dropout)),
+        ]))
+        self.linear_layer = nn.Linear(self.conv_output_size, 1)
+
+    def forward(self, encoder_output, mask):
+        cl = self.conv_layer
+        out = F.relu(cl.conv1d_1(encoder_output))
+        out = cl.dropout_1(_ln(cl.layer_norm_1, out))
+        out = F.relu(cl.conv1d_2(out))
+        out = cl.dropout_2(_ln(cl.layer_norm_2, out))
+        out = linear(out, self.linear_layer.weight, self.linear_layer.bias).squeeze(-1)
+        if mask is not None:
+            out = out.masked_fill(mask, 0.0)
+        return out
+
+
+class DurationPredictor(nn.Module):
+    """Reference text_encoder.py:131-209."""
+
+    def __init__(self, d_model=256, filter_size=256, kernel_size=3, dropout=0.1):
+        super().__init__()
+        model_config = {"transformer": {"encoder_hidden": d_model},
+                        "variance_predictor": {"filter_size": filter_size, "kernel_size": kernel_size,
+                                               "dropout": dropout}}
+        self.predictor = VariancePredictor(model_config)
+
+    def forward(self, encoder_output, mask=None):
+        return self.predictor(encoder_output, mask)
+
+    def compute_loss(self, log_duration_pred, duration_target, mask=None):
+        log_duration_target = torch.log(duration_target.float() + 1e-8)
+        loss = F.mse_loss(log_duration_pred, log_duration_target, reduction="none")
+        if mask is not None:
+            loss = loss.masked_fill(mask, 0.0)
+            loss = loss.sum() / (~mask).sum().float()
+        else:
+            loss = loss.mean()
+        return loss
+
+
+class TextProcessor:
+    """Phoneme vocabulary and batching (reference text_encoder.py:212-428; host
+    side, no GPU work): vocab from a JSON list or a Python list; unknown
+    phonemes map to <UNK>, or to the padding id when the vocabulary has no
+    <UNK>; batches padded with the padding id, mask True = pad."""
+
+    def __init__(self, vocab_path=None, vocab_list=None, padding_token="<PAD>", unk_token="<UNK>"):
+        import json
+        if vocab_path is not None:
+            with open(vocab_path, "r", encoding="utf-8") as f:
+                vocab_list = json.load(f)
+        elif vocab_list is None:
+            raise ValueError("Either vocab_path or vocab_list must be provided")
+        self.vocab_list = list(vocab_list)
+        self.phoneme_to_id = {ph: i for i, ph in enumerate(self.vocab_list)}
+        self.id_to_phoneme = {i: ph for ph, i in self.phoneme_to_id.items()}
+        self.vocab_size = len(self.vocab_list)
+        self.padding_token, self.unk_token = padding_token, unk_token
+        self.padding_id = self.phoneme_to_id.get(padding_token, 0)
+        self.unk_id = self.phoneme_to_id.get(unk_token, self.padding_id)
+
+    def text_to_phonemes(self, text, g2p_processor=None):
+        if g2p_processor is None:
+            return text.split()                  # pre-phonemized, space separated
+        r = g2p_processor(text)
+        if isinstance(r, dict):
+            return r.get("ph", "").split()
+        return r.split() if isinstance(r, str) else r
+
+    def phonemes_to_ids(self, phonemes):
+        return [self.phoneme_to_id.get(ph, self.unk_id) for ph in phonemes]
+
+    def ids_to_phonemes(self, ids):
+        return [self.id_to_phoneme.get(i, self.unk_token) for i in ids]
+
+    def process_text(self, text, g2p_processor=None, max_length=None):
+        phonemes = self.text_to_phonemes(text, g2p_processor)
+        if max_length is not None:
+            phonemes = phonemes[:max_length]
+        return self.phonemes_to_ids(phonemes), phonemes
+
+    def create_phoneme_embedding(self, embedding_dim, padding_idx=None):
+        return nn.Embedding(self.vocab_size, embedding_dim,
+                            padding_idx=self.padding_id if padding_idx is None else padding_idx)
+
+    def create_positional_encoding(self, max_length, embedding_dim, padding_idx=None):
+        return get_sinusoid_encoding_table(max_length, embedding_dim,
+                                           self.padding_id if padding_idx is None else padding_idx)
+
+    def batch_process(self, texts, g2p_processor=None, max_length=None, pad_to_max=True):
+        """-> (ids (B, L) LongTensor | list of LongTensors, lengths, mask (B, L) | None)."""
+        seqs = [self.process_text(t, g2p_processor, max_length)[0] for t in texts]
+        lengths = [len(s) for s in seqs]
+        if not pad_to_max:
+            return [torch.LongTensor(s) for s in seqs], lengths, None
+        L = max(lengths) if lengths else 0
+        ids = torch.LongTensor([s + [self.padding_id] * (L - len(s)) for s in seqs])
+        mask = torch.arange(L)[None, :] >= torch.tensor(lengths, dtype=torch.long)[:, None] if lengths else \
+            torch.zeros(0, 0, dtype=torch.bool)
+        return ids, lengths, mask
+
+
+__all__ = ["TextProcessor", "TextEncoder", "DurationPredictor", "VariancePredictor", "FFTBlock", "MultiHeadAttention",
+           "PositionwiseFeedForward", "Conv", "get_sinusoid_encoding_table", "conv1d_same"]

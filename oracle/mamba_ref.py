@@ -176,6 +176,68 @@ def codec_ce_loss_ref(logits, targets, pad_id=0):
     return F.cross_entropy(logits.reshape(B * T, V), targets.reshape(B * T), ignore_index=pad_id)
 
 
+def sinusoid_table_ref(n_position, d_hid, padding_idx=None):
+    """FastSpeech2 transformer/Models.py get_sinusoid_encoding_table (the
+    reference's text_encoder.py:16, :74-77), elementwise in float64."""
+    t = torch.zeros(n_position, d_hid, dtype=torch.float64)
+    for pos in range(n_position):
+        for i in range(d_hid):
+            a = pos / 10000 ** (2 * (i // 2) / d_hid)
+            t[pos, i] = math.sin(a) if i % 2 == 0 else math.cos(a)
+    if padding_idx is not None:
+        t[padding_idx] = 0.0
+    return t
+
+
+def _conv_ref(x, w, b, pad):
+    return F.conv1d(x.transpose(1, 2), w, b, padding=pad).transpose(1, 2)
+
+
+def text_encoder_ref(p, ids, mask, n_layers, n_head, d_k, kernel=(9, 1)):
+    """Restates text_encoder.py:87-128 with FastSpeech2's FFTBlock /
+    MultiHeadAttention / ScaledDotProductAttention / PositionwiseFeedForward
+    (transformer/Layers.py, SubLayers.py, Modules.py; ming024, unpinned):
+    x = emb + pos; per layer: attn = softmax(q k^T / sqrt(d_k), pad keys -inf)
+    v -> fc -> LN(+res) -> masked_fill(pad, 0) -> conv FFN -> LN(+res) ->
+    masked_fill(pad, 0).  Dropout off."""
+    B, L = ids.shape
+    x = p["phoneme_emb.weight"][ids] + p["position_enc"][0, :L][None]
+    for i in range(n_layers):
+        pre = f"layer_stack.{i}."
+        res = x
+        q = x @ p[pre + "slf_attn.w_qs.weight"].T + p[pre + "slf_attn.w_qs.bias"]
+        k = x @ p[pre + "slf_attn.w_ks.weight"].T + p[pre + "slf_attn.w_ks.bias"]
+        v = x @ p[pre + "slf_attn.w_vs.weight"].T + p[pre + "slf_attn.w_vs.bias"]
+        qh = q.view(B, L, n_head, d_k).transpose(1, 2)
+        kh = k.view(B, L, n_head, d_k).transpose(1, 2)
+        vh = v.view(B, L, n_head, d_k).transpose(1, 2)
+        s = (qh @ kh.transpose(-1, -2)) / math.sqrt(d_k)
+        s = s.masked_fill(mask[:, None, None, :], float("-inf"))
+        o = (torch.softmax(s, -1) @ vh).transpose(1, 2).reshape(B, L, n_head * d_k)
+        o = o @ p[pre + "slf_attn.fc.weight"].T + p[pre + "slf_attn.fc.bias"]
+        x = layer_norm_ref(o + res, p[pre + "slf_attn.layer_norm.weight"], p[pre + "slf_attn.layer_norm.bias"])
+        x = x.masked_fill(mask[..., None], 0.0)
+        res = x
+        h = torch.relu(_conv_ref(x, p[pre + "pos_ffn.w_1.weight"], p[pre + "pos_ffn.w_1.bias"], (kernel[0] - 1) // 2))
+        h = _conv_ref(h, p[pre + "pos_ffn.w_2.weight"], p[pre + "pos_ffn.w_2.bias"], (kernel[1] - 1) // 2)
+        x = layer_norm_ref(h + res, p[pre + "pos_ffn.layer_norm.weight"], p[pre + "pos_ffn.layer_norm.bias"])
+        x = x.masked_fill(mask[..., None], 0.0)
+    return x
+
+
+def duration_predictor_ref(p, x, mask, kernel=3):
+    """Restates text_encoder.py:131-181 -> FastSpeech2 model/modules.py
+    VariancePredictor: [conv(k, pad (k-1)/2) -> relu -> LN] x 2 (the second
+    conv's padding is 1) -> linear -> squeeze -> masked_fill(pad, 0)."""
+    c = "predictor.conv_layer."
+    h = torch.relu(_conv_ref(x, p[c + "conv1d_1.conv.weight"], p[c + "conv1d_1.conv.bias"], (kernel - 1) // 2))
+    h = layer_norm_ref(h, p[c + "layer_norm_1.weight"], p[c + "layer_norm_1.bias"])
+    h = torch.relu(_conv_ref(h, p[c + "conv1d_2.conv.weight"], p[c + "conv1d_2.conv.bias"], 1))
+    h = layer_norm_ref(h, p[c + "layer_norm_2.weight"], p[c + "layer_norm_2.bias"])
+    out = (h @ p["predictor.linear_layer.weight"].T + p["predictor.linear_layer.bias"]).squeeze(-1)
+    return out.masked_fill(mask, 0.0) if mask is not None else out
+
+
 def length_regulator_ref(hidden, durations, max_len=None):
     """Restates style_cross_attention.py:156-198 (LengthRegulator.forward):
     durations rounded half-to-even (torch.round) and clamped >= 0; row b of

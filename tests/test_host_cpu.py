@@ -30,3 +30,31 @@ def test_clip_into_optimizer_equals_clip_grad_norm():
         torch.testing.assert_close(n1, n2)
         for a, b in zip(ps1, ps2):
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_text_processor_batching():
+    """text_encoder.TextProcessor (host side of reference text_encoder.py:212-428)
+    with the reference's own phoneme vocabulary (tests/golden/phoneme_vocab.json,
+    a data file of the reference): ids, the <UNK> -> padding-id fallback of a
+    vocabulary without <UNK>, truncation, padding and the True = pad mask."""
+    import json
+    import os
+    import text_encoder as te
+    from conftest import GOLDEN
+    path = os.path.join(GOLDEN, "phoneme_vocab.json")
+    vocab = json.load(open(path))
+    tp = te.TextProcessor(vocab_path=path)
+    assert tp.vocab_size == len(vocab) and tp.padding_id == vocab.index("<PAD>")
+    assert tp.unk_id == (vocab.index("<UNK>") if "<UNK>" in vocab else tp.padding_id)
+    ids, ph = tp.process_text("HH AH0 L OW1 QQQ")
+    assert ph == ["HH", "AH0", "L", "OW1", "QQQ"]
+    assert ids == [vocab.index("HH"), vocab.index("AH0"), vocab.index("L"), vocab.index("OW1"), tp.unk_id]
+    assert tp.ids_to_phonemes(ids[:4]) == ph[:4]
+    batch, lengths, mask = tp.batch_process(["HH AH0", "L OW1 HH AH0 L", "OW1"], max_length=4)
+    assert lengths == [2, 4, 1] and batch.shape == (3, 4)
+    assert batch[0].tolist() == [vocab.index("HH"), vocab.index("AH0"), tp.padding_id, tp.padding_id]
+    assert mask.tolist() == [[False, False, True, True], [False] * 4, [False, True, True, True]]
+    seqs, lengths, mask = tp.batch_process(["HH", "L OW1"], pad_to_max=False)
+    assert [s.tolist() for s in seqs] == [[vocab.index("HH")], [vocab.index("L"), vocab.index("OW1")]] and mask is None
+    tab = tp.create_positional_encoding(10, 8)
+    assert tab.shape == (10, 8) and float(tab[tp.padding_id].abs().sum()) == 0.0
