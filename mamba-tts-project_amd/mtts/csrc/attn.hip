@@ -300,19 +300,21 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
   const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;  // tr_read addressing
   const int b = blockIdx.z, hh = blockIdx.y, chunk = blockIdx.x;
   const int d = f.heads * HD;
-  const int qbeg = MODE == kBwdKV ? 0 : MODE == kBwdQ ? 32 * chunk : chunk * p.qchunk;
-  const int qend = MODE == kBwdKV ? f.q_len : min(f.q_len, MODE == kBwdQ ? qbeg + 32 : qbeg + p.qchunk);
+  const int nkg = (f.kv_len + KG - 1) / KG;
+  // mode 1: grid.x = key group x query chunk (chunk of p.qchunk queries)
+  const int kv_kg = chunk % nkg, qc = MODE == kBwdKV ? chunk / nkg : chunk;
+  const int qbeg = MODE == kBwdQ ? 32 * chunk : qc * p.qchunk;
+  const int qend = min(f.q_len, MODE == kBwdQ ? qbeg + 32 : qbeg + p.qchunk);
   const float c = f.scale * kLog2e;
   const float inv_scale = 1.f / f.scale;
   const uint8_t* mb = f.key_padding_mask ? f.key_padding_mask + b * f.mask_bs : nullptr;
-  const int nkg = (f.kv_len + KG - 1) / KG;
   float* const dbuf = p.delta ? p.delta + ((int64_t)b * f.heads + hh) * f.q_len : nullptr;
   constexpr int NQT = (ND + NW - 1) / NW;   // mode 2: dQ tiles per wave, held across key groups
   f32x16 QA[NQT];
 #pragma unroll
   for (int t = 0; t < NQT; ++t) QA[t] = f32x16{};
 
-  for (int kg = MODE == kBwdKV ? chunk : 0; kg < (MODE == kBwdKV ? chunk + 1 : nkg); ++kg) {
+  for (int kg = MODE == kBwdKV ? kv_kg : 0; kg < (MODE == kBwdKV ? kv_kg + 1 : nkg); ++kg) {
     const int kg0 = kg * KG;
     __syncthreads();
     {
@@ -521,8 +523,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
         const int kk = kg0 + wave * 32 + acc_row(i, h);
         if (kk >= f.kv_len) continue;
         const float vk = dK[dt][i] * f.scale, vv = dV[dt][i];
-        if (MODE == kBwdShort && p.nchunk > 1) {
-          float* pr = p.part + (((int64_t)chunk * f.batch + b) * f.kv_len + kk) * (2 * d) + hh * HD + dim;
+        if (p.nchunk > 1) {
+          float* pr = p.part + (((int64_t)qc * f.batch + b) * f.kv_len + kk) * (2 * d) + hh * HD + dim;
           pr[0] = vk;
           pr[d] = vv;
         } else {
@@ -766,8 +768,22 @@ BwdPlan plan_bwd(int batch, int heads, int head_dim, int q_len, int kv_len, int 
   pl.nchunk = (q_len + pl.qchunk - 1) / pl.qchunk;
   if (pl.nchunk < 1) pl.nchunk = 1;
   const int64_t d = (int64_t)heads * head_dim;
-  pl.split = kv_len > pl.kg && !getenv("MTTS_ATTN_BWD_FUSED");
+  // split backward (dQ pass + dK/dV pass) for a key side longer than one key
+  // group; the dK/dV pass may be chunked over queries into partials.  (For
+  // one key group, C2's 128 text keys, the split form measured 112 us against
+  // the fused mode-0 kernel's 106 us per call and is not used.)
+  pl.split = (kv_len > pl.kg || getenv("MTTS_ATTN_BWD_SPLIT")) && !getenv("MTTS_ATTN_BWD_FUSED");
   if (pl.split) {
+    const int nkg = (kv_len + pl.kg - 1) / pl.kg;
+    const int wgs = nkg * base;
+    int nc = wgs >= 256 ? 1 : (256 + wgs - 1) / wgs;
+    if (const char* e = getenv("MTTS_ATTN_CHUNKS")) nc = atoi(e);
+    nc = nc < 1 ? 1 : (nc > slices ? (slices > 0 ? slices : 1) : nc);
+    const int per2 = (slices + nc - 1) / nc;
+    pl.qchunk = 32 * (per2 > 0 ? per2 : 1);
+    pl.nchunk = (q_len + pl.qchunk - 1) / pl.qchunk;
+    if (pl.nchunk < 1) pl.nchunk = 1;
+    pl.part_bytes = pl.nchunk > 1 ? (int64_t)pl.nchunk * batch * kv_len * 2 * d * 4 : 0;
     pl.delta_bytes = ((int64_t)batch * heads * q_len * 4 + 255) / 256 * 256;
     return pl;
   }
@@ -790,7 +806,7 @@ void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
     } else {
       attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
     }
-    attn_bwd_kernel<T, HD, kBwdKV><<<dim3((f.kv_len + KG - 1) / KG, f.heads, f.batch), NT, 0, st>>>(p);
+    attn_bwd_kernel<T, HD, kBwdKV><<<dim3((f.kv_len + KG - 1) / KG * p.nchunk, f.heads, f.batch), NT, 0, st>>>(p);
     return;
   }
   attn_bwd_kernel<T, HD, kBwdShort><<<dim3(p.nchunk, f.heads, f.batch), NT, 0, st>>>(p);
@@ -804,7 +820,7 @@ void dispatch_bwd(const BwdParams& p, bool split, hipStream_t st) {
     case 64: launch_bwd<T, 64>(p, split, st); break;
     default: launch_bwd<T, 128>(p, split, st); break;
   }
-  if (!split && p.nchunk > 1) {
+  if (p.nchunk > 1) {
     const int64_t n = (int64_t)p.a.f.batch * p.a.f.kv_len * 2 * p.a.f.heads * p.a.f.head_dim;
     int blocks = (int)((n + 255) / 256);
     if (blocks > 4096) blocks = 4096;

@@ -1,0 +1,43 @@
+"""Attention fwd/bwd timing at the C2 (T_kv=128) and C5 (T_kv=5248) shapes,
+with env variants (MTTS_ATTN_CHUNKS ...).  python tools/attn_ab.py"""
+import os
+import sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mamba-tts-project_amd")]
+import torch  # noqa: E402
+from mtts import attn_kernels as A  # noqa: E402
+
+
+def timed(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record()
+    for _ in range(it):
+        fn()
+    e[1].record()
+    e[1].synchronize()
+    return e[0].elapsed_time(e[1]) / it
+
+
+for name, (B, T, S) in {"C2": (8, 2048, 128), "C5": (4, 5120, 5248)}.items():
+    H, hd = 8, 128
+    d = H * hd
+    g = torch.Generator(device="cuda").manual_seed(0)
+    q = torch.randn(B, T, d, device="cuda", generator=g).to(torch.bfloat16)
+    k = torch.randn(B, S, d, device="cuda", generator=g).to(torch.bfloat16)
+    v = torch.randn(B, S, d, device="cuda", generator=g).to(torch.bfloat16)
+    kpm = torch.zeros(B, S, dtype=torch.bool, device="cuda")
+    kpm[:, int(S * 0.9):] = True
+    out, lse = A.attention_fwd(q, k, v, H, kpm, want_lse=True)
+    do = torch.randn_like(out)
+    fl = 4 * B * T * S * d
+    tf = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
+    print(f"{name} fwd {tf * 1e3:.1f} us {fl / tf / 1e9:.0f} TF/s", flush=True)
+    for ch in ([None, "8", "16", "32"] if name == "C2" else [None]):
+        if ch:
+            os.environ["MTTS_ATTN_CHUNKS"] = ch
+        tb = timed(lambda: A.attention_bwd(q, k, v, H, kpm, out, lse, do))
+        os.environ.pop("MTTS_ATTN_CHUNKS", None)
+        print(f"{name} bwd chunks={ch} {tb * 1e3:.1f} us {2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
