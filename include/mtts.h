@@ -186,6 +186,12 @@ typedef struct {
   const void* z;             /* optional */
   const float* dt_bias;      /* optional */
   void* out;                 /* (B, D) */
+  /* optional fused dt_proj (Mamba.step: dt = dt_proj(x_db[:, :dt_rank])):
+   * with dt_rank > 0, `dt` is the (B, dt_rank) low-rank input (row stride
+   * dt_bs, dtype_io) and raw delta[b, c] = sum_r dt[b, r] * dt_w[c, r],
+   * dt_w (D, dt_rank) row-major, dtype_io. */
+  int dt_rank;
+  const void* dt_w;
 } MttsStateUpdateArgs;
 
 int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* stream);
@@ -382,6 +388,18 @@ int mtts_clip_adam(const MttsAdamTensor* tensors, int ntensors, int64_t total_ch
 int mtts_embed_sum(const int64_t* tokens, int64_t tok_bs, const int* quant_ids, const int* pos_ids,
                    const float* tok_w, const float* q_w, const float* pos_w, int batch, int L, int d, int vocab,
                    void* out, int dtype, int64_t out_bs, int* err_flag, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Decode-step projections (MambaTTSDecoder.decode_step, mamba_decoder.py:
+ * 188-256 -> Mamba.step in_proj/x_proj/dt_proj/out_proj, the cross-attention
+ * q/out projections and the FFN of every layer): y = x W^T (+ bias), then
+ * act 0 = identity, 1 = GELU (exact erf, F.gelu).  bf16 in / out, fp32
+ * accumulation; x is M x K (M <= 32 rows, row stride ldx), W is N x K (the
+ * nn.Linear weight, row stride ldw), bias bf16 or NULL, y M x N (row stride
+ * ldy).  K must be a multiple of 64; x and W 16-byte aligned.
+ * ------------------------------------------------------------------------ */
+int mtts_gemm_rows_bf16(const void* x, int64_t ldx, int M, const void* W, int64_t ldw, int N, int K,
+                        const void* bias, int act, void* y, int64_t ldy, void* stream);
 
 #ifdef __cplusplus
 }

@@ -65,7 +65,7 @@ class StateUpdateArgs(C.Structure):
                 ("dt_softplus", i32),
                 ("x_bs", i64), ("dt_bs", i64), ("z_bs", i64), ("out_bs", i64), ("B_bs", i64), ("C_bs", i64),
                 ("state", vp), ("x", vp), ("dt", vp), ("A", vp), ("Bm", vp), ("Cm", vp), ("D", vp), ("z", vp),
-                ("dt_bias", vp), ("out", vp)]
+                ("dt_bias", vp), ("out", vp), ("dt_rank", i32), ("dt_w", vp)]
 
 
 class LNArgs(C.Structure):
@@ -128,6 +128,7 @@ _SIGS = {
     "mtts_clip_adam": ([vp, i32, i64, vp, f32, f32, f32, f32, f32, f32, vp, vp, vp], i32),
     "mtts_embed_sum": ([vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, i32, i64, vp, vp], i32),
     "mtts_cast_tiles": ([i32, i32], i64),
+    "mtts_gemm_rows_bf16": ([vp, i64, i32, vp, i64, i32, i32, vp, i32, vp, i64, vp], i32),
     "mtts_cast_bf16_multi": ([vp, i32, i64, vp], i32),
     "mtts_length_regulate_lengths": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_length_regulate_fwd": ([vp, i32, i32, i32, i32, i64, i64, vp, i64, i32, vp, i64, i64, vp], i32),

@@ -739,6 +739,104 @@ void launch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
   attn_fwd_kernel<T, HD><<<grid, 64 * nw, 0, st>>>(*a);
 }
 
+// ---------------------------------------------------------------------------
+// Single-query forward (q_len == 1: MambaTTSDecoder.decode_step's
+// cross-attention, mamba_decoder.py:222-236).  One workgroup per (batch,
+// head), 4 waves; a group of G = HD/8 lanes owns one key at a time (8 dims
+// per lane, one 16-byte load of K and of V per lane and key), the key axis
+// is strided over the 256/G groups of the workgroup and each group keeps an
+// online softmax (m, l, acc[8]); the groups are merged through LDS.  K and V
+// of up to 4 keys per group are loaded before any arithmetic.  HBM-bound:
+// every K/V byte of the (batch, head) read exactly once.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float* v) {
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    const s16x8 x = *reinterpret_cast<const s16x8*>(p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(((uint32_t)(uint16_t)x[e]) << 16);
+  } else {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = a[e], v[4 + e] = b[e];
+  }
+}
+
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void attn_decode_kernel(MttsAttnFwdArgs a) {
+  constexpr int G = HD / 8, NG = 256 / G, U = 4;
+  __shared__ float sm[NG], sl[NG], sacc[NG][HD + 1];
+  const int bh = blockIdx.x, b = bh / a.heads, hh = bh % a.heads;
+  const int g = threadIdx.x / G, gl = threadIdx.x % G, d0 = gl * 8;
+  const float c = a.scale * kLog2e;
+  const uint8_t* mb = a.key_padding_mask ? a.key_padding_mask + b * a.mask_bs : nullptr;
+  float q[8];
+  ld8((const T*)a.q + b * a.q_bs + hh * HD + d0, q);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] *= c;
+  const T* kb = (const T*)a.k + b * a.k_bs + hh * HD + d0;
+  const T* vb = (const T*)a.v + b * a.v_bs + hh * HD + d0;
+  float m = -INFINITY, l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j0 = g; j0 < a.kv_len; j0 += NG * U) {
+    float kx[U][8], vx[U][8];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * NG;
+      ok[u] = j < a.kv_len && !(mb && mb[j]);
+      const int jj = j < a.kv_len ? j : j0;
+      ld8(kb + (int64_t)jj * a.k_ls, kx[u]);
+      ld8(vb + (int64_t)jj * a.v_ls, vx[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += q[e] * kx[u][e];
+#pragma unroll
+      for (int o = 1; o < G; o <<= 1) s += __shfl_xor(s, o);
+      if (!ok[u]) continue;
+      const float mn = fmaxf(m, s), f = exp2f(m - mn), p = exp2f(s - mn);
+      l = l * f + p;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = acc[e] * f + p * vx[u][e];
+      m = mn;
+    }
+  }
+  if (gl == 0) sm[g] = m, sl[g] = l;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sacc[g][d0 + e] = acc[e];
+  __syncthreads();
+  if (threadIdx.x < HD) {
+    float M = -INFINITY;
+    for (int i = 0; i < NG; ++i) M = fmaxf(M, sm[i]);
+    float L = 0.f, o = 0.f;
+    for (int i = 0; i < NG; ++i) {
+      const float f = sm[i] == -INFINITY ? 0.f : exp2f(sm[i] - M);
+      L += sl[i] * f;
+      o += sacc[i][threadIdx.x] * f;
+    }
+    // fully masked: L = 0 -> 0/0 = NaN (torch MHA), lse = -inf
+    mtts::stf((T*)a.out + b * a.o_bs + hh * HD + threadIdx.x, o / L);
+    if (a.lse && threadIdx.x == 0) a.lse[(int64_t)b * a.heads + hh] = M == -INFINITY ? -INFINITY : (M + log2f(L)) * kLn2;
+  }
+}
+
+template <typename T, int HD>
+void launch_decode(const MttsAttnFwdArgs* a, hipStream_t st) {
+  hipLaunchKernelGGL((attn_decode_kernel<T, HD>), dim3(a->batch * a->heads), dim3(256), 0, st, *a);
+}
+
+template <typename T>
+void dispatch_decode(const MttsAttnFwdArgs* a, hipStream_t st) {
+  switch (a->head_dim) {
+    case 16: launch_decode<T, 16>(a, st); break;
+    case 32: launch_decode<T, 32>(a, st); break;
+    case 64: launch_decode<T, 64>(a, st); break;
+    default: launch_decode<T, 128>(a, st); break;
+  }
+}
+
 template <typename T>
 void dispatch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
   switch (a->head_dim) {
@@ -836,10 +934,11 @@ extern "C" int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream) {
   if (rc) return rc;
   if (a->batch == 0 || a->q_len == 0) return MTTS_OK;
   hipStream_t st = (hipStream_t)stream;
+  const bool one = a->q_len == 1 && !getenv("MTTS_ATTN_DECODE_OFF");   // decode step: single-query kernel
   if (a->dtype == MTTS_BF16)
-    dispatch_fwd<bf16_t>(a, st);
+    one ? dispatch_decode<bf16_t>(a, st) : dispatch_fwd<bf16_t>(a, st);
   else
-    dispatch_fwd<float>(a, st);
+    one ? dispatch_decode<float>(a, st) : dispatch_fwd<float>(a, st);
   MTTS_LAUNCH_CHECK("attention_fwd");
   return MTTS_OK;
 }

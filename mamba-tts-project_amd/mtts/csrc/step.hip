@@ -33,7 +33,35 @@ __global__ void state_update_kernel(const MttsStateUpdateArgs a) {
   const int c = idx % a.dim;
   const int b = idx / a.dim;
   const float x = ldf((const Tio*)a.x + (int64_t)b * a.x_bs + c);
-  float dt = ldf((const Tio*)a.dt + (int64_t)b * a.dt_bs + c) + (a.dt_bias ? a.dt_bias[c] : 0.f);
+  float dt;
+  if (a.dt_rank > 0) {   // fused dt_proj: low-rank input row of batch b . dt_w row c
+    const Tio* xr = (const Tio*)a.dt + (int64_t)b * a.dt_bs;
+    const Tio* wr = (const Tio*)a.dt_w + (int64_t)c * a.dt_rank;
+    float s0 = 0.f, s1 = 0.f;
+    int r = 0;
+    if constexpr (sizeof(Tio) == 2) {   // 16-byte pieces when the rows allow it
+      if ((a.dt_rank & 7) == 0 && (((uintptr_t)xr | (uintptr_t)wr) & 15) == 0) {
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        for (; r < a.dt_rank; r += 8) {
+          const s16x8 xv = *reinterpret_cast<const s16x8*>(xr + r), wv = *reinterpret_cast<const s16x8*>(wr + r);
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            s0 = fmaf(bf2f((bf16_t)xv[e]), bf2f((bf16_t)wv[e]), s0);
+            s1 = fmaf(bf2f((bf16_t)xv[e + 1]), bf2f((bf16_t)wv[e + 1]), s1);
+          }
+        }
+      }
+    }
+    for (; r + 1 < a.dt_rank; r += 2) {
+      s0 = fmaf(ldf(xr + r), ldf(wr + r), s0);
+      s1 = fmaf(ldf(xr + r + 1), ldf(wr + r + 1), s1);
+    }
+    if (r < a.dt_rank) s0 = fmaf(ldf(xr + r), ldf(wr + r), s0);
+    dt = s0 + s1;
+  } else {
+    dt = ldf((const Tio*)a.dt + (int64_t)b * a.dt_bs + c);
+  }
+  dt += a.dt_bias ? a.dt_bias[c] : 0.f;
   if (a.dt_softplus) dt = softplus_f(dt);
   const float dtx = dt * x;
   float4* sp = reinterpret_cast<float4*>(a.state + idx * 16);
@@ -84,6 +112,7 @@ extern "C" int mtts_causal_conv1d_update(const MttsConvUpdateArgs* a, void* stre
 extern "C" int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* stream) {
   MTTS_CHECK(a && a->state && a->x && a->dt && a->A && a->Bm && a->Cm && a->out, "state_update: null tensor");
   MTTS_CHECK(a->batch > 0 && a->dim > 0, "state_update: bad sizes");
+  MTTS_CHECK(a->dt_rank >= 0 && (a->dt_rank == 0 || a->dt_w), "state_update: dt_rank > 0 needs dt_w");
   if (a->dstate != 16) {
     set_error("state_update: dstate=%d unsupported", a->dstate);
     return MTTS_EUNSUPPORTED;

@@ -14,12 +14,17 @@ Engine path (inference only: torch.no_grad, HIP tensors):
     conv-window + state-update kernels, states updated in place) -> fused
     residual+LN -> q-projection + attention over cached K/V -> fused
     residual+LN+FiLM -> FFN; the FFN residual is fused into the next LN;
+  * the <= 32-row projections (in/x/dt/out_proj, q/out_proj, FFN, head) on
+    the HIP skinny GEMM of csrc/rows.hip (bias + GELU fused) for bf16;
+  * dt_proj fused into the selective state update (B / C read in place);
   * optional hipGraph capture of the whole step (static token / position /
     state buffers): replay costs one launch instead of ~25 per layer.
 Numerics are those of the eager module path (tests/test_gpu_modules.py).
 Call `reset()` after modifying weights in place between decode steps.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
@@ -35,10 +40,23 @@ def _key(t):
     return (t.data_ptr(), t._version, tuple(t.shape), t.dtype)
 
 
+def _proj_blas(x, w, b=None, act=None):
+    y = x @ w.t() if b is None else torch.addmm(b, x, w.t())
+    return F.gelu(y) if act == "gelu" else y
+
+
+def _proj_rows(x, w, b=None, act=None):
+    """HIP skinny GEMM (csrc/rows.hip) for the <= 32-row decode projections."""
+    if ops.gemm_rows_ok(x, w):
+        return ops.gemm_rows(x, w, b, act)
+    return _proj_blas(x, w, b, act)
+
+
 class DecodeEngine:
-    def __init__(self, model, use_graph=True):
+    def __init__(self, model, use_graph=True, use_rows=True):
         self.m = model
         self.use_graph = use_graph
+        self.use_rows = use_rows and os.environ.get("MTTS_DECODE_ROWS", "1") != "0"
         self.reset()
 
     def reset(self):
@@ -87,6 +105,7 @@ class DecodeEngine:
         cd = c["cd"]
         x = (F.embedding(tok, m.token_embed.weight) + F.embedding(pos, m.pos_embed.weight)[None]).to(cd)
         x = x.view(c["B"], -1)                                               # (B, d)
+        mm_ = _proj_rows if (self.use_rows and cd == torch.bfloat16) else _proj_blas
         pending = None
         for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
             conv_state, ssm_state = states[i]
@@ -96,22 +115,22 @@ class DecodeEngine:
                 x = xs
             mm = l.mamba
             di, N, r = mm.d_inner, mm.d_state, mm.dt_rank
-            xz = h @ p["Win"].t()
+            xz = mm_(h, p["Win"])
             u = ops.conv_update(xz[:, :di], conv_state, p["conv_w"], p["conv_b"], True)
-            x_dbl = u @ p["Wx"].t()
-            delta = x_dbl[:, :r] @ p["Wdt"].t()
-            y = ops.state_update(ssm_state, u, delta, p["A"], x_dbl[:, r:r + N].contiguous(),
-                                 x_dbl[:, r + N:].contiguous(), p["D"], xz[:, di:], p["dt_bias"], True)
-            h_m = y @ p["Wout"].t()
+            x_dbl = mm_(u, p["Wx"])
+            # dt_proj fused into the state update; B / C read in place from x_dbl
+            y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
+                                 xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"])
+            h_m = mm_(y, p["Wout"])
             h, x = ops.layer_norm(h_m, l.norm_cross.weight, l.norm_cross.bias, l.norm_cross.eps, res=x)
-            q = torch.addmm(p["bq"], h, p["Wq"].t())
+            q = mm_(h, p["Wq"], p["bq"])
             o = attention(q[:, None], p["k"], p["v"], l.cross_attn.num_heads, c["kpm"])[:, 0]
-            a = torch.addmm(p["bo"], o, p["Wo"].t())
+            a = mm_(o, p["Wo"], p["bo"])
             h, x = ops.layer_norm(a, l.norm_ff.weight, l.norm_ff.bias, l.norm_ff.eps, res=x,
                                   gamma=p["gamma"], beta=p["beta"], rows_per_group=1)
-            pending = torch.addmm(p["b2"], F.gelu(torch.addmm(p["b1"], h, p["W1"].t())), p["W2"].t())
+            pending = mm_(mm_(h, p["W1"], p["b1"], "gelu"), p["W2"], p["b2"])
         h, _ = ops.layer_norm(pending, m.norm_out.weight, m.norm_out.bias, m.norm_out.eps, res=x)
-        return torch.addmm(c["bh"], h, c["Wh"].t())[:, None]
+        return mm_(h, c["Wh"], c["bh"])[:, None]
 
     # -- public ----------------------------------------------------------------
     @torch.no_grad()

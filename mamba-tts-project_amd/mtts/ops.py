@@ -258,9 +258,14 @@ def conv_update(x, conv_state, w, bias=None, silu=True, out=None):
     return out
 
 
-def state_update(state, x, dt, A, Bm, Cm, D=None, z=None, dt_bias=None, softplus=True, out=None):
-    """state (B, D, N) fp32 updated IN PLACE; x/dt/z (B, D); Bm/Cm (B, N)."""
-    _check_cuda(state, x, dt, A, Bm, Cm)
+def state_update(state, x, dt, A, Bm, Cm, D=None, z=None, dt_bias=None, softplus=True, out=None, dt_w=None):
+    """state (B, D, N) fp32 updated IN PLACE; x/z (B, D); Bm/Cm (B, N) with
+    unit element stride; dt (B, D) raw delta, or with dt_w (D, R) given the
+    (B, R) low-rank input of dt_proj (fused: delta = dt @ dt_w.t())."""
+    _check_cuda(state, x, dt, A, Bm, Cm, dt_w)
+    for t in (Bm, Cm, dt):
+        if t.stride(-1) != 1:
+            raise ValueError("state_update: B / C / dt need unit element stride")
     Bsz, Dm = x.shape
     out = torch.empty(Bsz, Dm, device=x.device, dtype=x.dtype) if out is None else out
     a = L.StateUpdateArgs()
@@ -271,6 +276,10 @@ def state_update(state, x, dt, A, Bm, Cm, D=None, z=None, dt_bias=None, softplus
         a.z_bs = z.stride(0)
     a.state, a.x, a.dt, a.A, a.Bm, a.Cm = state.data_ptr(), x.data_ptr(), dt.data_ptr(), A.data_ptr(), Bm.data_ptr(), Cm.data_ptr()
     a.D, a.z, a.dt_bias, a.out = L.ptr(D), L.ptr(z), L.ptr(dt_bias), out.data_ptr()
+    if dt_w is not None:
+        if dt_w.dtype != x.dtype or dt_w.shape != (Dm, dt.shape[1]) or not dt_w.is_contiguous() or dt.dtype != x.dtype:
+            raise ValueError("state_update: dt_w must be a contiguous (D, R) tensor of x's dtype")
+        a.dt_rank, a.dt_w = dt_w.shape[1], dt_w.data_ptr()
     L.call("mtts_selective_state_update", a)
     return out
 
@@ -477,3 +486,38 @@ def length_regulate(hidden, durations, max_len=None):
     if max_len is None:
         max_len = int(lengths.max().item()) if lengths.numel() > 0 else 0
     return LengthRegulateFn.apply(hidden, durations, int(max_len)), lengths
+
+
+# ---------------------------------------------------------------------------
+# decode-step projections (M <= 32 rows)
+# ---------------------------------------------------------------------------
+GEMM_ROWS_MAX = 32
+
+
+def gemm_rows_ok(x, weight):
+    """True when mtts_gemm_rows_bf16 takes y = x @ weight.t() as given."""
+    return (x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.dim() == 2
+            and 0 < x.shape[0] <= GEMM_ROWS_MAX and x.shape[1] % 64 == 0 and x.stride(1) == 1
+            and weight.stride(1) == 1 and x.stride(0) % 8 == 0 and weight.stride(0) % 8 == 0
+            and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
+
+
+def gemm_rows(x, weight, bias=None, act=None):
+    """y = act(x @ weight.t() + bias) for the decode step's skinny GEMMs
+    (x: M <= 32 rows, bf16; act None or "gelu" = exact-erf F.gelu)."""
+    _check_cuda(x, weight, bias)
+    if not gemm_rows_ok(x, weight):
+        raise ValueError(f"gemm_rows: unsupported operands x{tuple(x.shape)}/{x.stride()} "
+                         f"w{tuple(weight.shape)}/{weight.stride()} {x.dtype}")
+    M, K = x.shape
+    N = weight.shape[0]
+    if weight.shape[1] != K:
+        raise ValueError("gemm_rows: K mismatch")
+    if bias is not None:
+        bias = bias.to(torch.bfloat16).contiguous()
+        if bias.numel() != N:
+            raise ValueError("gemm_rows: bias size")
+    y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+    L.call_raw("mtts_gemm_rows_bf16", x.data_ptr(), x.stride(0), M, weight.data_ptr(), weight.stride(0), N, K,
+               L.ptr(bias), {None: 0, "gelu": 1}[act], y.data_ptr(), y.stride(0))
+    return y

@@ -58,6 +58,11 @@ CASES = [  # B, T, S, H, hd
     (2, 1, 128, 8, 128),
     (1, 5, 300, 2, 64),
     (2, 17, 1, 2, 32),
+    # single query (decode step; attn_decode_kernel): every head dim, ragged / long key sides
+    (3, 1, 12, 4, 16),
+    (2, 1, 5, 2, 32),
+    (1, 1, 300, 2, 64),
+    (32, 1, 1000, 8, 128),
 ]
 
 
@@ -124,7 +129,7 @@ def _ref_grads(q, kv, H, kpm, do):
 
 @pytest.mark.parametrize("chunks", [None, "1", "3"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("case", CASES[:-3] + [(1, 5, 300, 2, 64)])
+@pytest.mark.parametrize("case", CASES[:6] + [(1, 5, 300, 2, 64), (3, 1, 12, 4, 16)])
 def test_backward_matches_reference(case, dtype, chunks, monkeypatch):
     if chunks is not None:
         monkeypatch.setenv("MTTS_ATTN_CHUNKS", chunks)
@@ -195,3 +200,24 @@ def test_backward_c5_shape_bf16():
     rq, rkv = _ref_grads(q, kv, H, kpm, do)
     close(dq, rq, 3e-2)
     close(dkv, rkv, 3e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_single_query_fully_masked_and_generic_agree(dtype, monkeypatch):
+    """q_len == 1 (single-query kernel): a fully masked batch row is NaN with
+    lse = -inf like torch, other rows match the float64 reference and the
+    generic MFMA kernel (MTTS_ATTN_DECODE_OFF) on the same inputs."""
+    from mtts import attn_kernels as A
+    B, S, H, hd = 4, 77, 8, 128
+    q, kv, kpm = make(B, 1, S, H, hd, dtype, seed=3, full_mask_batch=2)
+    d = H * hd
+    out, lse = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+    assert torch.isnan(out[2]).all() and torch.isneginf(lse[2]).all()
+    keep = [0, 1, 3]
+    ref, ref_lse = ref_attention(q[keep], kv[keep, :, :d], kv[keep, :, d:], H, kpm[keep])
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    close(out[keep], ref, tol)
+    close(lse[keep], ref_lse, 1e-5)
+    monkeypatch.setenv("MTTS_ATTN_DECODE_OFF", "1")
+    out2, _ = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+    close(out[keep], out2[keep].double(), tol)

@@ -111,6 +111,38 @@ def test_bf16_decoder_tracks_fp32(golden):
     close(lg.float(), ref, rtol=5e-2, name="bf16 logits")
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_bf16_decode_engine_rows_vs_blas(golden, graph, monkeypatch):
+    """bf16 engine: the HIP skinny-GEMM projections (csrc/rows.hip) against
+    the same engine on hipBLASLt, and both against the fp32 module path."""
+    from mtts import ops
+    from mtts.decode import DecodeEngine
+    calls = []
+    real = ops.gemm_rows
+    monkeypatch.setattr(ops, "gemm_rows", lambda *a, **k: calls.append(1) or real(*a, **k))
+    m, g = _decoder(golden)
+    m.eval()
+    tokens = torch.from_numpy(g["tokens"]).to(DEV)
+    kw = dict(text_mask=torch.from_numpy(g["text_mask"]).to(DEV), ref_hidden=torch.from_numpy(g["ref"]).to(DEV),
+              ref_mask=torch.from_numpy(g["ref_mask"]).to(DEV))
+    text = torch.from_numpy(g["text"]).to(DEV)
+    z = torch.from_numpy(g["z_style"]).to(DEV)
+    m.compute_dtype = torch.bfloat16
+    outs = []
+    for rows in (True, False):
+        eng = DecodeEngine(m, use_graph=graph, use_rows=rows)
+        states = [None, None]
+        seq = []
+        with torch.no_grad():
+            for t in range(g["decode/logits"].shape[1]):
+                lg, states = eng.step(tokens[:, t:t + 1], text, z, states, t, **kw)
+                seq.append(lg.float().clone())
+        outs.append(torch.cat(seq, 1))
+    assert len(calls) >= 6 * 2, "skinny-GEMM path not taken"
+    close(outs[0], outs[1], rtol=3e-2, name="rows vs hipBLASLt engine (bf16)")
+    close(outs[0], g["decode/logits"], rtol=5e-2, name="bf16 rows engine vs fp32 reference")
+
+
 def test_style_pipeline_vs_reference(golden):
     import style_cross_attention as sca
     g = golden("style.npz")

@@ -328,3 +328,55 @@ def test_cast_bf16_multi(shapes):
     ps[0].add_(1.0)                # a later step re-casts the same buffers in place
     _cast_multi_bf16(ps)
     assert torch.equal(ps[0]._mtts_cast[1], ps[0].to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K,bias,act", [(32, 4096, 1024, False, None), (32, 96, 2048, False, None),
+                                            (32, 2048, 64, False, None), (32, 1024, 2048, True, None),
+                                            (32, 2048, 1024, True, "gelu"), (32, 10, 1024, True, None),
+                                            (7, 130, 192, True, "gelu"), (1, 33, 64, False, None)])
+def test_gemm_rows(M, N, K, bias, act):
+    """Decode-step skinny GEMM (csrc/rows.hip) vs a float64 reference of the
+    same bf16 operands; bound: one bf16 rounding of the output (2^-8 relative
+    to max|y|)."""
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV, torch.bfloat16) if bias else None
+    y = ops.gemm_rows(x, w, b, act)
+    ref = x.double() @ w.double().t()
+    if b is not None:
+        ref = ref + b.double()
+    if act == "gelu":
+        ref = torch.nn.functional.gelu(ref)
+    close(y, ref, rtol=2 ** -8, name="gemm_rows")
+    # strided x view (x_dbl[:, :dt_rank] in the decode step)
+    xb = torch.randn(M, K + 64, generator=g).to(DEV, torch.bfloat16)
+    close(ops.gemm_rows(xb[:, :K], w), xb[:, :K].double() @ w.double().t(), rtol=2 ** -8, name="strided")
+
+
+@pytest.mark.parametrize("dtype,R", [(torch.float32, 64), (torch.bfloat16, 64), (torch.bfloat16, 4),
+                                     (torch.float32, 7)])
+def test_state_update_fused_dt_proj(dtype, R):
+    """dt_proj fused into the state update (dt_rank > 0, strided B / C views of
+    x_dbl) equals dt_proj as a separate fp32 product followed by the plain
+    update, within one bf16 rounding of delta for bf16 I/O."""
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(R)
+    Bsz, D, N = 5, 96, 16
+    x_dbl = torch.randn(Bsz, R + 2 * N, generator=g).to(DEV, dtype)
+    u = torch.randn(Bsz, D, generator=g).to(DEV, dtype)
+    z = torch.randn(Bsz, D, generator=g).to(DEV, dtype)
+    w = (torch.randn(D, R, generator=g) / R ** 0.5).to(DEV, dtype)
+    A = -torch.rand(D, N, generator=g).to(DEV) - 0.5
+    Dv = torch.randn(D, generator=g).to(DEV)
+    bias = torch.randn(D, generator=g).to(DEV) * 0.1
+    st0 = torch.randn(Bsz, D, N, generator=g).to(DEV)
+    s1, s2 = st0.clone(), st0.clone()
+    y1 = ops.state_update(s1, u, x_dbl[:, :R], A, x_dbl[:, R:R + N], x_dbl[:, R + N:], Dv, z, bias, True, dt_w=w)
+    delta = (x_dbl[:, :R].float() @ w.float().t()).to(dtype)
+    y2 = ops.state_update(s2, u, delta, A, x_dbl[:, R:R + N].contiguous(), x_dbl[:, R + N:].contiguous(), Dv, z,
+                          bias, True)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    close(s1, s2, rtol=tol, name="state")
+    close(y1.float(), y2.float(), rtol=tol, name="y")
