@@ -391,15 +391,52 @@ int mtts_embed_sum(const int64_t* tokens, int64_t tok_bs, const int* quant_ids, 
 
 /* ------------------------------------------------------------------------
  * Decode-step projections (MambaTTSDecoder.decode_step, mamba_decoder.py:
- * 188-256 -> Mamba.step in_proj/x_proj/dt_proj/out_proj, the cross-attention
- * q/out projections and the FFN of every layer): y = x W^T (+ bias), then
- * act 0 = identity, 1 = GELU (exact erf, F.gelu).  bf16 in / out, fp32
- * accumulation; x is M x K (M <= 32 rows, row stride ldx), W is N x K (the
- * nn.Linear weight, row stride ldw), bias bf16 or NULL, y M x N (row stride
- * ldy).  K must be a multiple of 64; x and W 16-byte aligned.
+ * 188-256 -> Mamba.step in_proj/x_proj/out_proj, the cross-attention q/out
+ * projections, the FFN and the head of every step):
+ *   y = act(x W^T + bias), act 0 = identity, 1 = GELU (exact erf, F.gelu)
+ * bf16 in / out, fp32 accumulation; x is M x K (M <= 32 rows, row stride
+ * ldx), W is N x K (the nn.Linear weight, row stride ldw), bias bf16 or
+ * NULL, y M x N (row stride ldy).  K % 64 == 0; x, W 16-byte aligned.
+ * Optional fusions (they remove the LayerNorm and conv-update launches of
+ * the step):
+ *  - ln_w != NULL, LayerNorm prologue: the x operand is first replaced by
+ *    bf16(LN(x) * ln_w + ln_b) (fp32 ln_w / ln_b of length K, eps ln_eps),
+ *    then gamma * . + beta per row when gamma != NULL (bf16 (M, K), row
+ *    stride ld_gb): exactly mtts_layernorm_fwd's output (mamba_decoder.py:
+ *    59,67,81,184 and the FiLM of :82-86) consumed in place.  K <= 2048.
+ *  - res != NULL, residual epilogue: y = bf16(bf16(product) + res) (bf16
+ *    (M, N), row stride ld_res): the residual-stream value that
+ *    mtts_layernorm_fwd writes to x_sum.
+ *  - conv_dim > 0 (a multiple of 32; not with res): columns c < conv_dim
+ *    also go through Mamba.step's causal_conv1d_update (width 4) + SiLU on
+ *    the bf16 value of y[:, c]: conv_state (M, conv_dim, 4) fp32 shifted in
+ *    place, u[:, c] (bf16, row stride ldu) = silu(conv_state . conv_w[c] +
+ *    conv_b[c]).
  * ------------------------------------------------------------------------ */
-int mtts_gemm_rows_bf16(const void* x, int64_t ldx, int M, const void* W, int64_t ldw, int N, int K,
-                        const void* bias, int act, void* y, int64_t ldy, void* stream);
+typedef struct {
+  int M, N, K, act;
+  int64_t ldx, ldw, ldy;
+  const void* x;
+  const void* W;
+  const void* bias;          /* optional */
+  void* y;
+  int conv_dim;              /* 0 = no conv epilogue */
+  float* conv_state;
+  const float* conv_w;
+  const float* conv_b;       /* optional */
+  void* u;
+  int64_t ldu;
+  const float* ln_w;         /* NULL = no LayerNorm prologue */
+  const float* ln_b;
+  float ln_eps;
+  const void* gamma;         /* optional FiLM */
+  const void* beta;
+  int64_t ld_gb;
+  const void* res;           /* NULL = no residual epilogue */
+  int64_t ld_res;
+} MttsRowsArgs;
+
+int mtts_gemm_rows(const MttsRowsArgs* a, void* stream);
 
 #ifdef __cplusplus
 }

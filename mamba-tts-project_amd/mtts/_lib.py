@@ -68,6 +68,14 @@ class StateUpdateArgs(C.Structure):
                 ("dt_bias", vp), ("out", vp), ("dt_rank", i32), ("dt_w", vp)]
 
 
+class RowsArgs(C.Structure):
+    _fields_ = [("M", i32), ("N", i32), ("K", i32), ("act", i32), ("ldx", i64), ("ldw", i64), ("ldy", i64),
+                ("x", vp), ("W", vp), ("bias", vp), ("y", vp),
+                ("conv_dim", i32), ("conv_state", vp), ("conv_w", vp), ("conv_b", vp), ("u", vp), ("ldu", i64),
+                ("ln_w", vp), ("ln_b", vp), ("ln_eps", f32), ("gamma", vp), ("beta", vp), ("ld_gb", i64),
+                ("res", vp), ("ld_res", i64)]
+
+
 class LNArgs(C.Structure):
     _fields_ = [("rows", i32), ("cols", i32), ("dtype", i32), ("rows_per_group", i32), ("eps", f32),
                 ("x_rs", i64), ("res_rs", i64), ("xsum_rs", i64), ("y_rs", i64), ("gb_rs", i64),
@@ -116,6 +124,7 @@ _SIGS = {
     "mtts_causal_conv1d_update": ([C.POINTER(ConvUpdateArgs), vp], i32),
     "mtts_selective_state_update": ([C.POINTER(StateUpdateArgs), vp], i32),
     "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
+    "mtts_gemm_rows": ([C.POINTER(RowsArgs), vp], i32),
     "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),
     "mtts_layernorm_bwd": ([C.POINTER(LNBwdArgs), vp], i32),
     "mtts_colsum_workspace": ([i32, i32, i32], i64),
@@ -128,7 +137,6 @@ _SIGS = {
     "mtts_clip_adam": ([vp, i32, i64, vp, f32, f32, f32, f32, f32, f32, vp, vp, vp], i32),
     "mtts_embed_sum": ([vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, i32, i64, vp, vp], i32),
     "mtts_cast_tiles": ([i32, i32], i64),
-    "mtts_gemm_rows_bf16": ([vp, i64, i32, vp, i64, i32, i32, vp, i32, vp, i64, vp], i32),
     "mtts_cast_bf16_multi": ([vp, i32, i64, vp], i32),
     "mtts_length_regulate_lengths": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_length_regulate_fwd": ([vp, i32, i32, i32, i32, i64, i64, vp, i64, i32, vp, i64, i64, vp], i32),

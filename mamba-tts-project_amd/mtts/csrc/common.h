@@ -128,4 +128,40 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// 16-byte row pieces as fp32 (LayerNorm rows, the decode LayerNorm tail)
+template <typename T, int VEC>
+__device__ __forceinline__ void ld_vec(const T* p, float (&o)[VEC]) {
+  if constexpr (VEC * sizeof(T) == 16) {
+    uint4 v = *reinterpret_cast<const uint4*>(p);
+    if constexpr (sizeof(T) == 4) {
+      o[0] = __uint_as_float(v.x); o[1] = __uint_as_float(v.y); o[2] = __uint_as_float(v.z); o[3] = __uint_as_float(v.w);
+    } else {
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { o[2 * q] = __uint_as_float(w[q] << 16); o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) o[q] = ldf(p + q);
+  }
+}
+template <typename T, int VEC>
+__device__ __forceinline__ void st_vec(T* p, const float (&v)[VEC]) {
+  if constexpr (VEC * sizeof(T) == 16) {
+    uint4 w;
+    if constexpr (sizeof(T) == 4) {
+      w = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+    } else {
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+      w = make_uint4(q[0], q[1], q[2], q[3]);
+    }
+    *reinterpret_cast<uint4*>(p) = w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) stf(p + q, v[q]);
+  }
+}
+
 }  // namespace mtts

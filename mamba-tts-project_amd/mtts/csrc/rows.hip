@@ -9,6 +9,11 @@
 // output column, 8 consecutive k = 16 contiguous bytes of a weight row; no
 // LDS), x fragments come from L2, and the KS partial 32x32 tiles are summed
 // through LDS in a fixed order with bias / GELU fused into the store.
+// Optional epilogue: the causal-conv1d state update + SiLU on the x half of
+// in_proj (Mamba.step), which removes the conv-update launch.  (A residual +
+// LayerNorm tail run by the last workgroup to finish was measured and
+// dropped: the agent-scope release/acquire it needs costs more than the
+// LayerNorm launch it saves, 15 us per use; DESIGN.md.)
 #include "common.h"
 
 namespace mtts {
@@ -20,49 +25,172 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-template <int KS>
-__global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx, int M,
-                                                            const bf16_t* __restrict__ W, int64_t ldw, int N, int K,
-                                                            const bf16_t* __restrict__ bias, int act,
-                                                            bf16_t* __restrict__ y, int64_t ldy) {
+template <int KS, int U, bool LNP>
+__global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a) {
   __shared__ float red[KS][32][33];
+  __shared__ float psum[LNP ? KS : 1][32], psq[LNP ? KS : 1][32];
+  __shared__ __attribute__((aligned(16))) float slw[LNP ? 2048 : 4], slb[LNP ? 2048 : 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.x * 32;
-  const int kc = K / KS, kb = wave * kc;
+  const int M = a.M, N = a.N;
+  const int kc = a.K / KS, kb = wave * kc;
   const bool rowok = i < M, colok = n0 + i < N;
-  const bf16_t* xr = x + (int64_t)(rowok ? i : 0) * ldx + kb + 8 * h;
-  const bf16_t* wr = W + (int64_t)(colok ? n0 + i : 0) * ldw + kb + 8 * h;
-  f32x16 acc = {};
-  for (int k = 0; k < kc; k += 64) {   // 4 k-steps per trip, all loads issued first
-    s16x8 a[4], b[4];
+  const bf16_t* xr = (const bf16_t*)a.x + (int64_t)(rowok ? i : 0) * a.ldx + kb + 8 * h;
+  const bf16_t* wr = (const bf16_t*)a.W + (int64_t)(colok ? n0 + i : 0) * a.ldw + kb + 8 * h;
+  // conv epilogue operands do not depend on the product: fetch them first
+  constexpr int E = 1024 / (64 * KS), EP = KS >= 4 ? E : 1;
+  const bool conv_tile = n0 < a.conv_dim;   // conv_dim % 32 == 0: whole tiles
+  float4 cst[EP], cwv[EP];
+  float cbv[EP];
+  if constexpr (KS >= 4) {
+    if (conv_tile) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a[u] = *reinterpret_cast<const s16x8*>(xr + k + 16 * u);
-      b[u] = *reinterpret_cast<const s16x8*>(wr + k + 16 * u);
+      for (int e = 0; e < E; ++e) {
+        const int idx = threadIdx.x + e * 64 * KS, row = idx >> 5, c = n0 + (idx & 31);
+        if (row < M) {
+          cst[e] = *reinterpret_cast<const float4*>(a.conv_state + ((int64_t)row * a.conv_dim + c) * 4);
+          cwv[e] = *reinterpret_cast<const float4*>(a.conv_w + (int64_t)c * 4);
+          cbv[e] = a.conv_b ? a.conv_b[c] : 0.f;
+        }
+      }
+    }
+  }
+  // bias / residual of the epilogue elements, fetched before the product too
+  float bv[E], rv[E];
+  const bf16_t* bias = (const bf16_t*)a.bias;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int idx = threadIdx.x + e * 64 * KS, row = idx >> 5, c = n0 + (idx & 31);
+    const bool ok = row < M && c < N;
+    bv[e] = bias && ok ? bf2f(bias[c]) : 0.f;
+    rv[e] = a.res && ok ? bf2f(((const bf16_t*)a.res)[(int64_t)row * a.ld_res + c]) : 0.f;
+  }
+  f32x16 acc = {};
+  s16x8 xa[U], wb[U];
+  auto load_w = [&](int k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) wb[u] = *reinterpret_cast<const s16x8*>(wr + k + 16 * u);
+  };
+  auto load_x = [&](int k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) xa[u] = *reinterpret_cast<const s16x8*>(xr + k + 16 * u);
+  };
+  if constexpr (LNP) {
+    // LayerNorm prologue, one trip (host: K == KS * 16 * U): the wave's x
+    // fragments hold all of its k slice, so the row statistics come from
+    // registers (per-wave partials, fixed-order sums through LDS) while the
+    // weights, FiLM rows and LN parameters (-> LDS) are in flight.
+    for (int c = threadIdx.x * 4; c < a.K; c += 64 * KS * 4) {
+      *reinterpret_cast<float4*>(slw + c) = *reinterpret_cast<const float4*>(a.ln_w + c);
+      *reinterpret_cast<float4*>(slb + c) = *reinterpret_cast<const float4*>(a.ln_b + c);
+    }
+    load_w(0);
+    load_x(0);
+    s16x8 ga[U], ba[U];
+    if (a.gamma) {
+      const int64_t ro = (int64_t)(rowok ? i : 0) * a.ld_gb + kb + 8 * h;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ga[u] = *reinterpret_cast<const s16x8*>((const bf16_t*)a.gamma + ro + 16 * u);
+        ba[u] = *reinterpret_cast<const s16x8*>((const bf16_t*)a.beta + ro + 16 * u);
+      }
+    }
+    float sx = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sx += bf2f((bf16_t)xa[u][q]);
+    sx += __shfl_xor(sx, 32);
+    if (lane < 32) psum[wave][i] = sx;
+    __syncthreads();
+    float mean = 0.f;
+#pragma unroll
+    for (int w = 0; w < KS; ++w) mean += psum[w][i];
+    mean /= a.K;
+    float sq = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { const float d = bf2f((bf16_t)xa[u][q]) - mean; sq = fmaf(d, d, sq); }
+    sq += __shfl_xor(sq, 32);
+    if (lane < 32) psq[wave][i] = sq;
+    __syncthreads();
+    float var = 0.f;
+#pragma unroll
+    for (int w = 0; w < KS; ++w) var += psq[w][i];
+    const float rstd = 1.f / sqrtf(var / a.K + a.ln_eps);
+    // operand = bf16(LN(x) * w + b [, gamma * . + beta]) as mtts_layernorm_fwd rounds it
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c0 = kb + 16 * u + 8 * h;
+      const float4 w0 = *reinterpret_cast<const float4*>(slw + c0), w1 = *reinterpret_cast<const float4*>(slw + c0 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(slb + c0), b1 = *reinterpret_cast<const float4*>(slb + c0 + 4);
+      const float lw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const float lb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float v = fmaf((bf2f((bf16_t)xa[u][q]) - mean) * rstd, lw[q], lb[q]);
+        if (a.gamma) v = fmaf(bf2f((bf16_t)ga[u][q]), v, bf2f((bf16_t)ba[u][q]));
+        xa[u][q] = (short)f2bf(v);
+      }
+    }
+  }
+  for (int k = 0; k < kc; k += 16 * U) {   // U k-steps per trip, all loads issued first
+    if constexpr (!LNP) {
+      load_w(k);
+      load_x(k);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (!rowok) a[u] = s16x8{};
-      if (!colok) b[u] = s16x8{};
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[u]), __builtin_bit_cast(bf16x8, b[u]),
-                                                    acc, 0, 0, 0);
+    for (int u = 0; u < U; ++u) {
+      if (!rowok) xa[u] = s16x8{};
+      if (!colok) wb[u] = s16x8{};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, xa[u]),
+                                                    __builtin_bit_cast(bf16x8, wb[u]), acc, 0, 0, 0);
     }
   }
   // acc register r: output row (batch) acc_row(r, h), column n0 + i
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[wave][acc_row(r, h)][i] = acc[r];
   __syncthreads();
-  for (int e = threadIdx.x; e < 32 * 32; e += 64 * KS) {
-    const int row = e >> 5, col = e & 31;
-    if (row >= M || n0 + col >= N) continue;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int idx = threadIdx.x + e * 64 * KS, row = idx >> 5, col = idx & 31, c = n0 + col;
+    if (row >= M || c >= N) continue;
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < KS; ++w) s += red[w][row][col];
-    if (bias) s += bf2f(bias[n0 + col]);
-    if (act == 1) s = 0.5f * s * (1.f + erff(s * 0.70710678118654752f));   // F.gelu (exact erf)
-    y[(int64_t)row * ldy + n0 + col] = f2bf(s);
+    s += bv[e];
+    if (a.act == 1) s = 0.5f * s * (1.f + erff(s * 0.70710678118654752f));   // F.gelu (exact erf)
+    const bf16_t sb = f2bf(s);
+    // residual epilogue: y = bf16(bf16(product) + res), the stream value mtts_layernorm_fwd writes to x_sum
+    ((bf16_t*)a.y)[(int64_t)row * a.ldy + c] = a.res ? f2bf(bf2f(sb) + rv[e]) : sb;
+    if (conv_tile) {   // causal_conv1d_update (width 4) + SiLU on the bf16-rounded column
+      float4* stp = reinterpret_cast<float4*>(a.conv_state + ((int64_t)row * a.conv_dim + c) * 4);
+      float4 st, w;
+      float cb;
+      if constexpr (KS >= 4) {
+        st = cst[e], w = cwv[e], cb = cbv[e];
+      } else {
+        st = *stp, w = *reinterpret_cast<const float4*>(a.conv_w + (int64_t)c * 4), cb = a.conv_b ? a.conv_b[c] : 0.f;
+      }
+      st = make_float4(st.y, st.z, st.w, bf2f(sb));
+      *stp = st;
+      const float v = fmaf(w.x, st.x, fmaf(w.y, st.y, fmaf(w.z, st.z, fmaf(w.w, st.w, cb))));
+      ((bf16_t*)a.u)[(int64_t)row * a.ldu + c] = f2bf(silu_f(v));
+    }
   }
+}
+
+template <int KS, int U>
+void launch_rows(const MttsRowsArgs* a, int tiles, hipStream_t st) {
+  if constexpr (KS <= 8) {
+    if (a->ln_w) {
+      hipLaunchKernelGGL((gemm_rows_kernel<KS, U, true>), dim3(tiles), dim3(64 * KS), 0, st, *a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm_rows_kernel<KS, U, false>), dim3(tiles), dim3(64 * KS), 0, st, *a);
 }
 
 }  // namespace
@@ -70,39 +198,69 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const bf16_t* __rest
 
 using namespace mtts;
 
-extern "C" int mtts_gemm_rows_bf16(const void* x, int64_t ldx, int M, const void* W, int64_t ldw, int N, int K,
-                                   const void* bias, int act, void* y, int64_t ldy, void* stream) {
-  MTTS_CHECK(x && W && y, "gemm_rows: null pointer");
+extern "C" int mtts_gemm_rows(const MttsRowsArgs* a, void* stream) {
+  MTTS_CHECK(a && a->x && a->W && a->y, "gemm_rows: null pointer");
+  const int M = a->M, N = a->N, K = a->K;
   MTTS_CHECK(M >= 0 && M <= 32 && N > 0 && K > 0, "gemm_rows: M=%d must be in [0, 32], N, K > 0", M);
   MTTS_CHECK(K % 64 == 0, "gemm_rows: K=%d must be a multiple of 64", K);
-  MTTS_CHECK(act == 0 || act == 1, "gemm_rows: act must be 0 (none) or 1 (gelu)");
-  MTTS_CHECK(((uintptr_t)x | (uintptr_t)W) % 16 == 0 && ldx % 8 == 0 && ldw % 8 == 0,
+  MTTS_CHECK(a->act == 0 || a->act == 1, "gemm_rows: act must be 0 (none) or 1 (gelu)");
+  MTTS_CHECK(((uintptr_t)a->x | (uintptr_t)a->W) % 16 == 0 && a->ldx % 8 == 0 && a->ldw % 8 == 0,
              "gemm_rows: x / W must be 16-byte aligned with 16-byte row strides");
+  MTTS_CHECK(a->conv_dim >= 0 && a->conv_dim <= N && a->conv_dim % 32 == 0,
+             "gemm_rows: conv_dim=%d must be a multiple of 32 in [0, N]", a->conv_dim);
+  MTTS_CHECK(a->conv_dim == 0 || (a->conv_state && a->conv_w && a->u && (uintptr_t)a->conv_state % 16 == 0 &&
+                                  (uintptr_t)a->conv_w % 16 == 0),
+             "gemm_rows: conv epilogue needs 16-byte aligned conv_state / conv_w and u");
+  if (a->ln_w) {
+    MTTS_CHECK(a->ln_b && (!a->gamma || a->beta), "gemm_rows: LayerNorm prologue needs ln_b, and beta with gamma");
+    MTTS_CHECK((uintptr_t)a->ln_w % 16 == 0 && (uintptr_t)a->ln_b % 16 == 0 &&
+                   (!a->gamma || ((uintptr_t)a->gamma % 16 == 0 && (uintptr_t)a->beta % 16 == 0 && a->ld_gb % 8 == 0)),
+               "gemm_rows: LayerNorm prologue operands must be 16-byte aligned");
+  }
+  MTTS_CHECK(!a->res || a->conv_dim == 0, "gemm_rows: residual and conv epilogues are exclusive");
   if (M == 0) return MTTS_OK;
   hipStream_t st = (hipStream_t)stream;
   const int tiles = (N + 31) / 32;
-  // K split: enough waves to stream the weights (>= ~512 in flight), 64-multiple k slice each
-  int ks = 1;
-  if (K % (64 * 4) == 0) ks = 4;
-  if (tiles < 128 && K % (64 * 8) == 0) ks = 8;
-  if (tiles < 32 && K % (64 * 16) == 0) ks = 16;
-  switch (ks) {
-    case 16:
-      hipLaunchKernelGGL((gemm_rows_kernel<16>), dim3(tiles), dim3(64 * 16), 0, st, (const bf16_t*)x, ldx, M,
-                         (const bf16_t*)W, ldw, N, K, (const bf16_t*)bias, act, (bf16_t*)y, ldy);
-      break;
-    case 8:
-      hipLaunchKernelGGL((gemm_rows_kernel<8>), dim3(tiles), dim3(64 * 8), 0, st, (const bf16_t*)x, ldx, M,
-                         (const bf16_t*)W, ldw, N, K, (const bf16_t*)bias, act, (bf16_t*)y, ldy);
-      break;
-    case 4:
-      hipLaunchKernelGGL((gemm_rows_kernel<4>), dim3(tiles), dim3(64 * 4), 0, st, (const bf16_t*)x, ldx, M,
-                         (const bf16_t*)W, ldw, N, K, (const bf16_t*)bias, act, (bf16_t*)y, ldy);
-      break;
-    default:
-      hipLaunchKernelGGL((gemm_rows_kernel<1>), dim3(tiles), dim3(64), 0, st, (const bf16_t*)x, ldx, M,
-                         (const bf16_t*)W, ldw, N, K, (const bf16_t*)bias, act, (bf16_t*)y, ldy);
-      break;
+  // K split over ks = 8 waves of one workgroup (fewer where K is short),
+  // each streaming its k slice in trips of 4 MFMA k-steps with all loads of
+  // a trip in flight.  Measured on the C4 step (tools/decode_ab.py, p50 ms):
+  // ks = 8 everywhere 1.20; 4 / 8 / 16 by tile count 1.23; ks = 4 1.25;
+  // ks = 2 1.44; one 8-step trip per wave with up to 16 waves 1.28.
+  int U = 4;
+  int ks = K % (64 * 8) == 0 ? 8 : K % (64 * 4) == 0 ? 4 : K % (64 * 2) == 0 ? 2 : 1;
+  if (const char* e = getenv("MTTS_ROWS_KS")) {   // tuning override
+    const int f = atoi(e);
+    if ((f == 1 || f == 2 || f == 4 || f == 8 || f == 16) && K % (64 * f) == 0) ks = f;
+  }
+  int u8 = U == 8;
+  if (a->ln_w) {   // LayerNorm prologue: exactly one trip per wave (K == ks * 16 * U), ks <= 8
+    int f = 0;
+    for (int c = 8; c >= 1 && !f; c >>= 1) {
+      if (K == c * 128) f = c, u8 = 1;
+      else if (K == c * 64) f = c, u8 = 0;
+    }
+    if (!f) {
+      set_error("gemm_rows: LayerNorm prologue needs K = 64 * {1,2,4,8} or 128 * {1,..,8} (K=%d)", K);
+      return MTTS_EUNSUPPORTED;
+    }
+    ks = f;
+  }
+  if (u8) {
+    switch (ks) {
+      case 16: launch_rows<16, 8>(a, tiles, st); break;
+      case 8: launch_rows<8, 8>(a, tiles, st); break;
+      case 4: launch_rows<4, 8>(a, tiles, st); break;
+      case 2: launch_rows<2, 8>(a, tiles, st); break;
+      default: launch_rows<1, 8>(a, tiles, st); break;
+    }
+  } else {
+    switch (ks) {
+      case 16: launch_rows<16, 4>(a, tiles, st); break;
+      case 8: launch_rows<8, 4>(a, tiles, st); break;
+      case 4: launch_rows<4, 4>(a, tiles, st); break;
+      case 2: launch_rows<2, 4>(a, tiles, st); break;
+      default: launch_rows<1, 4>(a, tiles, st); break;
+    }
   }
   MTTS_LAUNCH_CHECK("gemm_rows");
   return MTTS_OK;

@@ -99,6 +99,61 @@ class DecodeEngine:
         return dict(B=B, kpm=kpm, layers=layers, cd=cd,
                     Wh=cast_weight(m.head.weight, cd), bh=cast_weight(m.head.bias, cd))
 
+    def _fused_ok(self, cd, B):
+        """The fused-epilogue step (_step_rows) applies: bf16, <= 32 rows and
+        the shapes csrc/rows.hip takes (checked once per context)."""
+        m = self.m
+        if (not self.use_rows or cd != torch.bfloat16 or B > ops.GEMM_ROWS_MAX
+                or os.environ.get("MTTS_DECODE_FUSED", "1") == "0"):
+            return False
+        d = m.token_embed.weight.shape[1]
+        if not ops.gemm_rows_ln_ok(d):
+            return False
+        for l in m.layers:
+            mm = l.mamba
+            if (mm.d_conv != 4 or d % 64 or mm.d_inner % 64 or d % 8 or d > 2048 or l.ff[0].weight.shape[0] % 64
+                    or any(n.weight.dtype != torch.float32 for n in (l.norm_mamba, l.norm_cross, l.norm_ff))):
+                return False
+        return m.norm_out.weight.dtype == torch.float32
+
+    # -- one step, fused epilogues (bf16, <= 32 sequences) ---------------------
+    def _step_rows(self, tok, pos, states):
+        """Per layer, 9 launches and no LayerNorm kernel (csrc/rows.hip):
+        in_proj (LN prologue, conv-update + SiLU epilogue) -> x_proj ->
+        state update (+dt_proj) -> out_proj (+residual) -> q (LN prologue)
+        -> attention -> out_proj (+residual) -> FFN up (LN + FiLM prologue,
+        GELU) -> FFN down (+residual); the head LayerNorms in its prologue.
+        x is the bf16 residual stream, exactly as the LayerNorm kernels'
+        x_sum of the generic step."""
+        m, c = self.m, self.ctx
+        cd = c["cd"]
+        x = (F.embedding(tok, m.token_embed.weight) + F.embedding(pos, m.pos_embed.weight)[None]).to(cd)
+        x = x.view(c["B"], -1)
+
+        def ln(norm, gamma=None, beta=None):
+            return (norm.weight, norm.bias, norm.eps, gamma, beta)
+
+        fuse_conv = os.environ.get("MTTS_DECODE_FUSE_CONV", "1") != "0"
+        for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
+            conv_state, ssm_state = states[i]
+            mm = l.mamba
+            di, N, r = mm.d_inner, mm.d_state, mm.dt_rank
+            if fuse_conv:
+                xz, u = ops.gemm_rows(x, p["Win"], conv=(conv_state, p["conv_w"], p["conv_b"]), ln=ln(l.norm_mamba))
+            else:
+                xz = ops.gemm_rows(x, p["Win"], ln=ln(l.norm_mamba))
+                u = ops.conv_update(xz[:, :di], conv_state, p["conv_w"], p["conv_b"], True)
+            x_dbl = ops.gemm_rows(u, p["Wx"])
+            y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
+                                 xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"])
+            x = ops.gemm_rows(y, p["Wout"], res=x)
+            q = ops.gemm_rows(x, p["Wq"], p["bq"], ln=ln(l.norm_cross))
+            o = attention(q[:, None], p["k"], p["v"], l.cross_attn.num_heads, c["kpm"])[:, 0]
+            x = ops.gemm_rows(o, p["Wo"], p["bo"], res=x)
+            f = ops.gemm_rows(x, p["W1"], p["b1"], "gelu", ln=ln(l.norm_ff, p["gamma"], p["beta"]))
+            x = ops.gemm_rows(f, p["W2"], p["b2"], res=x)
+        return ops.gemm_rows(x, c["Wh"], c["bh"], ln=ln(m.norm_out))[:, None]
+
     # -- one step, eager -----------------------------------------------------
     def _step(self, tok, pos, states):
         m, c = self.m, self.ctx
@@ -166,8 +221,9 @@ class DecodeEngine:
                 st[1].copy_(given[1])
         self.tok_buf.copy_(last_token)
         self.pos_buf.fill_(int(step_index))
+        step = self._step_rows if self._fused_ok(cd, B) else self._step
         if not self.use_graph:
-            logits = self._step(self.tok_buf, self.pos_buf, self.states)
+            logits = step(self.tok_buf, self.pos_buf, self.states)
             return logits, list(self.states)
         if self.graph is None:
             saved = [(a.clone(), b.clone()) for a, b in self.states]
@@ -175,14 +231,14 @@ class DecodeEngine:
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 for _ in range(2):  # warm up (allocator, library handles)
-                    self._step(self.tok_buf, self.pos_buf, self.states)
+                    step(self.tok_buf, self.pos_buf, self.states)
             torch.cuda.current_stream().wait_stream(s)
             for (a, b), (sa, sb) in zip(self.states, saved):
                 a.copy_(sa)
                 b.copy_(sb)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.out_buf = self._step(self.tok_buf, self.pos_buf, self.states)
+                self.out_buf = step(self.tok_buf, self.pos_buf, self.states)
             for (a, b), (sa, sb) in zip(self.states, saved):  # capture ran the step once
                 a.copy_(sa)
                 b.copy_(sb)

@@ -502,9 +502,22 @@ def gemm_rows_ok(x, weight):
             and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
 
 
-def gemm_rows(x, weight, bias=None, act=None):
+def gemm_rows_ln_ok(K):
+    """K values the one-trip LayerNorm prologue of csrc/rows.hip takes."""
+    return K in {64 * c for c in (1, 2, 4, 8)} | {128 * c for c in (1, 2, 4, 8)}
+
+
+def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
     """y = act(x @ weight.t() + bias) for the decode step's skinny GEMMs
-    (x: M <= 32 rows, bf16; act None or "gelu" = exact-erf F.gelu)."""
+    (x: M <= 32 rows, bf16; act None or "gelu" = exact-erf F.gelu).
+
+    conv = (conv_state (M, C, 4) fp32, conv_w (C, 4) fp32, conv_b or None):
+        columns [0, C) also pass through causal_conv1d_update + SiLU;
+        returns (y, u) with u (M, C) bf16.
+    ln = (w, b, eps[, gamma, beta]): the x operand is LayerNorm'd (+FiLM) on
+        the fly, exactly as ops.layer_norm would produce it.
+    res: (M, N) bf16; y = bf16(y + res) (the residual stream after the add).
+    """
     _check_cuda(x, weight, bias)
     if not gemm_rows_ok(x, weight):
         raise ValueError(f"gemm_rows: unsupported operands x{tuple(x.shape)}/{x.stride()} "
@@ -517,7 +530,35 @@ def gemm_rows(x, weight, bias=None, act=None):
         bias = bias.to(torch.bfloat16).contiguous()
         if bias.numel() != N:
             raise ValueError("gemm_rows: bias size")
-    y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
-    L.call_raw("mtts_gemm_rows_bf16", x.data_ptr(), x.stride(0), M, weight.data_ptr(), weight.stride(0), N, K,
-               L.ptr(bias), {None: 0, "gelu": 1}[act], y.data_ptr(), y.stride(0))
-    return y
+    dev = x.device
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    a = L.RowsArgs()
+    a.M, a.N, a.K, a.act = M, N, K, {None: 0, "gelu": 1}[act]
+    a.ldx, a.ldw, a.ldy = x.stride(0), weight.stride(0), y.stride(0)
+    a.x, a.W, a.bias, a.y = x.data_ptr(), weight.data_ptr(), L.ptr(bias), y.data_ptr()
+    out = [y]
+    if conv is not None:
+        cs, cw, cb = conv
+        C = cw.shape[0]
+        if cs.dtype != torch.float32 or cs.shape != (M, C, 4) or not cs.is_contiguous() or cw.shape != (C, 4):
+            raise ValueError("gemm_rows: conv state must be (M, C, 4) fp32 contiguous, weight (C, 4)")
+        u = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+        a.conv_dim, a.conv_state, a.conv_w, a.conv_b = C, cs.data_ptr(), cw.data_ptr(), L.ptr(cb)
+        a.u, a.ldu = u.data_ptr(), u.stride(0)
+        out.append(u)
+    if ln is not None:
+        lw, lb, eps = ln[0], ln[1], ln[2]
+        if lw.dtype != torch.float32 or lb.dtype != torch.float32 or lw.numel() != K or not lw.is_contiguous():
+            raise ValueError("gemm_rows: LayerNorm weight / bias must be contiguous fp32 of length K")
+        a.ln_w, a.ln_b, a.ln_eps = lw.data_ptr(), lb.data_ptr(), float(eps)
+        if len(ln) > 3 and ln[3] is not None:
+            g, be = ln[3], ln[4]
+            if g.dtype != torch.bfloat16 or g.stride() != be.stride() or g.shape != (M, K):
+                raise ValueError("gemm_rows: FiLM gamma / beta must be (M, K) bf16 with equal strides")
+            a.gamma, a.beta, a.ld_gb = g.data_ptr(), be.data_ptr(), g.stride(0)
+    if res is not None:
+        if res.dtype != torch.bfloat16 or res.shape != (M, N) or res.stride(1) != 1:
+            raise ValueError("gemm_rows: res must be (M, N) bf16 with unit column stride")
+        a.res, a.ld_res = res.data_ptr(), res.stride(0)
+    L.call("mtts_gemm_rows", a)
+    return out[0] if len(out) == 1 else tuple(out)

@@ -380,3 +380,63 @@ def test_state_update_fused_dt_proj(dtype, R):
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     close(s1, s2, rtol=tol, name="state")
     close(y1.float(), y2.float(), rtol=tol, name="y")
+
+
+@pytest.mark.parametrize("M,C,N", [(32, 2048, 4096), (3, 128, 256)])
+def test_gemm_rows_conv_epilogue(M, C, N):
+    """in_proj with the causal-conv1d update + SiLU folded into its epilogue
+    equals in_proj followed by mtts_causal_conv1d_update (state and u)."""
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(C)
+    K = 128
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    cw, cb = torch.randn(C, 4, generator=g).to(DEV), torch.randn(C, generator=g).to(DEV)
+    st = torch.randn(M, C, 4, generator=g).to(DEV)
+    st2 = st.clone()
+    for _ in range(2):
+        y, u = ops.gemm_rows(x, w, conv=(st, cw, cb))
+        y2 = ops.gemm_rows(x, w)
+        u2 = ops.conv_update(y2[:, :C], st2, cw, cb, True)
+        assert torch.equal(y, y2)
+        close(st, st2, rtol=1e-6, name="conv state")
+        close(u.float(), u2.float(), rtol=2 ** -8, name="u")
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 4096, 1024), (32, 1024, 256), (5, 512, 512), (7, 96, 128), (3, 64, 64)])
+@pytest.mark.parametrize("film", [False, True])
+def test_gemm_rows_ln_prologue_and_residual(M, N, K, film):
+    """LayerNorm (+FiLM) prologue of the decode projections (statistics from
+    the operand registers) against mtts_layernorm_fwd followed by the plain
+    GEMM: the same arithmetic up to fp32 summation order of mean / variance,
+    so within one bf16 rounding of the normalised operand; the residual
+    epilogue equals the LayerNorm kernel's x_sum bit for bit."""
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(M * N + K)
+    x = (torch.randn(M, K, generator=g) * 3 + 0.5).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    lw, lb = torch.randn(K, generator=g).to(DEV), torch.randn(K, generator=g).to(DEV)
+    gam = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if film else None
+    bet = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if film else None
+    y = ops.gemm_rows(x, w, b, ln=(lw, lb, 1e-5, gam, bet))
+    h, _ = ops.layer_norm(x, lw, lb, 1e-5, gamma=gam, beta=bet, rows_per_group=1)
+    y2 = ops.gemm_rows(h, w, b)
+    close(y.float(), y2.float(), rtol=2 ** -7, name="ln prologue")
+    assert (y != y2).float().mean().item() < 0.02      # bf16-level disagreements are rare
+    res = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    xs = ops.gemm_rows(x, w, b, res=res)
+    if N % 512 == 0:
+        _, xs2 = ops.layer_norm(ops.gemm_rows(x, w, b), torch.ones(N, device=DEV), torch.zeros(N, device=DEV),
+                                1e-5, res=res)
+        assert torch.equal(xs, xs2)
+    close(xs.float(), ops.gemm_rows(x, w, b).float() + res.float(), rtol=2 ** -7, name="residual")
+
+
+def test_gemm_rows_ln_prologue_rejects_multi_trip_k():
+    from mtts import ops
+    x = torch.zeros(4, 2048, device=DEV, dtype=torch.bfloat16)
+    w = torch.zeros(64, 2048, device=DEV, dtype=torch.bfloat16)
+    lw = torch.ones(2048, device=DEV)
+    with pytest.raises(RuntimeError, match="LayerNorm prologue"):
+        ops.gemm_rows(x, w, ln=(lw, lw, 1e-5))

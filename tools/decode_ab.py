@@ -48,7 +48,7 @@ def shapes():
         print(f"N={N:5d} K={K:5d}  rows {tr:6.2f} us ({gbs:6.0f} GB/s)   hipBLASLt {tb:6.2f} us", flush=True)
 
 
-def step():
+def step(modes=(True, False)):
     import mamba_decoder
     from mtts.decode import DecodeEngine
     c = dict(bench.C2)
@@ -61,7 +61,7 @@ def step():
     _, text, z, mask = bench.make_batch(c, dev, 7)
     res = {}
     n = int(os.environ.get("DEC_STEPS", 300))
-    for rows in ((True, False) if n < 300 else (True, False, True, False)):
+    for rows in (modes if n < 300 else modes + modes):
         m._engine = DecodeEngine(m, use_graph=True, use_rows=rows)
         tok = torch.zeros(32, 1, dtype=torch.long, device=dev)
         states = [None] * c["n_layers"]
@@ -84,3 +84,20 @@ if __name__ == "__main__":
         shapes()
     if "step" in what:
         step()
+    if "tune" in what:
+        for k, v in [("MTTS_DECODE_FUSE_CONV", "0"), ("MTTS_DECODE_FUSE_CONV", "1"), ("MTTS_ROWS_KS", "4"),
+                     ("MTTS_ROWS_KS", "8"), ("MTTS_ROWS_KS", "16")]:
+            os.environ[k] = v
+            print(k, v, end=" ", flush=True)
+            step((True,))
+            os.environ.pop(k)
+    if "rowsonly" in what:
+        step((True,))
+    if "modes" in what:
+        for env in ({}, {"MTTS_ROWS_KS": "2"}, {"MTTS_ROWS_KS": "4"}, {"MTTS_ROWS_KS": "8"},
+                    {"MTTS_DECODE_FUSED": "0"}, {}):
+            os.environ.update(env)
+            print(env, end=" ", flush=True)
+            step((True, False))
+            for k in env:
+                os.environ.pop(k)
