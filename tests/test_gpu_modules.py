@@ -201,3 +201,39 @@ def test_decode_engine_matches_module_path(golden, mode):
     close(outs[mode][0], g["decode/logits"], name="engine vs reference")
     for i in range(2):
         close(outs[mode][1][i][1], g[f"decode/ssm_state{i}"], name="ssm state")
+
+
+@pytest.mark.parametrize("B", [32, 5, 33])
+def test_bf16_decode_engine_c4_shapes(B):
+    """C4-shaped layers (d_model=1024, d_ff=2048, 8 heads; 2 layers): the
+    fused engine step (LayerNorm prologues, residual / conv epilogues,
+    single-query attention; B <= 32) and its fallback (B = 33: hipBLASLt
+    projections) against the generic module path, bf16, several steps.
+    Bound: 3e-2 of the logit scale (bf16 roundings of the activations)."""
+    import mamba_decoder
+    from mtts.decode import DecodeEngine
+    torch.manual_seed(1)
+    m = mamba_decoder.MambaTTSDecoder(10, d_model=1024, n_layers=2, n_heads=8, d_ff=2048, d_style=256).to(DEV).eval()
+    m.compute_dtype = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(2)
+    text = torch.randn(B, 40, 1024, device=DEV, generator=g)
+    z = torch.randn(B, 256, device=DEV, generator=g)
+    mask = torch.ones(B, 40, dtype=torch.bool, device=DEV)
+    mask[:, 30:] = False
+    tok = torch.randint(0, 10, (B, 1), device=DEV, generator=g)
+    outs = []
+    for mode in ("engine", "module"):
+        m.decode_mode = None
+        eng = DecodeEngine(m, use_graph=True) if mode == "engine" else None
+        states = [None, None]
+        seq = []
+        with torch.no_grad():
+            for t in range(6):
+                if eng is not None:
+                    lg, states = eng.step(tok, text, z, states, t, text_mask=mask)
+                else:
+                    lg, states = m.decode_step(tok, text, z, states, t, text_mask=mask)
+                seq.append(lg.float().clone())
+        outs.append(torch.cat(seq, 1))
+    assert (B <= 32) == DecodeEngine(m)._fused_ok(torch.bfloat16, B)
+    close(outs[0], outs[1], rtol=3e-2, name=f"engine vs module path, B={B}")
