@@ -198,6 +198,7 @@ class DecodeEngine:
         if key != self.ctx_key:
             self.ctx = self._build_ctx(text_hidden, z_style, text_mask, ref_hidden, ref_mask, cd)
             self.ctx_key = key
+            self.fused = self._fused_ok(cd, last_token.shape[0])
             self.graph = None
             self.states = None
         B = last_token.shape[0]
@@ -221,7 +222,7 @@ class DecodeEngine:
                 st[1].copy_(given[1])
         self.tok_buf.copy_(last_token)
         self.pos_buf.fill_(int(step_index))
-        step = self._step_rows if self._fused_ok(cd, B) else self._step
+        step = self._step_rows if self.fused else self._step
         if not self.use_graph:
             logits = step(self.tok_buf, self.pos_buf, self.states)
             return logits, list(self.states)

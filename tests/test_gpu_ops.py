@@ -440,3 +440,16 @@ def test_gemm_rows_ln_prologue_rejects_multi_trip_k():
     lw = torch.ones(2048, device=DEV)
     with pytest.raises(RuntimeError, match="LayerNorm prologue"):
         ops.gemm_rows(x, w, ln=(lw, lw, 1e-5))
+
+
+def test_wgrad_split_k_matches_fp64():
+    from mtts.linear import wgrad
+    g = torch.Generator(device="cpu").manual_seed(5)
+    dy = torch.randn(8192, 1024, generator=g).to(DEV, torch.bfloat16)
+    x = torch.randn(8192, 2048, generator=g).to(DEV, torch.bfloat16)
+    ref = dy.double().t() @ x.double()
+    close(wgrad(dy, x), ref, rtol=1e-5, name="wgrad")
+    big = torch.zeros(3072, 2048, device=DEV)
+    wgrad(dy, x, out=big[1024:2048])
+    close(big[1024:2048], ref, rtol=1e-5, name="wgrad row slice")
+    assert big[:1024].abs().max().item() == 0 and big[2048:].abs().max().item() == 0
