@@ -780,6 +780,17 @@ __device__ __forceinline__ void wait_vm(uint32_t (&w)[W]) {
   for (int q = 0; q < W; ++q) asm volatile("" : "+v"(w[q]));
 #endif
 }
+// s_waitcnt vmcnt(N) for any N < 64 (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,
+// expcnt 7, lgkmcnt 15), redefining the staged registers like wait_vm
+template <int N, int W>
+__device__ __forceinline__ void wait_vmn(uint32_t (&w)[W]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+#pragma unroll
+  for (int q = 0; q < W; ++q) asm volatile("" : "+v"(w[q]));
+#endif
+}
 __device__ __forceinline__ void wait_vmem() {
 #if defined(__HIP_DEVICE_COMPILE__)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -839,7 +850,11 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
   static_assert(TT * CPR == kBlock, "one chunk per thread per array");
   static_assert(DT::conflict_free(), "swizzle");
   // tile buffers: 3 (DMA two tiles ahead) when they fit 4 blocks per CU, else 2
+#ifdef MTTS_FWD_NB
+  constexpr int NB = MTTS_FWD_NB;  // timing builds: buffer count forced (LDS then sets blocks per CU)
+#else
   constexpr int NB = (3 * NA * IMG * ES + 2 * TT * 2 * kN * 4 + (XL ? 4096 : 0)) <= 40960 ? 3 : 2;
+#endif
   __shared__ __attribute__((aligned(16))) Tio sX[NB][NA][IMG];
   __shared__ __attribute__((aligned(16))) float sBC[2][TT * 2 * kN];
   // per-wave (delta, delta*u) exchange: the lane that formed step s of a
@@ -1857,10 +1872,247 @@ static bool wide_io_ok(const MttsScanFwdArgs* a) {
   return true;
 }
 
+// ------------------------------------------------------------- forward, one lane per channel (B*D >= 64k)
+// When B*D alone gives every SIMD a wave (north-star: 32 x 2048 channels =
+// 1024 waves), a lane owns ALL 16 states of one channel.  The P-lane
+// machinery of the kernels above (delta / delta*u exchange, the per-step
+// reduce-scatter of y and its lane selects, per-lane B/C slices) disappears:
+// B/C are wave-uniform (broadcast LDS reads) and the per-channel scalar work
+// (softplus, SiLU gate, D skip) runs once per channel-step in the lane that
+// uses it.  VALU per channel-step: 16 v_exp + 32 packed mul/fma + ~20 scalar.
+// One wave per SIMD (the block's LDS makes a block of 4 waves own its CU);
+// the waves are independent: each runs its own LDS-DMA ring of u/delta/z
+// tiles NB-1 tiles ahead and its own B/C staging, with no workgroup barrier.
+// Outputs replace u in the tile image and leave as 16-byte row chunks.
+// VMEM issue order per tile `it`: [stores of it-1] [B/C regs of it+1]
+// [DMA of it+NB-1]; waiting until only that DMA is in flight makes tile it+1
+// (B/C and the DMA issued NB-2 iterations earlier) complete.
+template <typename Tio, typename Tbc, bool SP, bool HZ>
+__global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdArgs a) {
+  constexpr int ES = (int)sizeof(Tio);
+  constexpr int EPC = 16 / ES;            // elements per 16-byte chunk
+  constexpr int CPR = 64 / EPC;           // chunks per 64-channel row
+  constexpr int RPD = 64 / CPR;           // rows per DMA instruction (1 KiB): 4 fp32, 8 bf16
+  constexpr int TT = 2 * RPD;             // steps per tile (2 DMA per array)
+  constexpr int NB = 4;                   // tile ring: DMA NB-1 tiles ahead
+  constexpr int NAR = HZ ? 3 : 2;
+  constexpr int IMG = TT * 64;
+  constexpr int BCV = TT * 2 * kN / 64;   // B/C values staged per lane per tile
+  constexpr int LPS = 2 * kN / BCV;       // lanes per B/C row
+  constexpr int BCB = BCV * (int)sizeof(Tbc);  // bytes per lane: 8, 16 or 32
+  constexpr int NBCI = BCB > 16 ? 2 : 1;  // B/C load instructions per tile
+  constexpr int NDMA = 2 * NAR;           // DMA instructions per tile
+  static_assert(kN % BCV == 0 && (BCB == 8 || BCB == 16 || BCB == 32), "B/C staging");
+  __shared__ __attribute__((aligned(16))) Tio sX[4][NB][NAR][IMG];
+  __shared__ __attribute__((aligned(16))) float sBC[4][2][TT * 2 * kN];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 4 + wave) * 64;
+  if (c0 >= a.dim) return;  // dim % 64 == 0 (host); no barrier anywhere below
+  const int c = c0 + lane;
+  const int b = blockIdx.y;
+  const int L = a.seqlen;
+  const int nt = (L + TT - 1) / TT;
+
+  const int drow = lane / CPR, dcol = (lane % CPR) * EPC;
+  const Tio* __restrict__ gu = (const Tio*)a.u + (int64_t)b * a.u_bs + c0 + dcol;
+  const Tio* __restrict__ gd = (const Tio*)a.delta + (int64_t)b * a.delta_bs + c0 + dcol;
+  const Tio* __restrict__ gz = HZ ? (const Tio*)a.z + (int64_t)b * a.z_bs + c0 + dcol : gu;
+  Tio* __restrict__ go = (Tio*)a.out + (int64_t)b * a.out_bs + c0 + dcol;
+  const int bs = lane / LPS, bcol = (lane % LPS) * BCV;
+  const Tbc* __restrict__ gbc = bcol < kN ? (const Tbc*)a.Bm + (int64_t)b * a.B_bs + bcol
+                                          : (const Tbc*)a.Cm + (int64_t)b * a.C_bs + (bcol - kN);
+  const int64_t bc_ls = bcol < kN ? a.B_ls : a.C_ls;
+
+  f2 A2[kN / 2], h[kN / 2];
+#pragma unroll
+  for (int p = 0; p < kN / 2; ++p) {
+    const float* ap = a.A + (int64_t)c * kN + 2 * p;
+    A2[p] = f2{ap[0] * kLog2e, ap[1] * kLog2e};
+    const int64_t o = ((int64_t)b * a.dim + c) * kN + 2 * p;
+    h[p] = a.h0 ? f2{a.h0[o], a.h0[o + 1]} : f2{0.f, 0.f};
+  }
+  const float Dc = a.D ? a.D[c] : 0.f;
+  const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
+  const int nck = a.ckpt ? (L + kSub - 1) / kSub : 0;
+  float* __restrict__ ck = nck ? a.ckpt + (int64_t)b * nck * a.dim * kN + (int64_t)c * kN : nullptr;
+
+  uint32_t stg[BCB / 4];
+  auto load_bc = [&](int it) __attribute__((always_inline)) {
+    const Tbc* p = gbc + (int64_t)min(it * TT + bs, L - 1) * bc_ls;
+    if constexpr (BCB == 8) {
+      uint32_t w[2];
+      ldg_asm<2>(w, p);
+      stg[0] = w[0]; stg[1] = w[1];
+    } else {
+#pragma unroll
+      for (int q = 0; q < NBCI; ++q) {
+        uint32_t w[4];
+        ldg_asm<4>(w, reinterpret_cast<const char*>(p) + 16 * q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) stg[4 * q + i] = w[i];
+      }
+    }
+  };
+  auto stage_bc = [&](int bb) __attribute__((always_inline)) {
+    float v[BCV];
+    if constexpr (sizeof(Tbc) == 4) {
+#pragma unroll
+      for (int q = 0; q < BCV; ++q) v[q] = __uint_as_float(stg[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < BCV / 2; ++q) unpack_bf2(stg[q], v[2 * q], v[2 * q + 1]);
+    }
+    float* d = &sBC[wave][bb][bs * 2 * kN + bcol];
+#pragma unroll
+    for (int q = 0; q < BCV / 4; ++q)
+      *reinterpret_cast<f4*>(d + 4 * q) = f4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+  };
+  auto dma_tile = [&](int it, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int t = min(it * TT + k * RPD + drow, L - 1);  // rows past L: any valid row (never stored)
+      dma16(gu + (int64_t)t * a.u_ls, &sX[wave][buf][0][k * RPD * 64]);
+      dma16(gd + (int64_t)t * a.delta_ls, &sX[wave][buf][1][k * RPD * 64]);
+      if constexpr (HZ) dma16(gz + (int64_t)t * a.z_ls, &sX[wave][buf][2][k * RPD * 64]);
+    }
+  };
+  auto store_tile = [&](int it, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int t = it * TT + k * RPD + drow;
+      const uint4 v = *reinterpret_cast<const uint4*>(&sX[wave][buf][0][(k * RPD + drow) * 64 + dcol]);
+      if (t < L) *reinterpret_cast<uint4*>(go + (int64_t)t * a.out_ls) = v;
+    }
+  };
+  auto compute_tile = [&](auto tail, int it, int buf, int bb) __attribute__((always_inline)) {
+    constexpr bool TAIL = decltype(tail)::value;
+    const int t0 = it * TT;
+    // (1) the tile's per-channel scalar work up front: TT independent chains
+    float dts[TT], dtus[TT], ugs[TT], gates[TT];
+#pragma unroll
+    for (int s = 0; s < TT; ++s) {
+      const int e = s * 64 + lane;
+      float dt = cvt_raw((raw_t<Tio>)sX[wave][buf][1][e]) + bias;
+      if constexpr (SP) dt = softplus_f(dt);
+      ugs[s] = cvt_raw((raw_t<Tio>)sX[wave][buf][0][e]);
+      const bool tv = !TAIL || t0 + s < L;
+      dts[s] = tv ? dt : 0.f;                  // padded steps: identity map
+      dtus[s] = tv ? dt * ugs[s] : 0.f;
+      gates[s] = HZ ? silu_f(cvt_raw((raw_t<Tio>)sX[wave][buf][2][e])) : 1.f;
+    }
+    // (2) the recurrence, B/C of step s+1 read (broadcast) while step s computes
+    f4 bcr[2][kN / 2];
+    auto read_bc = [&](int s, f4 (&o)[kN / 2]) __attribute__((always_inline)) {
+      const f4* p = reinterpret_cast<const f4*>(&sBC[wave][bb][s * 2 * kN]);
+#pragma unroll
+      for (int q = 0; q < kN / 2; ++q) o[q] = p[q];
+    };
+    // exp(delta*A) of step s+1 also forms during step s (independent of h):
+    // the transcendental stream of one step overlaps the FMA chain of the other
+    f2 ex[2][kN / 2];
+    auto exps = [&](int s, f2 (&o)[kN / 2]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int p = 0; p < kN / 2; ++p) {
+        const f2 x = f2{dts[s], dts[s]} * A2[p];
+        o[p] = f2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+      }
+    };
+    read_bc(0, bcr[0]);
+    exps(0, ex[0]);
+#pragma unroll
+    for (int s = 0; s < TT; ++s) {
+      if (nck && s % kSub == 0 && ((t0 + s) & (kSub - 1)) == 0 && (!TAIL || t0 + s < L)) {
+#pragma unroll
+        for (int q = 0; q < kN / 4; ++q)
+          *reinterpret_cast<f4*>(ck + (int64_t)((t0 + s) / kSub) * a.dim * kN + 4 * q) =
+              f4{h[2 * q][0], h[2 * q][1], h[2 * q + 1][0], h[2 * q + 1][1]};
+      }
+      if (s + 1 < TT) read_bc(s + 1, bcr[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < TT) exps(s + 1, ex[(s + 1) & 1]);
+      const int e = s * 64 + lane;
+      const float dtu = dtus[s], ug = ugs[s], gate = gates[s];
+      const f4* bc = bcr[s & 1];
+      f2 ya = {0.f, 0.f}, yb = {0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < kN / 4; ++q) {
+        const f4 bq = bc[q], cq = bc[kN / 4 + q];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int p = 2 * q + r;
+          const f2 bv = r ? f2{bq[2], bq[3]} : f2{bq[0], bq[1]};
+          const f2 cv = r ? f2{cq[2], cq[3]} : f2{cq[0], cq[1]};
+          h[p] = __builtin_elementwise_fma(ex[s & 1][p], h[p], f2{dtu, dtu} * bv);
+          if (r) yb = __builtin_elementwise_fma(cv, h[p], yb);
+          else ya = __builtin_elementwise_fma(cv, h[p], ya);
+        }
+      }
+      const f2 y2 = ya + yb;
+      const float y = fmaf(Dc, ug, y2[0] + y2[1]) * gate;
+      stf(&sX[wave][buf][0][e], y);  // the output replaces u in the tile image
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // prologue: B/C of tile 0 and the DMA of tiles 0..NB-2, all complete before tile 0
+  load_bc(0);
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k)
+    if (k < nt) dma_tile(k, k);
+  wait_vm<0>(stg);
+  stage_bc(0);
+  for (int it = 0; it < nt; ++it) {
+    const int buf = it % NB;
+    const int prev = (it + NB - 1) % NB;
+    if (it > 0) store_tile(it - 1, prev);  // its LDS read completes before the DMA below refills it
+    const bool more = it + 1 < nt;
+    const bool ahead = it + NB - 1 < nt;
+    if (more) load_bc(it + 1);
+    if (ahead) dma_tile(it + NB - 1, prev);
+    if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf, it & 1);
+    else compute_tile(TrueT{}, it, buf, it & 1);
+    if (more) {
+      if (ahead) wait_vmn<NDMA>(stg);
+      else wait_vm<0>(stg);
+      stage_bc((it + 1) & 1);
+    }
+  }
+  store_tile(nt - 1, (nt - 1) % NB);
+  if (a.last_state) {
+#pragma unroll
+    for (int q = 0; q < kN / 4; ++q)
+      *reinterpret_cast<f4*>(a.last_state + ((int64_t)b * a.dim + c) * kN + 4 * q) =
+          f4{h[2 * q][0], h[2 * q][1], h[2 * q + 1][0], h[2 * q + 1][1]};
+  }
+}
+
+// the one-lane-per-channel forward applies: whole 64-channel waves, 16-byte
+// B/C staging loads, and (unless forced for tests) B*D filling every SIMD
+static bool c1_ok(const MttsScanFwdArgs* a) {
+  if (getenv("MTTS_SCAN_NO_C1") || !wide_io_ok(a) || a->dim % 64) return false;
+  const int es = a->dtype_io == MTTS_BF16 ? 2 : 4, eb = a->dtype_bc == MTTS_BF16 ? 2 : 4;
+  const int bcb = (32 / es) * 2 * kN / 64 * eb;    // B/C bytes per lane per tile
+  const int64_t al = std::min(bcb, 16) / eb;       // element alignment of each load
+  auto ok = [&](const void* p, int64_t bs, int64_t ls) {
+    return ((uintptr_t)p % (al * eb)) == 0 && bs % al == 0 && ls % al == 0;
+  };
+  if (!ok(a->Bm, a->B_bs, a->B_ls) || !ok(a->Cm, a->C_bs, a->C_ls)) return false;
+  if (getenv("MTTS_SCAN_C1")) return true;
+  return (int64_t)a->batch * a->dim >= 65536;
+}
+
 template <int P, typename Tio, typename Tbc, bool SP>
 static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream_t st) {
   const int nbx = (a->dim + kBlock / P - 1) / (kBlock / P);
   float* seg = (float*)a->workspace;
+  if (c1_ok(a)) {
+    const dim3 grid((a->dim / 64 + 3) / 4, a->batch);
+    if (a->z) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true>), grid, dim3(256), 0, st, *a);
+    else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false>), grid, dim3(256), 0, st, *a);
+    return;
+  }
   if (wide_io_ok(a) && !getenv("MTTS_SCAN_FWD_V1")) {
     if (getenv("MTTS_SCAN_XDPP")) {
       if (pl.K > 1)

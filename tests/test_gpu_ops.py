@@ -34,18 +34,22 @@ def g32(a):
     return torch.from_numpy(np.asarray(a)).to(DEV, torch.float32)
 
 
-@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2", "4v1", "2v1:s2", "4d", "2d:s2"])
+@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2", "4v1", "2v1:s2", "4d", "2d:s2", "4c1"])
 def scan_p(request):
     """P (lanes per channel) and, with ':sK', a forced split of L into K
     segments for both the forward and the backward (two-pass path); 'n'
     forces the narrow (per-lane element) forward kernel instead of the
     16-byte-chunk one; 'v1' the register-staged wide forward kernel instead of
     the LDS-DMA one; 'd' the LDS-DMA kernel with DPP broadcasts instead of
-    the LDS (delta, delta*u) exchange."""
+    the LDS (delta, delta*u) exchange; 'c1' the one-lane-per-channel forward
+    (scan_fwd_c1_kernel) forced below its B*D threshold wherever D % 64 == 0."""
     keys = ("MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_BWD_SEGS", "MTTS_SCAN_NARROW", "MTTS_SCAN_FWD_V1",
-            "MTTS_SCAN_XDPP")
+            "MTTS_SCAN_XDPP", "MTTS_SCAN_C1")
     old = {k: os.environ.get(k) for k in keys}
     p, _, segs = request.param.partition(":s")
+    if p.endswith("c1"):
+        p = p[:-2]
+        os.environ["MTTS_SCAN_C1"] = "1"
     if p.endswith("v1"):
         p = p[:-2]
         os.environ["MTTS_SCAN_FWD_V1"] = "1"
@@ -125,6 +129,90 @@ def test_scan_ragged_shapes_and_h0_split(shape, scan_p):
                                  z[:, L1:], bias, True, h0=l1, want_last=True)
         close(torch.cat([o1, o2], 1), out, rtol=1e-5, name="split-out")
         close(l2, last, rtol=1e-5, name="split-last")
+
+
+def _scan_inputs(B, L, D, dtype, bc_dtype, seed, strided_bc=False):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    u = torch.randn(B, L, D, device=DEV, generator=g).to(dtype)
+    z = torch.randn(B, L, D, device=DEV, generator=g).to(dtype)
+    dl = (torch.randn(B, L, D, device=DEV, generator=g) * 0.5).to(dtype)
+    if strided_bc:  # B / C as column slices of an x_proj-style (B, L, R + 2N) row, as the decoder passes them
+        xd = torch.randn(B, L, 64 + 32, device=DEV, generator=g).to(bc_dtype)
+        Bm, Cm = xd[..., 64:80], xd[..., 80:96]
+    else:
+        Bm = torch.randn(B, L, 16, device=DEV, generator=g).to(bc_dtype)
+        Cm = torch.randn(B, L, 16, device=DEV, generator=g).to(bc_dtype)
+    A = -torch.exp(torch.randn(D, 16, device=DEV, generator=g) * 0.5)
+    Dp = torch.randn(D, device=DEV, generator=g)
+    bias = torch.randn(D, device=DEV, generator=g) * 0.1
+    h0 = torch.randn(B, D, 16, device=DEV, generator=g) * 0.5
+    return u, dl, A, Bm, Cm, Dp, z, bias, h0
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: v for k, v in env.items() if v is not None})
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("B,L,D", [(1, 1, 64), (2, 37, 128), (3, 200, 192), (2, 1003, 64), (1, 16, 320)])
+@pytest.mark.parametrize("io,bc", [("f32", "f32"), ("f32", "bf16"), ("bf16", "bf16"), ("bf16", "f32")])
+@pytest.mark.parametrize("with_z,strided", [(True, False), (False, True)])
+def test_scan_c1_kernel_vs_oracle(B, L, D, io, bc, with_z, strided):
+    """scan_fwd_c1_kernel (forced) against the float64 oracle on the same
+    (already rounded) inputs: outputs, last state and the backward's
+    checkpoints (h every 16 steps, compared with the P=4 LDS-DMA kernel's);
+    h0, ragged L (tail tiles), D % 256 != 0 (idle waves), strided B/C."""
+    from mtts import ops
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16}
+    u, dl, A, Bm, Cm, Dp, z, bias, h0 = _scan_inputs(B, L, D, dt[io], dt[bc], B * L + D, strided)
+    z = z if with_z else None
+    run = lambda: ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, h0=h0, want_last=True,  # noqa: E731
+                               want_ckpt=True)
+    out, last, ck = _with_env({"MTTS_SCAN_C1": "1", "MTTS_SCAN_NO_C1": None}, run)
+    out_w, last_w, ck_w = _with_env({"MTTS_SCAN_C1": None, "MTTS_SCAN_NO_C1": "1"}, run)
+    ref, rlast = R.selective_scan_ref(*(t.double().cpu() for t in (u.transpose(1, 2), dl.transpose(1, 2), A,
+                                                                  Bm.transpose(1, 2), Cm.transpose(1, 2), Dp)),
+                                      None if z is None else z.double().cpu().transpose(1, 2),
+                                      bias.double().cpu(), delta_softplus=True, return_last_state=True,
+                                      h0=h0.double().cpu())
+    tol = RTOL if io == "f32" else 1e-2  # bf16 output rounding
+    close(out.transpose(1, 2), ref, rtol=tol, name="c1 out")
+    close(last, rlast, name="c1 last")
+    close(ck, ck_w, rtol=1e-5, name="c1 ckpt vs w2")
+    close(out.float(), out_w.float(), rtol=tol, name="c1 vs w2 out")
+
+
+def test_scan_c1_north_star_width():
+    """At the north-star width (B=32, D=2048: the c1 kernel is the default)
+    with a shorter L: c1 against the P=4 LDS-DMA kernel on every element, and
+    against the float64 oracle on a 64-channel slice of two batch rows."""
+    from mtts import ops
+    B, L, D = 32, 520, 2048
+    u, dl, A, Bm, Cm, Dp, z, bias, _ = _scan_inputs(B, L, D, torch.float32, torch.float32, 7)
+    dl = dl * 0.2
+    run = lambda: ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, want_last=True)  # noqa: E731
+    out, last, _ = _with_env({"MTTS_SCAN_C1": None, "MTTS_SCAN_NO_C1": None}, run)
+    out_w, last_w, _ = _with_env({"MTTS_SCAN_NO_C1": "1"}, run)
+    close(out, out_w, rtol=1e-5, name="c1 vs w2 out")
+    close(last, last_w, rtol=1e-5, name="c1 vs w2 last")
+    for b, c in ((0, 0), (31, 1984)):
+        sl = lambda t: t[b:b + 1, :, c:c + 64].double().cpu().transpose(1, 2)  # noqa: E731
+        ref = R.selective_scan_ref(sl(u), sl(dl), A[c:c + 64].double().cpu(),
+                                   Bm[b:b + 1].double().cpu().transpose(1, 2),
+                                   Cm[b:b + 1].double().cpu().transpose(1, 2), Dp[c:c + 64].double().cpu(), sl(z),
+                                   bias[c:c + 64].double().cpu(), delta_softplus=True)
+        close(out[b:b + 1, :, c:c + 64].transpose(1, 2), ref, name=f"c1 oracle slice b={b} c={c}")
 
 
 def test_scan_bf16_io(golden):
