@@ -1893,18 +1893,20 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   constexpr int EPC = 16 / ES;            // elements per 16-byte chunk
   constexpr int CPR = 64 / EPC;           // chunks per 64-channel row
   constexpr int RPD = 64 / CPR;           // rows per DMA instruction (1 KiB): 4 fp32, 8 bf16
-  constexpr int TT = 2 * RPD;             // steps per tile (2 DMA per array)
-  constexpr int NB = 4;                   // tile ring: DMA NB-1 tiles ahead
+  constexpr int DPT = ES == 4 ? 4 : 2;    // DMA instructions per array per tile
+  constexpr int TT = DPT * RPD;           // steps per tile: 16
+  constexpr int NB = ES == 4 ? 3 : 4;     // tile ring: DMA NB-1 tiles ahead (LDS: 155 / 112 KiB)
   constexpr int NAR = HZ ? 3 : 2;
   constexpr int IMG = TT * 64;
   constexpr int BCV = TT * 2 * kN / 64;   // B/C values staged per lane per tile
   constexpr int LPS = 2 * kN / BCV;       // lanes per B/C row
   constexpr int BCB = BCV * (int)sizeof(Tbc);  // bytes per lane: 8, 16 or 32
   constexpr int NBCI = BCB > 16 ? 2 : 1;  // B/C load instructions per tile
-  constexpr int NDMA = 2 * NAR;           // DMA instructions per tile
+  constexpr int NDMA = DPT * NAR;         // DMA instructions per tile
   static_assert(kN % BCV == 0 && (BCB == 8 || BCB == 16 || BCB == 32), "B/C staging");
   __shared__ __attribute__((aligned(16))) Tio sX[4][NB][NAR][IMG];
-  __shared__ __attribute__((aligned(16))) float sBC[4][2][TT * 2 * kN];
+  // one B/C buffer per wave: staging for tile it+1 follows tile it's last read in program order
+  __shared__ __attribute__((aligned(16))) float sBC[4][1][TT * 2 * kN];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1971,7 +1973,7 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   };
   auto dma_tile = [&](int it, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < DPT; ++k) {
       const int t = min(it * TT + k * RPD + drow, L - 1);  // rows past L: any valid row (never stored)
       dma16(gu + (int64_t)t * a.u_ls, &sX[wave][buf][0][k * RPD * 64]);
       dma16(gd + (int64_t)t * a.delta_ls, &sX[wave][buf][1][k * RPD * 64]);
@@ -1980,7 +1982,7 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   };
   auto store_tile = [&](int it, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < DPT; ++k) {
       const int t = it * TT + k * RPD + drow;
       const uint4 v = *reinterpret_cast<const uint4*>(&sX[wave][buf][0][(k * RPD + drow) * 64 + dcol]);
       if (t < L) *reinterpret_cast<uint4*>(go + (int64_t)t * a.out_ls) = v;
@@ -2071,12 +2073,12 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
     const bool ahead = it + NB - 1 < nt;
     if (more) load_bc(it + 1);
     if (ahead) dma_tile(it + NB - 1, prev);
-    if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf, it & 1);
-    else compute_tile(TrueT{}, it, buf, it & 1);
+    if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf, 0);
+    else compute_tile(TrueT{}, it, buf, 0);
     if (more) {
       if (ahead) wait_vmn<NDMA>(stg);
       else wait_vm<0>(stg);
-      stage_bc((it + 1) & 1);
+      stage_bc(0);
     }
   }
   store_tile(nt - 1, (nt - 1) % NB);
