@@ -1903,6 +1903,10 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   constexpr int BCB = BCV * (int)sizeof(Tbc);  // bytes per lane: 8, 16 or 32
   constexpr int NBCI = BCB > 16 ? 2 : 1;  // B/C load instructions per tile
   constexpr int NDMA = DPT * NAR;         // DMA instructions per tile
+#ifndef MTTS_C1_EA
+#define MTTS_C1_EA 1
+#endif
+  constexpr int EA = MTTS_C1_EA;          // exp(delta*A) formed EA steps ahead of its use
   static_assert(kN % BCV == 0 && (BCB == 8 || BCB == 16 || BCB == 32), "B/C staging");
   __shared__ __attribute__((aligned(16))) Tio sX[4][NB][NAR][IMG];
   // one B/C buffer per wave: staging for tile it+1 follows tile it's last read in program order
@@ -1991,6 +1995,15 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   auto compute_tile = [&](auto tail, int it, int buf, int bb) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail)::value;
     const int t0 = it * TT;
+    // step 0's B/C reads go out first (their latency hides under the scalar work);
+    // (2) below: B/C of step s+1 read (broadcast) while step s computes
+    f4 bcr[2][kN / 2];
+    auto read_bc = [&](int s, f4 (&o)[kN / 2]) __attribute__((always_inline)) {
+      const f4* p = reinterpret_cast<const f4*>(&sBC[wave][bb][s * 2 * kN]);
+#pragma unroll
+      for (int q = 0; q < kN / 2; ++q) o[q] = p[q];
+    };
+    read_bc(0, bcr[0]);
     // (1) the tile's per-channel scalar work up front: TT independent chains
     float dts[TT], dtus[TT], ugs[TT], gates[TT];
 #pragma unroll
@@ -2004,16 +2017,9 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
       dtus[s] = tv ? dt * ugs[s] : 0.f;
       gates[s] = HZ ? silu_f(cvt_raw((raw_t<Tio>)sX[wave][buf][2][e])) : 1.f;
     }
-    // (2) the recurrence, B/C of step s+1 read (broadcast) while step s computes
-    f4 bcr[2][kN / 2];
-    auto read_bc = [&](int s, f4 (&o)[kN / 2]) __attribute__((always_inline)) {
-      const f4* p = reinterpret_cast<const f4*>(&sBC[wave][bb][s * 2 * kN]);
-#pragma unroll
-      for (int q = 0; q < kN / 2; ++q) o[q] = p[q];
-    };
     // exp(delta*A) of step s+1 also forms during step s (independent of h):
     // the transcendental stream of one step overlaps the FMA chain of the other
-    f2 ex[2][kN / 2];
+    f2 ex[EA + 1][kN / 2];
     auto exps = [&](int s, f2 (&o)[kN / 2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int p = 0; p < kN / 2; ++p) {
@@ -2021,8 +2027,8 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
         o[p] = f2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
       }
     };
-    read_bc(0, bcr[0]);
-    exps(0, ex[0]);
+#pragma unroll
+    for (int k = 0; k < EA && k < TT; ++k) exps(k, ex[k]);
 #pragma unroll
     for (int s = 0; s < TT; ++s) {
       if (nck && s % kSub == 0 && ((t0 + s) & (kSub - 1)) == 0 && (!TAIL || t0 + s < L)) {
@@ -2033,7 +2039,7 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
       }
       if (s + 1 < TT) read_bc(s + 1, bcr[(s + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < TT) exps(s + 1, ex[(s + 1) & 1]);
+      if (s + EA < TT) exps(s + EA, ex[(s + EA) % (EA + 1)]);
       const int e = s * 64 + lane;
       const float dtu = dtus[s], ug = ugs[s], gate = gates[s];
       const f4* bc = bcr[s & 1];
@@ -2046,7 +2052,7 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
           const int p = 2 * q + r;
           const f2 bv = r ? f2{bq[2], bq[3]} : f2{bq[0], bq[1]};
           const f2 cv = r ? f2{cq[2], cq[3]} : f2{cq[0], cq[1]};
-          h[p] = __builtin_elementwise_fma(ex[s & 1][p], h[p], f2{dtu, dtu} * bv);
+          h[p] = __builtin_elementwise_fma(ex[s % (EA + 1)][p], h[p], f2{dtu, dtu} * bv);
           if (r) yb = __builtin_elementwise_fma(cv, h[p], yb);
           else ya = __builtin_elementwise_fma(cv, h[p], ya);
         }
