@@ -165,7 +165,8 @@ def _with_env(env, fn):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("B,L,D", [(1, 1, 64), (2, 37, 128), (3, 200, 192), (2, 1003, 64), (1, 16, 320)])
+@pytest.mark.parametrize("B,L,D", [(1, 1, 64), (2, 37, 128), (3, 200, 192), (2, 1003, 64), (1, 16, 320), (2, 203, 256),
+                                   (1, 50, 512)])
 @pytest.mark.parametrize("io,bc", [("f32", "f32"), ("f32", "bf16"), ("bf16", "bf16"), ("bf16", "f32")])
 @pytest.mark.parametrize("with_z,strided", [(True, False), (False, True)])
 def test_scan_c1_kernel_vs_oracle(B, L, D, io, bc, with_z, strided):
