@@ -1995,15 +1995,15 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   auto compute_tile = [&](auto tail, int it, int buf, int bb) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail)::value;
     const int t0 = it * TT;
-    // step 0's B/C reads go out first (their latency hides under the scalar work);
-    // (2) below: B/C of step s+1 read (broadcast) while step s computes
-    f4 bcr[2][kN / 2];
-    auto read_bc = [&](int s, f4 (&o)[kN / 2]) __attribute__((always_inline)) {
-      const f4* p = reinterpret_cast<const f4*>(&sBC[wave][bb][s * 2 * kN]);
+    // step 0's B reads go out first (their latency hides under the scalar work);
+    // (2) below: B of step s+1 and C of step s read (broadcast) during step s
+    f4 bB[2][kN / 4], bC[2][kN / 4];
+    auto read_row = [&](int s, int half, f4 (&o)[kN / 4]) __attribute__((always_inline)) {
+      const f4* p = reinterpret_cast<const f4*>(&sBC[wave][bb][s * 2 * kN + half * kN]);
 #pragma unroll
-      for (int q = 0; q < kN / 2; ++q) o[q] = p[q];
+      for (int q = 0; q < kN / 4; ++q) o[q] = p[q];
     };
-    read_bc(0, bcr[0]);
+    read_row(0, 0, bB[0]);
     // (1) the tile's per-channel scalar work up front: TT independent chains
     float dts[TT], dtus[TT], ugs[TT], gates[TT];
 #pragma unroll
@@ -2029,6 +2029,19 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
     };
 #pragma unroll
     for (int k = 0; k < EA && k < TT; ++k) exps(k, ex[k]);
+    // y of step s-1 (from h before step s's update) is formed in step s, so
+    // no step ends on the dependent y tail (sum, D skip, gate, LDS write)
+    auto yout = [&](int s, const f4 (&cq)[kN / 4]) __attribute__((always_inline)) {
+      f2 ya = {0.f, 0.f}, yb = {0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < kN / 4; ++q) {
+        ya = __builtin_elementwise_fma(f2{cq[q][0], cq[q][1]}, h[2 * q], ya);
+        yb = __builtin_elementwise_fma(f2{cq[q][2], cq[q][3]}, h[2 * q + 1], yb);
+      }
+      const f2 y2 = ya + yb;
+      const float y = fmaf(Dc, ugs[s], y2[0] + y2[1]) * gates[s];
+      stf(&sX[wave][buf][0][s * 64 + lane], y);  // the output replaces u in the tile image
+    };
 #pragma unroll
     for (int s = 0; s < TT; ++s) {
       if (nck && s % kSub == 0 && ((t0 + s) & (kSub - 1)) == 0 && (!TAIL || t0 + s < L)) {
@@ -2037,31 +2050,22 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
           *reinterpret_cast<f4*>(ck + (int64_t)((t0 + s) / kSub) * a.dim * kN + 4 * q) =
               f4{h[2 * q][0], h[2 * q][1], h[2 * q + 1][0], h[2 * q + 1][1]};
       }
-      if (s + 1 < TT) read_bc(s + 1, bcr[(s + 1) & 1]);
+      if (s + 1 < TT) read_row(s + 1, 0, bB[(s + 1) & 1]);
+      read_row(s, 1, bC[s & 1]);
       __builtin_amdgcn_sched_barrier(0);
       if (s + EA < TT) exps(s + EA, ex[(s + EA) % (EA + 1)]);
-      const int e = s * 64 + lane;
-      const float dtu = dtus[s], ug = ugs[s], gate = gates[s];
-      const f4* bc = bcr[s & 1];
-      f2 ya = {0.f, 0.f}, yb = {0.f, 0.f};
+      if (s >= 1) yout(s - 1, bC[(s - 1) & 1]);
+      const float dtu = dtus[s];
 #pragma unroll
       for (int q = 0; q < kN / 4; ++q) {
-        const f4 bq = bc[q], cq = bc[kN / 4 + q];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const int p = 2 * q + r;
-          const f2 bv = r ? f2{bq[2], bq[3]} : f2{bq[0], bq[1]};
-          const f2 cv = r ? f2{cq[2], cq[3]} : f2{cq[0], cq[1]};
-          h[p] = __builtin_elementwise_fma(ex[s % (EA + 1)][p], h[p], f2{dtu, dtu} * bv);
-          if (r) yb = __builtin_elementwise_fma(cv, h[p], yb);
-          else ya = __builtin_elementwise_fma(cv, h[p], ya);
-        }
+        const f4 bq = bB[s & 1][q];
+        h[2 * q] = __builtin_elementwise_fma(ex[s % (EA + 1)][2 * q], h[2 * q], f2{dtu, dtu} * f2{bq[0], bq[1]});
+        h[2 * q + 1] =
+            __builtin_elementwise_fma(ex[s % (EA + 1)][2 * q + 1], h[2 * q + 1], f2{dtu, dtu} * f2{bq[2], bq[3]});
       }
-      const f2 y2 = ya + yb;
-      const float y = fmaf(Dc, ug, y2[0] + y2[1]) * gate;
-      stf(&sX[wave][buf][0][e], y);  // the output replaces u in the tile image
       __builtin_amdgcn_sched_barrier(0);
     }
+    yout(TT - 1, bC[(TT - 1) & 1]);
   };
 
   // prologue: B/C of tile 0 and the DMA of tiles 0..NB-2, all complete before tile 0
