@@ -1906,6 +1906,9 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
 #ifndef MTTS_C1_EA
 #define MTTS_C1_EA 1
 #endif
+#ifndef MTTS_C1_DIRECT_STORE
+#define MTTS_C1_DIRECT_STORE 1  // y stored per step from registers (0: through the tile image as 16-B row chunks)
+#endif
   constexpr int EA = MTTS_C1_EA;          // exp(delta*A) formed EA steps ahead of its use
   static_assert(kN % BCV == 0 && (BCB == 8 || BCB == 16 || BCB == 32), "B/C staging");
   __shared__ __attribute__((aligned(16))) Tio sX[4][NB][NAR][IMG];
@@ -1926,6 +1929,7 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   const Tio* __restrict__ gd = (const Tio*)a.delta + (int64_t)b * a.delta_bs + c0 + dcol;
   const Tio* __restrict__ gz = HZ ? (const Tio*)a.z + (int64_t)b * a.z_bs + c0 + dcol : gu;
   Tio* __restrict__ go = (Tio*)a.out + (int64_t)b * a.out_bs + c0 + dcol;
+  Tio* __restrict__ goc = (Tio*)a.out + (int64_t)b * a.out_bs + c;  // direct-store build
   const int bs = lane / LPS, bcol = (lane % LPS) * BCV;
   const Tbc* __restrict__ gbc = bcol < kN ? (const Tbc*)a.Bm + (int64_t)b * a.B_bs + bcol
                                           : (const Tbc*)a.Cm + (int64_t)b * a.C_bs + (bcol - kN);
@@ -2040,7 +2044,11 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
       }
       const f2 y2 = ya + yb;
       const float y = fmaf(Dc, ugs[s], y2[0] + y2[1]) * gates[s];
+#if MTTS_C1_DIRECT_STORE
+      if (!TAIL || t0 + s < L) stf(goc + (int64_t)(t0 + s) * a.out_ls, y);  // one 4-byte store per lane and step
+#else
       stf(&sX[wave][buf][0][s * 64 + lane], y);  // the output replaces u in the tile image
+#endif
     };
 #pragma unroll
     for (int s = 0; s < TT; ++s) {
@@ -2078,7 +2086,7 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   for (int it = 0; it < nt; ++it) {
     const int buf = it % NB;
     const int prev = (it + NB - 1) % NB;
-    if (it > 0) store_tile(it - 1, prev);  // its LDS read completes before the DMA below refills it
+    if (!MTTS_C1_DIRECT_STORE && it > 0) store_tile(it - 1, prev);  // its LDS read completes before the DMA below refills it
     const bool more = it + 1 < nt;
     const bool ahead = it + NB - 1 < nt;
     if (more) load_bc(it + 1);
@@ -2086,12 +2094,12 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
     if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf, 0);
     else compute_tile(TrueT{}, it, buf, 0);
     if (more) {
-      if (ahead) wait_vmn<NDMA>(stg);
+      if (ahead) wait_vmn<NDMA + (MTTS_C1_DIRECT_STORE ? TT : 0)>(stg);  // stores of a full tile follow the DMA
       else wait_vm<0>(stg);
       stage_bc(0);
     }
   }
-  store_tile(nt - 1, (nt - 1) % NB);
+  if (!MTTS_C1_DIRECT_STORE) store_tile(nt - 1, (nt - 1) % NB);
   if (a.last_state) {
 #pragma unroll
     for (int q = 0; q < kN / 4; ++q)
