@@ -1,7 +1,11 @@
 """Benchmark: MambaTTSDecoder teacher-forced training step on MI355X.
 
 python bench.py --gpus N --steps K --warmup W
-  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+  N > 1: one rank per GPU over RCCL.  Under torch.distributed.run (WORLD_SIZE
+  set) the ranks run directly; a plain `python bench.py --gpus N` starts
+  `python -m torch.distributed.run --nproc-per-node N ... bench.py` as a
+  child process before touching the GPU and relays its exit code (rank 0
+  prints the JSON line).
 
 Headline (BASELINE.json metric, configs[1] = C2): audio tokens/s of one
 fwd+bwd+clip+Adam step of the 12-layer d_model=1024 decoder at B=8 per GPU,
@@ -9,7 +13,16 @@ T_audio=2048, T_text=128 (10 % padded), bf16 compute, random-init weights,
 synthetic tokens.  Batch-DP across ranks (weak scaling) with an RCCL
 all-reduce of the gradients.
 
-Also reported on rank 0 (same JSON line):
+`value` is the whole job's throughput (all ranks' tokens / max-over-ranks
+time, weak scaling: B=8 per GPU); `value_per_gpu` = value / N.
+
+Every N: `scan_scaling` -- the north-star selective_scan forward (B=32,
+L=8192, d_inner=2048, fp32 I/O) as a second scaling leg, no collective on the
+data path: "weak" (every rank scans its own B=32 batch) and "strong" (the
+B=32 batch sharded 32/N rows per rank); bytes of all ranks / max-over-ranks
+time.
+
+Also reported on rank 0 at N = 1 (same JSON line):
   roofline      selective_scan fwd at the north-star shape (B=32, L=8192,
                 d_inner=2048, N=16) with fp32 I/O -- the reference's own
                 precision (train.py runs mamba-ssm in fp32) -- HIP-event
@@ -156,8 +169,12 @@ def train_bench(args, rank, world, dev):
     return c, ms, tokens_per_s, (first_loss, float(loss.item()))
 
 
-def scan_roofline(dtype, B=32, L=8192, D=2048, iters=20):
-    """selective_scan fwd at the north-star shape; returns (ms, bytes, GB/s)."""
+def scan_roofline(dtype, B=32, L=8192, D=2048, iters=20, rounds=5, barrier=False):
+    """selective_scan fwd at the north-star shape; returns (ms, bytes, GB/s):
+    the median over `rounds` of the per-launch HIP-event time of `iters`
+    back-to-back launches on the launch stream (torch's current stream, which
+    ops.scan_fwd launches on).  barrier: bracket each round by a process-group
+    barrier (scaling leg)."""
     from mtts import ops
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
@@ -177,16 +194,19 @@ def scan_roofline(dtype, B=32, L=8192, D=2048, iters=20):
         run()
     torch.cuda.synchronize()
     # median over 5 timed rounds of `iters` back-to-back launches (per-launch average of each round)
-    rounds = []
-    for _ in range(5):
+    times = []
+    for _ in range(rounds):
+        if barrier:
+            torch.cuda.synchronize()
+            dist.barrier()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
         for _ in range(iters):
             run()
         ev1.record()
         ev1.synchronize()
-        rounds.append(ev0.elapsed_time(ev1) / iters)
-    ms = sorted(rounds)[len(rounds) // 2]
+        times.append(ev0.elapsed_time(ev1) / iters)
+    ms = sorted(times)[len(times) // 2]
     es = torch.finfo(dtype).bits // 8
     nbytes = 4 * B * D * L * es + 2 * B * N * L * es + (D * N + 2 * D) * 4
     del u, z, delta, Bm, Cm, out
@@ -422,19 +442,97 @@ def cpu_baseline(budget_s=20.0):
                       f"{n} iters in {dt:.1f}s"}
 
 
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: run torch.distributed.run
+    with N ranks (one per GPU) as a CHILD process -- started before anything
+    here touches the GPU -- and return its exit code.  Rank 0's JSON line
+    reaches stdout directly (inherited descriptors)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def _max_over_ranks(v, world, dev):
+    if world == 1:
+        return v
+    t = torch.tensor([v], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def launch_check(args, world):
+    """The N-rank plumbing without GPU work (CPU, gloo): process group,
+    barrier-bracketed 'timed region', max-over-ranks time, rank-0 JSON."""
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(os.environ.get("MTTS_DIST_BACKEND", "gloo"))
+        dist.barrier()
+    t0 = time.perf_counter()
+    x = torch.ones(1024) * (rank + 1)
+    if world > 1:
+        dist.all_reduce(x)
+        dist.barrier()
+    dt = _max_over_ranks(time.perf_counter() - t0, world, "cpu")
+    if rank == 0:
+        print(json.dumps({"metric": "launch-check", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "allreduce_ok": bool(x[0].item() == world * (world + 1) / 2), "seconds": dt}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def scan_scaling(rank, world, dev, iters=10):
+    """Second scaling leg: the north-star selective_scan forward (fp32 I/O)
+    with no collective on the data path.  weak: every rank scans its own
+    B=32 batch; strong: the B=32 batch split 32/N rows per rank.  Per leg:
+    barrier, `iters` launches, synchronize, barrier; time = max over ranks;
+    value = algorithmic bytes of all ranks / time."""
+    out = {}
+    for leg in ("weak", "strong"):
+        B = 32 if leg == "weak" else max(1, 32 // world)
+        if world > 1:
+            dist.barrier()
+        ms, nbytes, _ = scan_roofline(torch.float32, B=B, iters=iters, rounds=1, barrier=world > 1)
+        ms = _max_over_ranks(ms, world, dev)
+        total = nbytes * world
+        out[leg] = {"batch_per_rank": B, "ms_per_launch": ms, "GB_per_s": total / (ms * 1e-3) / 1e9,
+                    "frac_of_n_x_hbm_peak": total / (ms * 1e-3) / (world * HBM_PEAK)}
+    out["unit"] = "GB/s (algorithmic bytes of all ranks / max-over-ranks time)"
+    log(f"[bench] scan scaling N={world}: {out}")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--decode-steps", type=int, default=400)
+    ap.add_argument("--decode-steps", type=int, default=4096)   # C4: 4096-step AR loop
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--skip-extras", action="store_true")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay the training step as one captured hipGraph (equal speed here: the step is GPU-bound)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="distributed plumbing only (process group, barrier, max-over-ranks timing, JSON line), "
+                         "no GPU work: CPU rehearsal of the N-rank launch with MTTS_DIST_BACKEND=gloo")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}")
+    if args.launch_check:
+        return launch_check(args, world)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -451,14 +549,16 @@ def main():
     # the roofline kernel is timed first, on the chip as the driver hands it over
     # (after the C2 training loop the same launches measure ~5-7 % slower: clocks)
     roof = None
-    if rank == 0 and not args.skip_extras:
+    if rank == 0 and world == 1 and not args.skip_extras:
         roof = (scan_roofline(torch.float32), scan_roofline(torch.bfloat16))
     c, ms, tps, loss = train_bench(args, rank, world, dev)
+    scaling_leg = scan_scaling(rank, world, dev)
     log(f"[bench] step {ms:.2f} ms  {tps:.0f} tok/s  loss first warmup step {loss[0]} -> last timed step {loss[1]:.3e} "
         f"(one fixed batch; the decoder's unshifted targets, SURVEY quirk 4, make it learn the identity fast)")
     rec = {
         "metric": "audio tokens/sec (teacher-forced fwd+bwd) per GPU; decode_step p50 latency",
-        "value": tps, "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": tps, "value_per_gpu": tps / world, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup,
         "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (random tokens/text/z_style, random-init weights)",
         "config": {"workload": "C2: MambaTTSDecoder 12L d_model=1024 fwd+bwd+clip+Adam, B=8/GPU T_audio=2048 "
@@ -468,18 +568,28 @@ def main():
     fl = flops_per_step(c)
     rec["step_mfma"] = {"bound": "mfma", "achieved": fl / (ms * 1e-3) / 1e12, "peak": BF16_PEAK / 1e12,
                         "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / BF16_PEAK, "flops_per_step": fl}
-    if rank == 0 and not args.skip_extras:
-        (fms, fb, fbw), (sms, sb, sbw) = roof
+    rec["scan_scaling"] = scaling_leg
+    if roof is None:
+        # N > 1 (or --skip-extras): the roofline kernel's per-GPU figure from the
+        # weak leg (each rank ran the full north-star batch; slowest rank)
+        wk = scaling_leg["weak"]
+        nb = wk["GB_per_s"] * 1e9 * wk["ms_per_launch"] * 1e-3 / world
+        roof = ((wk["ms_per_launch"], nb, nb / (wk["ms_per_launch"] * 1e-3)), None)
+    if rank == 0:
+        (fms, fb, fbw) = roof[0]
         log(f"[bench] scan fp32 north-star {fms:.3f} ms {fbw / 1e9:.0f} GB/s")
         rec["roofline"] = {"kernel": "selective_scan_fwd (north-star B=32 L=8192 d_inner=2048 N=16, fp32 I/O = the "
                                      "reference's precision, f32 math)",
                            "bound": "hbm", "achieved": fbw / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                            "frac": fbw / HBM_PEAK, "traffic": pmc_traffic("fp32"), "ms": fms, "algorithmic_bytes": fb,
                            "traffic_source": "profiles/r01c1_scan_pmc_summary.json (2*FETCH_SIZE+WRITE_SIZE)"}
-        log(f"[bench] scan bf16 north-star {sms:.3f} ms {sbw / 1e9:.0f} GB/s")
-        rec["roofline_bf16"] = {"bound": "hbm (VALU-limited, DESIGN.md section 3)", "achieved": sbw / 1e9,
-                                "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": sbw / HBM_PEAK, "ms": sms,
-                                "algorithmic_bytes": sb, "traffic": pmc_traffic("bf16")}
+        if roof[1] is not None:
+            (sms, sb, sbw) = roof[1]
+            log(f"[bench] scan bf16 north-star {sms:.3f} ms {sbw / 1e9:.0f} GB/s")
+            rec["roofline_bf16"] = {"bound": "hbm (VALU-limited, DESIGN.md section 3)", "achieved": sbw / 1e9,
+                                    "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": sbw / HBM_PEAK, "ms": sms,
+                                    "algorithmic_bytes": sb, "traffic": pmc_traffic("bf16")}
+    if rank == 0 and world == 1 and not args.skip_extras:
         rec["c5_decoder"] = c5_decoder_bench()
         log(f"[bench] c5 decoder {rec['c5_decoder']}")
         rec["text_encoder"] = text_bench()

@@ -15,7 +15,8 @@ Reference quirks reproduced on purpose:
   * key_padding_mask = ~text_mask (True in text_mask = attend);
   * decode_step adds no quant_embed;
   * FiLM is gamma*h + beta with tanh-bounded gamma; GELU is exact (erf);
-  * 3D tokens with Q > 1 raise (size mismatch), as in the reference.
+  * 3D tokens (B, Q, T) with Q > 1 raise RuntimeError (the reference adds
+    pos_embed(arange(T)) to Q*T token rows: size mismatch, :169-171).
 
 Precision: set `model.compute_dtype = torch.bfloat16` to run activations and
 GEMMs in bf16 (params stay fp32 masters; scan/LN math is fp32 internally).
@@ -200,10 +201,15 @@ class MambaTTSDecoder(nn.Module):
         text_hidden = text_hidden.to(cd)
         text_hidden, text_mask = self._concat_ref(text_hidden, text_mask, ref_hidden, ref_mask, B, device)
 
-        # token + position + quantizer embeddings (:201-206), fused backward
-        if audio_tokens.shape[1] > self.pos_embed.num_embeddings:
-            raise IndexError(f"sequence length {audio_tokens.shape[1]} exceeds pos_embed max_len "
-                             f"{self.pos_embed.num_embeddings}")
+        # token + position + quantizer embeddings (:167-171), fused backward.
+        # The reference embeds positions arange(T) of the UNflattened length,
+        # so `tok (B, Q*T, d) + pos (B, T, d)` fails for Q > 1 (quirk 3):
+        # raise the same broadcast error instead of computing a result.
+        if T > self.pos_embed.num_embeddings:
+            raise IndexError("index out of range in self")                    # pos_embed(arange(T)), :169-170
+        if audio_tokens.shape[1] != T:
+            raise RuntimeError(f"The size of tensor a ({audio_tokens.shape[1]}) must match the size of tensor b "
+                               f"({T}) at non-singleton dimension 1")            # tok + pos, :171
         x = embed_sum(audio_tokens, quant_ids, self.token_embed.weight, self.quant_embed.weight,
                       self.pos_embed.weight, cd)
 

@@ -8,8 +8,10 @@ gamma/beta of the (constant) style vector; the engine computes them once per
 conditioning context and keeps them in HBM with the per-layer SSM/conv state.
 
 Engine path (inference only: torch.no_grad, HIP tensors):
-  * context cache keyed on the identity/version/shape of text_hidden,
-    text_mask, ref_hidden, ref_mask, z_style and the compute dtype;
+  * context cache keyed on the object identity (strong references are
+    held, so addresses cannot be recycled) and autograd version of
+    text_hidden, text_mask, ref_hidden, ref_mask, z_style, plus the compute
+    dtype and batch shape;
   * per step: token+pos embedding, then per layer LN -> Mamba.step (HIP
     conv-window + state-update kernels, states updated in place) -> fused
     residual+LN -> q-projection + attention over cached K/V -> fused
@@ -34,10 +36,19 @@ from .attn_kernels import attention
 from .linear import cast_weight
 
 
-def _key(t):
-    if t is None:
-        return None
-    return (t.data_ptr(), t._version, tuple(t.shape), t.dtype)
+def _same_ctx(refs, versions, tensors):
+    """True when `tensors` are the very objects cached in `refs` (identity,
+    not address: the engine holds strong references, so a freed tensor's
+    address can never be reused for a new one while the cache is alive)
+    and none was modified in place since (autograd version counter)."""
+    if refs is None or len(refs) != len(tensors):
+        return False
+    for r, v, t in zip(refs, versions, tensors):
+        if r is not t:
+            return False
+        if t is not None and t._version != v:
+            return False
+    return True
 
 
 def _proj_blas(x, w, b=None, act=None):
@@ -61,6 +72,8 @@ class DecodeEngine:
 
     def reset(self):
         self.ctx_key = None
+        self.ctx_refs = None
+        self.ctx_versions = None
         self.ctx = None
         self.graph = None
         self.states = None
@@ -193,11 +206,13 @@ class DecodeEngine:
              ref_mask=None):
         m = self.m
         cd = m._cd()
-        key = (_key(text_hidden), _key(z_style), _key(text_mask), _key(ref_hidden), _key(ref_mask), cd,
-               tuple(last_token.shape))
-        if key != self.ctx_key:
+        conds = (text_hidden, z_style, text_mask, ref_hidden, ref_mask)
+        key = (cd, tuple(last_token.shape))
+        if key != self.ctx_key or not _same_ctx(self.ctx_refs, self.ctx_versions, conds):
             self.ctx = self._build_ctx(text_hidden, z_style, text_mask, ref_hidden, ref_mask, cd)
             self.ctx_key = key
+            self.ctx_refs = conds                  # strong references (see _same_ctx)
+            self.ctx_versions = tuple(None if t is None else t._version for t in conds)
             self.fused = self._fused_ok(cd, last_token.shape[0])
             self.graph = None
             self.states = None

@@ -25,17 +25,20 @@ class GradAllReduce:
         self.params = [p for p in params if p.requires_grad]
         order = list(reversed(self.params))
         dev = order[0].device
+        dtype = order[0].dtype
         total = sum(p.numel() for p in order)
-        self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
-        cap = max(1, int(bucket_mb * 1024 * 1024 // 4))
+        self.flat = torch.zeros(total, device=dev, dtype=dtype)
+        cap = max(1, int(bucket_mb * 1024 * 1024 // self.flat.element_size()))
         self.buckets = []        # (start, end, n_params)
         self.bucket_of = {}
         off, start, count = 0, 0, 0
+        self.views = {}
         for p in order:
-            if p.dtype != torch.float32:
-                raise TypeError("GradAllReduce expects fp32 master parameters")
+            if p.dtype != dtype or dtype not in (torch.float32, torch.float64):
+                raise TypeError("GradAllReduce expects fp32 (or, for tests, fp64) master parameters of one dtype")
             n = p.numel()
-            p.grad = self.flat[off:off + n].view_as(p)
+            self.views[p] = self.flat[off:off + n].view_as(p)
+            p.grad = self.views[p]
             self.bucket_of[p] = len(self.buckets)
             off += n
             count += 1
@@ -49,11 +52,23 @@ class GradAllReduce:
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
 
     def zero_grad(self):
+        """Zero the flat buffer and re-bind every p.grad to its view (the
+        contract: call this, not optimizer.zero_grad(), between steps)."""
         self.flat.zero_()
+        for p, v in self.views.items():
+            p.grad = v
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
 
     def _hook(self, p):
+        v = self.views[p]
+        if p.grad is not v and p.grad.data_ptr() != v.data_ptr():
+            # autograd allocated a fresh gradient (the optimizer's zero_grad
+            # set_to_none=True dropped the view): fold it into the bucket view
+            # (the stale bucket content is overwritten, as after a zeroing) so
+            # the all-reduce sees it, and re-bind
+            v.copy_(p.grad)
+            p.grad = v
         b = self.bucket_of[p]
         self.pending[b] += 1
         if self.pending[b] == self.buckets[b][2]:
@@ -68,6 +83,10 @@ class GradAllReduce:
                 self.handles[b] = dist.all_reduce(self.flat[s:e], group=self.group, async_op=True)
         for h in self.handles:
             h.wait()
+        for p, v in self.views.items():
+            if p.grad is not None and p.grad is not v and p.grad.data_ptr() != v.data_ptr():
+                raise RuntimeError("GradAllReduce: a gradient left the flat buffer after its hook; "
+                                   "zero gradients with GradAllReduce.zero_grad()")
         if self.world > 1:
             self.flat.mul_(1.0 / self.world)
         self.handles = [None] * len(self.buckets)

@@ -52,13 +52,15 @@ class MambaInnerFn(torch.autograd.Function):
         need = any(ctx.needs_input_grad)
         y, last, ckpt = ops.scan_fwd(u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, want_last=True, want_ckpt=need)
         if need:
-            ctx.save_for_backward(xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt)
+            ctx.save_for_backward(xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt,
+                                  conv_state_in, h0)
         ctx.mark_non_differentiable(conv_state, last)
         return y, conv_state, last
 
     @staticmethod
     def backward(ctx, dy, _dconv, _dlast):
-        xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt = ctx.saved_tensors
+        (xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt,
+         conv_state_in, h0) = ctx.saved_tensors
         cd = u.dtype
         Wx, Wdt = cast_weight(W_x, cd), cast_weight(W_dt, cd)
         di = xz.shape[-1] // 2
@@ -70,9 +72,10 @@ class MambaInnerFn(torch.autograd.Function):
         A = -torch.exp(A_log.float())
         dxz = torch.empty_like(xz)
         dx_dbl = torch.empty(Bsz, Ln, r + 2 * N, device=xz.device, dtype=torch.float32)
-        du, ddelta, _, _, _, dA, dD, dbias, _ = ops.scan_bwd(
-            u, delta, A, Bm, Cm, D, z, dt_bias, True, None, ckpt, dy,
-            dz=dxz[..., di:], dB=dx_dbl[..., r:r + N], dC=dx_dbl[..., r + N:])
+        need_dh0 = h0 is not None and ctx.needs_input_grad[9]
+        du, ddelta, _, _, _, dA, dD, dbias, dh0 = ops.scan_bwd(
+            u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, ckpt, dy,
+            dz=dxz[..., di:], dB=dx_dbl[..., r:r + N], dC=dx_dbl[..., r + N:], need_dh0=need_dh0)
         # dt_proj: delta = dt @ W_dt^T
         dd2 = ddelta.reshape(-1, di)
         dx_dbl[..., :r] = (ddelta @ Wdt).float()
@@ -81,10 +84,39 @@ class MambaInnerFn(torch.autograd.Function):
         gx = dx_dbl.to(cd)
         du.view(-1, di).addmm_(gx.view(-1, r + 2 * N), Wx)   # du += d(x_dbl) W_x, accumulated by the GEMM
         dW_x = wgrad(gx.reshape(-1, r + 2 * N), u.reshape(-1, di))
-        _, dw, db = ops.conv_bwd(x, conv_w, conv_b, du, True, dx=dxz[..., :di])
+        # the conv's left history (a prefilled conv_state) enters the
+        # recomputed pre-activations and the weight gradient
+        _, dw, db = ops.conv_bwd(x, conv_w, conv_b, du, True, dx=dxz[..., :di], state_in=conv_state_in)
+        dstate = None
+        if conv_state_in is not None and ctx.needs_input_grad[8]:
+            dstate = _conv_state_grad(x, conv_w, conv_b, conv_state_in, du)
         dA_log = (dA * A).to(A_log.dtype)
         return (dxz, dw.reshape(conv_w.shape).to(conv_w.dtype), db.to(conv_b.dtype), dW_x.to(W_x.dtype),
-                dW_dt.to(W_dt.dtype), dA_log, dD.to(D.dtype), dbias.to(dt_bias.dtype), None, None)
+                dW_dt.to(W_dt.dtype), dA_log, dD.to(D.dtype), dbias.to(dt_bias.dtype), dstate,
+                None if dh0 is None else dh0.to(h0.dtype))
+
+
+def _conv_state_grad(x, conv_w, conv_b, state, du):
+    """d conv_state (B, D, K): the history column j (time j - K) feeds the
+    pre-activations of the first K - 1 steps with weight w[j - 1 - t]
+    (out[t] = sum_k w[k] [state | x][t + 1 + k]).  O(B * D * K^2) on the
+    first K - 1 steps only, so a few tiny device ops."""
+    K = state.shape[-1]
+    di = state.shape[1]
+    w = conv_w.reshape(di, K).float()
+    L = x.shape[1]
+    n = min(K - 1, L)
+    full = torch.cat([state.float(), x[:, :n].transpose(1, 2).float()], dim=-1)   # (B, D, K + n)
+    pre = torch.stack([(full[:, :, 1 + t:1 + t + K] * w).sum(-1) for t in range(n)], dim=-1)
+    if conv_b is not None:
+        pre = pre + conv_b.float()[None, :, None]
+    s = torch.sigmoid(pre)
+    g = du[:, :n].transpose(1, 2).float() * s * (1 + pre * (1 - s))               # dL/dpre, (B, D, n)
+    ds = torch.zeros_like(state, dtype=torch.float32)
+    for j in range(1, K):
+        for t in range(min(j, n)):
+            ds[:, :, j] += w[:, j - 1 - t] * g[:, :, t]
+    return ds.to(state.dtype)
 
 
 class Mamba(nn.Module):

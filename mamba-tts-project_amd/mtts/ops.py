@@ -195,10 +195,13 @@ def conv_fwd(x, w, bias=None, silu=True, state_in=None, want_state=False, out=No
     return out, st
 
 
-def conv_bwd(x, w, bias, dout, silu=True, dx=None):
+def conv_bwd(x, w, bias, dout, silu=True, dx=None, state_in=None):
+    """Backward of conv_fwd: dx (into `dx` if given), dw, db.  `state_in`
+    (B, D, K) is the forward's left history (recomputed pre-activations and
+    dw include it); its own gradient is not produced here."""
     Bsz, Ln, Dm = x.shape
     w = _f32c(w.reshape(Dm, -1))
-    bias = _f32c(bias)
+    bias, state_in = _f32c(bias), _f32c(state_in)
     dout = dout if dout.stride(-1) == 1 else dout.contiguous()
     if dout.dtype != x.dtype:
         dout = dout.to(x.dtype)
@@ -208,7 +211,7 @@ def conv_bwd(x, w, bias, dout, silu=True, dx=None):
     ws = torch.empty(L.lib().mtts_causal_conv1d_bwd_workspace(Bsz, Dm, Ln, w.shape[1]), device=x.device,
                      dtype=torch.uint8)
     b = L.ConvBwdArgs()
-    b.f = _conv_args(x, w, bias, silu, None, dout, None)
+    b.f = _conv_args(x, w, bias, silu, state_in, dout, None)
     b.dout, b.dout_bs, b.dout_ls = dout.data_ptr(), dout.stride(0), dout.stride(1)
     b.dx, b.dx_bs, b.dx_ls = dx.data_ptr(), dx.stride(0), dx.stride(1)
     b.dw, b.dbias, b.workspace = dw.data_ptr(), db.data_ptr(), ws.data_ptr()

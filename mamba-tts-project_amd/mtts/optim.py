@@ -36,7 +36,10 @@ class FusedClipAdam(torch.optim.Optimizer):
         and moments are fixed; gradients may move between steps (zero_grad
         set_to_none), so a changed list is re-uploaded from a pinned buffer
         with an asynchronous copy (no host stall)."""
-        pkey = tuple(p.data_ptr() for p in ps)
+        # the descriptors hold raw pointers of p AND of its moments: key on
+        # both, so replaced state tensors (load_state_dict) get a new plan
+        pkey = tuple((p.data_ptr(), self.state[p]["exp_avg"].data_ptr(), self.state[p]["exp_avg_sq"].data_ptr())
+                     for p in ps)
         gkey = tuple(p.grad.data_ptr() for p in ps)
         plan = self._plans.get(pkey)
         lib = L.lib()
@@ -145,6 +148,19 @@ class FusedClipAdam(torch.optim.Optimizer):
         for g in sd["param_groups"]:
             g.pop("_dstep", None)
         return sd
+
+    def load_state_dict(self, state_dict):
+        """torch.optim.Adam.load_state_dict, then drop every cached descriptor
+        plan (they point at the replaced moment tensors) and the device step
+        counters (re-seeded from the loaded state["step"] on the next step)."""
+        super().load_state_dict(state_dict)
+        self._plans = {}
+        for g in self.param_groups:
+            g.pop("_dstep", None)
+        for st in self.state.values():
+            # torch's loader may move "step" to the parameter's device; keep it a host scalar as __init__ does
+            if "step" in st and torch.is_tensor(st["step"]) and st["step"].device.type != "cpu":
+                st["step"] = st["step"].detach().cpu()
 
 
 @torch.no_grad()

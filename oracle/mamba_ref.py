@@ -21,7 +21,9 @@ vectors produced in the build container from
 See tests/golden/make_golden.py.
 
 Layouts follow upstream mamba-ssm: u/delta/z are (B, D, L), B/C are (B, N, L).
-Everything runs in the dtype of the inputs (tests use float64 for grads).
+Everything runs in the dtype and on the device of the inputs (tests use
+float64 for grads; the large-shape parity tests evaluate this same
+restatement on the GPU in float64 so that it finishes in seconds).
 """
 from __future__ import annotations
 
@@ -59,7 +61,7 @@ def selective_scan_ref(u, delta, A, B, C, D=None, z=None, delta_bias=None,
     if delta_softplus:
         dt = softplus(dt)
     Bsz, Dm, L = u.shape
-    h = torch.zeros(Bsz, Dm, A.shape[1], dtype=u.dtype) if h0 is None else h0.to(u.dtype)
+    h = torch.zeros(Bsz, Dm, A.shape[1], dtype=u.dtype, device=u.device) if h0 is None else h0.to(u.dtype)
     ys = []
     for t in range(L):
         dA = torch.exp(dt[:, :, t, None] * A[None])                      # (B, D, N)
@@ -85,7 +87,7 @@ def causal_conv1d_ref(x, weight, bias=None, activation=None, conv_state=None):
     """
     Bsz, Dm, L = x.shape
     K = weight.shape[1]
-    prev = torch.zeros(Bsz, Dm, K, dtype=x.dtype) if conv_state is None else conv_state.to(x.dtype)
+    prev = torch.zeros(Bsz, Dm, K, dtype=x.dtype, device=x.device) if conv_state is None else conv_state.to(x.dtype)
     full = torch.cat([prev, x], dim=-1)                                  # (B, D, K+L)
     out = torch.zeros_like(x)
     for k in range(K):
@@ -164,8 +166,8 @@ def embed_codec_tokens_ref(tokens_3d, tok_w, pos_w, q_w):
     q_w[arange(Q).repeat_interleave(T)]; mask True where the id is 0."""
     B, Q, T = tokens_3d.shape
     flat = tokens_3d.reshape(B, Q * T)
-    quant_ids = torch.arange(Q).repeat_interleave(T).unsqueeze(0).expand(B, -1)
-    pos_ids = torch.arange(T).repeat(Q)
+    quant_ids = torch.arange(Q, device=tokens_3d.device).repeat_interleave(T).unsqueeze(0).expand(B, -1)
+    pos_ids = torch.arange(T, device=tokens_3d.device).repeat(Q)
     ref = F.embedding(flat, tok_w) + F.embedding(pos_ids, pos_w)[None].expand(B, -1, -1) + F.embedding(quant_ids, q_w)
     return ref, (tokens_3d == 0).reshape(B, Q * T)
 
@@ -319,7 +321,7 @@ def _concat_ref(text_hidden, text_mask, ref_hidden, ref_mask):
         return text_hidden, text_mask
     B = ref_hidden.shape[0]
     if ref_mask is None:
-        ref_mask = torch.ones(B, ref_hidden.shape[1], dtype=torch.bool)
+        ref_mask = torch.ones(B, ref_hidden.shape[1], dtype=torch.bool, device=ref_hidden.device)
     text_hidden = torch.cat([ref_hidden, text_hidden], dim=1)
     text_mask = ref_mask if text_mask is None else torch.cat([ref_mask, text_mask], dim=1)
     return text_hidden, text_mask
@@ -330,6 +332,8 @@ def decoder_forward_ref(p, n_layers, n_heads, audio_tokens, text_hidden, z_style
     """Restates MambaTTSDecoder.forward (mamba_decoder.py:120-186), 2D tokens."""
     B, T = audio_tokens.shape
     text_hidden, text_mask = _concat_ref(text_hidden, text_mask, ref_hidden, ref_mask)
+    if T > p["pos_embed.weight"].shape[0]:
+        raise IndexError("index out of range in self")                # pos_embed(arange(T)), :169-170
     x = (p["token_embed.weight"][audio_tokens] + p["pos_embed.weight"][:T][None]
          + p["quant_embed.weight"][torch.zeros_like(audio_tokens)])
     for i in range(n_layers):

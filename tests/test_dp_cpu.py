@@ -1,7 +1,16 @@
 """Multi-process data-parallel gradient all-reduce (mtts/dp.py) on CPU with
-the gloo backend, world_size 2: averaged gradients equal the single-process
-gradient of the concatenated batch, buckets overlap the backward, unused
-parameters still reduce."""
+the gloo backend, world_size 2, on the DECODER's parameter set: a 2-layer
+MambaTTSDecoder's state_dict as trainable tensors, its forward evaluated by
+the float64 oracle restatement (the HIP forward needs a GPU: the same test on
+the real module + FusedClipAdam is tests/test_gpu_dp.py), CE(ignore 0) loss,
+clip_grad_norm_(1.0) + Adam (train.py:228-235).
+
+Checks: after 2 steps the averaged gradients and the updated parameters of
+every rank equal a single process stepping on the mean of the per-shard
+losses; small buckets (many overlapped all-reduces) and one big bucket;
+zero_grad through GradAllReduce, and through the optimizer's
+zero_grad(set_to_none=True) (the hooks re-bind fresh gradients into the
+flat buffer)."""
 import os
 import socket
 
@@ -9,6 +18,10 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+WORLD = 2
+SHARD = 2        # sequences per rank
+T, TT, D = 16, 6, 32
 
 
 def _free_port():
@@ -19,58 +32,84 @@ def _free_port():
     return p
 
 
-class Toy(torch.nn.Module):
-    def __init__(self):
-        super().__init__()
-        self.a = torch.nn.Linear(16, 32)
-        self.b = torch.nn.Linear(32, 8)
-        self.unused = torch.nn.Linear(4, 4)
-
-    def forward(self, x):
-        return self.b(torch.tanh(self.a(x)))
-
-
-def _worker(rank, world, port, bucket_mb, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from mtts.dp import GradAllReduce
+def _model():
+    """The drop-in module only for its parameter set (keys / shapes / init)."""
+    import mamba_decoder
     torch.manual_seed(0)
-    m = Toy()
+    m = mamba_decoder.MambaTTSDecoder(10, d_model=D, n_layers=2, n_heads=4, d_ff=64, d_style=8, max_len=64)
+    return {k: torch.nn.Parameter(v.detach().double().clone()) for k, v in m.state_dict().items()}
+
+
+def _batch():
     g = torch.Generator().manual_seed(100)
-    x = torch.randn(world * 6, 16, generator=g)
-    dp = GradAllReduce(m.parameters(), bucket_mb=bucket_mb)
-    for _ in range(2):  # twice: state must reset between steps
-        dp.zero_grad()
-        m(x[rank * 6:(rank + 1) * 6]).square().mean().backward()
+    tok = torch.randint(0, 10, (WORLD * SHARD, T), generator=g)
+    text = torch.randn(WORLD * SHARD, TT, D, generator=g, dtype=torch.float64)
+    z = torch.randn(WORLD * SHARD, 8, generator=g, dtype=torch.float64)
+    mask = torch.ones(WORLD * SHARD, TT, dtype=torch.bool)
+    mask[:, 4:] = False
+    return tok, text, z, mask
+
+
+def _loss(p, tok, text, z, mask):
+    from oracle import mamba_ref as R
+    logits = R.decoder_forward_ref(p, 2, 4, tok, text, z, text_mask=mask)
+    return torch.nn.functional.cross_entropy(logits.reshape(-1, 10), tok.reshape(-1), ignore_index=0)
+
+
+def _worker(rank, port, bucket_mb, zero_mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    from mtts.dp import GradAllReduce
+    p = _model()
+    params = list(p.values())
+    tok, text, z, mask = _batch()
+    sl = slice(rank * SHARD, (rank + 1) * SHARD)
+    dp = GradAllReduce(params, bucket_mb=bucket_mb)
+    opt = torch.optim.Adam(params, lr=1e-3)
+    for _ in range(2):  # twice: bucket state and gradient views must reset between steps
+        if zero_mode == "dp":
+            dp.zero_grad()
+        else:
+            opt.zero_grad(set_to_none=True)
+        _loss(p, tok[sl], text[sl], z[sl], mask[sl]).backward()
         dp.finish()
-    # numpy copies travel by value: a torch tensor would go through shared memory
-    # that can vanish when this process exits before the parent reads it
-    q.put((rank, {n: p.grad.detach().numpy().copy() for n, p in m.named_parameters()}, len(dp.buckets)))
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+    # numpy copies travel by value (no shared memory that dies with this process)
+    q.put((rank, {k: (v.grad.detach().numpy().copy(), v.detach().numpy().copy()) for k, v in p.items()},
+           len(dp.buckets)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_mb", [1e-3, 128.0])
-def test_grad_allreduce_gloo_world2(bucket_mb):
-    world = 2
+@pytest.mark.parametrize("bucket_mb,zero_mode", [(1e-3, "dp"), (128.0, "dp"), (1e-2, "set_to_none")])
+def test_decoder_grad_allreduce_gloo_world2(bucket_mb, zero_mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    torch.manual_seed(0)
-    m = Toy()
-    g = torch.Generator().manual_seed(100)
-    x = torch.randn(world * 6, 16, generator=g)
-    # mean over ranks of per-shard mean losses == gradient of the average
-    sum(m(x[r * 6:(r + 1) * 6]).square().mean() for r in range(world)).div(world).backward()
-    for rank, grads, nb in res:
+    procs = [ctx.Process(target=_worker, args=(r, port, bucket_mb, zero_mode, q)) for r in range(WORLD)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=300) for _ in range(WORLD)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    # single process: mean over ranks of the per-shard losses (each rank's CE
+    # averages over its own non-ignored tokens, so this is what DP computes)
+    p = _model()
+    params = list(p.values())
+    tok, text, z, mask = _batch()
+    opt = torch.optim.Adam(params, lr=1e-3)
+    for _ in range(2):
+        opt.zero_grad(set_to_none=True)
+        sum(_loss(p, tok[r * SHARD:(r + 1) * SHARD], text[r * SHARD:(r + 1) * SHARD], z[r * SHARD:(r + 1) * SHARD],
+                  mask[r * SHARD:(r + 1) * SHARD]) for r in range(WORLD)).div(WORLD).backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+    for rank, got, nb in res:
         if bucket_mb < 1:
-            assert nb > 1
-        for n, p in m.named_parameters():
-            ref = p.grad if p.grad is not None else torch.zeros_like(p)
-            torch.testing.assert_close(torch.from_numpy(grads[n]), ref, rtol=1e-5, atol=1e-6)
+            assert nb > 1, "small buckets must split the flat buffer"
+        for k, v in p.items():
+            g, w = got[k]
+            ref_g = v.grad if v.grad is not None else torch.zeros_like(v)
+            torch.testing.assert_close(torch.from_numpy(g), ref_g, rtol=1e-9, atol=1e-12, msg=f"grad {k}")
+            torch.testing.assert_close(torch.from_numpy(w), v.detach(), rtol=1e-9, atol=1e-12, msg=f"param {k}")

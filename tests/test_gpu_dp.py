@@ -1,0 +1,107 @@
+"""Batch data parallelism of the REAL training step on the GPU: two ranks
+(spawned processes) share cuda:0 through the gloo backend (RCCL needs one GPU
+per rank; the all-reduce code path in mtts/dp.py is backend-independent),
+each runs the HIP decoder (2 layers) on its batch shard, GradAllReduce
+averages the gradients during the backward, FusedClipAdam (mtts_clip_adam:
+clip_grad_norm_(1.0) + Adam, train.py:232-235) steps.  After 2 steps every
+rank's parameters equal a single process stepping on the mean of the
+per-shard losses (fp32 1e-5 relative; the only difference is the order of
+the cross-shard gradient sum)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+WORLD, SHARD, T, TT, D = 2, 2, 64, 12, 64
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup():
+    import mamba_decoder
+    from mtts.optim import FusedClipAdam
+    torch.manual_seed(0)
+    m = mamba_decoder.MambaTTSDecoder(10, d_model=D, n_layers=2, n_heads=4, d_ff=128, d_style=16,
+                                      max_len=128).to("cuda")
+    g = torch.Generator().manual_seed(7)
+    tok = torch.randint(0, 10, (WORLD * SHARD, T), generator=g).cuda()
+    text = torch.randn(WORLD * SHARD, TT, D, generator=g).cuda()
+    z = torch.randn(WORLD * SHARD, 16, generator=g).cuda()
+    opt = FusedClipAdam(list(m.parameters()), lr=1e-3, max_grad_norm=1.0)
+    return m, opt, tok, text, z
+
+
+def _loss(m, tok, text, z):
+    logits = m(tok, text, z)
+    return torch.nn.functional.cross_entropy(logits.float().reshape(-1, 10), tok.reshape(-1), ignore_index=0)
+
+
+def _worker(rank, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mamba-tts-project_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    from mtts.dp import GradAllReduce
+    m, opt, tok, text, z = _setup()
+    dp = GradAllReduce(list(m.parameters()), bucket_mb=0.05)
+    sl = slice(rank * SHARD, (rank + 1) * SHARD)
+    grads = None
+    for _ in range(2):
+        dp.zero_grad()
+        _loss(m, tok[sl], text[sl], z[sl]).backward()
+        dp.finish()
+        if grads is None:
+            grads = {n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters()}
+        opt.step()
+    torch.cuda.synchronize()
+    q.put((rank, {n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()}, grads, len(dp.buckets)))
+    dist.destroy_process_group()
+
+
+def test_decoder_dp_world2_fused_adam_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, opt, tok, text, z = _setup()
+    ref_grads = None
+    for _ in range(2):
+        opt.zero_grad(set_to_none=True)
+        sum(_loss(m, tok[r * SHARD:(r + 1) * SHARD], text[r * SHARD:(r + 1) * SHARD], z[r * SHARD:(r + 1) * SHARD])
+            for r in range(WORLD)).div(WORLD).backward()
+        if ref_grads is None:
+            ref_grads = {n: p.grad.detach().cpu() for n, p in m.named_parameters()}
+        opt.step()
+    lr = 1e-3
+    for rank, got, grads, nb in res:
+        assert nb > 1
+        for n, p in m.named_parameters():
+            g_ref = ref_grads[n]
+            g_err = (torch.from_numpy(grads[n]) - g_ref).abs().max().item()
+            assert g_err <= 1e-5 * max(g_ref.abs().max().item(), 1e-6), f"rank {rank} grad {n}: {g_err:.3e}"
+            ref = p.detach().cpu()
+            err = (torch.from_numpy(got[n]) - ref).abs()
+            # Adam normalises an update to ~lr whatever the gradient's size: an
+            # element whose gradient is at rounding level may take the other
+            # sign on one side (<= 2 lr per step); every other element agrees
+            assert err.max().item() <= 4 * lr, f"rank {rank} {n}: {err.max().item():.3e}"
+            assert (err > 1e-5).float().mean().item() <= 1e-3, f"rank {rank} {n}: too many differing elements"
