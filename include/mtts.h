@@ -438,6 +438,52 @@ typedef struct {
 
 int mtts_gemm_rows(const MttsRowsArgs* a, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Training-path GEMM (replaces the nn.Linear / Mamba in_proj, x_proj,
+ * dt_proj, out_proj / MHA in/out projection / FFN matmuls of
+ * mamba_decoder.py:29-43 as applied at :61-88, forward and backward).
+ * bf16 operands, fp32 accumulation on v_mfma_f32_16x16x32_bf16.
+ *   layout NT: C[m,n] = A[m,k] . B[n,k]^T  (A, B k-contiguous; row strides
+ *              lda, ldb): forward x W^T, data gradient dy (W^T)^T
+ *   layout TN: C[m,n] = A[k,m]^T . B[k,n]  (A, B m/n-contiguous): weight
+ *              gradient dy^T x; fp32 out, no epilogue, optional split-K
+ *              (splits > 1: fp32 partial slabs in `workspace`,
+ *              mtts_gemm_workspace() bytes, summed in fixed order)
+ * out_dtype 0 = fp32 (C = AB + beta C), 1 = bf16 with epilogues:
+ *   BIAS  : + bias[n] (bias_dtype 0 fp32 / 1 bf16)
+ *   GELU  : aux[m,n] = bf16(AB (+bias)) (pre-activation, for the backward),
+ *           C = bf16(gelu(aux))  (exact erf; F.gelu on the bf16 value)
+ *   DGELU : C = bf16(bf16(AB) * gelu'(aux[m,n]))  (GELU backward fused into
+ *           the data gradient of the layer that consumes the activation)
+ * Requirements: k % (64 * splits) == 0, n % 8 == 0 (TN: m % 8 == 0 too),
+ * A/B 16-byte aligned with row strides a multiple of 8 elements, C 16-byte
+ * aligned with ldc % 4 == 0.
+ * ------------------------------------------------------------------------ */
+#define MTTS_GEMM_NT 0
+#define MTTS_GEMM_TN 1
+#define MTTS_GEMM_EPI_BIAS 1
+#define MTTS_GEMM_EPI_GELU 2
+#define MTTS_GEMM_EPI_DGELU 4
+typedef struct {
+  int m, n, k;
+  int layout;                /* MTTS_GEMM_NT / MTTS_GEMM_TN */
+  int splits;                /* TN split-K factor (1 = none) */
+  int epilogue;              /* MTTS_GEMM_EPI_* flags (bf16 out only) */
+  int out_dtype;             /* 0 fp32, 1 bf16 */
+  int bias_dtype;            /* 0 fp32, 1 bf16 */
+  int64_t lda, ldb, ldc, ld_aux;
+  const void* a;
+  const void* b;
+  void* c;
+  const void* bias;          /* optional */
+  void* aux;                 /* GELU / DGELU pre-activation (bf16 m x n) */
+  void* workspace;           /* split-K slabs */
+  float beta;                /* fp32 out: C = AB + beta C */
+} MttsGemmArgs;
+
+int64_t mtts_gemm_workspace(const MttsGemmArgs* a);
+int mtts_gemm(const MttsGemmArgs* a, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from mtts.mamba import Mamba
 from mtts.attention import CrossAttention
 from mtts import ops
-from mtts.linear import cast_scope, linear
+from mtts.linear import cast_scope, ffn, linear
 from mtts.decode import DecodeEngine
 from mtts.embed import embed_sum
 
@@ -85,8 +85,7 @@ class MambaTTSDecoderLayer(nn.Module):
         h, x = ops.layer_norm(attn_out, self.norm_ff.weight, self.norm_ff.bias, self.norm_ff.eps, res=x,
                               gamma=gamma, beta=beta, rows_per_group=T)
         f0, f2 = self.ff[0], self.ff[2]
-        ff_h = F.gelu(linear(h, f0.weight, f0.bias))
-        ff_out = linear(ff_h, f2.weight, f2.bias)
+        ff_out = ffn(h, f0.weight, f0.bias, f2.weight, f2.bias)             # :88 (gelu(ff0) -> ff2)
         return x, ff_out, new_state
 
 

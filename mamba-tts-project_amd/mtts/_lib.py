@@ -76,6 +76,12 @@ class RowsArgs(C.Structure):
                 ("res", vp), ("ld_res", i64)]
 
 
+class GemmArgs(C.Structure):
+    _fields_ = [("m", i32), ("n", i32), ("k", i32), ("layout", i32), ("splits", i32), ("epilogue", i32),
+                ("out_dtype", i32), ("bias_dtype", i32), ("lda", i64), ("ldb", i64), ("ldc", i64), ("ld_aux", i64),
+                ("a", vp), ("b", vp), ("c", vp), ("bias", vp), ("aux", vp), ("workspace", vp), ("beta", f32)]
+
+
 class LNArgs(C.Structure):
     _fields_ = [("rows", i32), ("cols", i32), ("dtype", i32), ("rows_per_group", i32), ("eps", f32),
                 ("x_rs", i64), ("res_rs", i64), ("xsum_rs", i64), ("y_rs", i64), ("gb_rs", i64),
@@ -125,6 +131,8 @@ _SIGS = {
     "mtts_selective_state_update": ([C.POINTER(StateUpdateArgs), vp], i32),
     "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
     "mtts_gemm_rows": ([C.POINTER(RowsArgs), vp], i32),
+    "mtts_gemm_workspace": ([C.POINTER(GemmArgs)], i64),
+    "mtts_gemm": ([C.POINTER(GemmArgs), vp], i32),
     "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),
     "mtts_layernorm_bwd": ([C.POINTER(LNBwdArgs), vp], i32),
     "mtts_colsum_workspace": ([i32, i32, i32], i64),

@@ -1,0 +1,523 @@
+// bf16 MFMA GEMM for the decoder's training projections (gfx950).
+//
+// C[M,N] = epilogue( A·B ) with fp32 accumulation, two operand layouts:
+//   NT (fwd y = x·Wᵀ, dgrad dx = dy·W on the cast kernel's Wᵀ copy):
+//       A[M,K], B[N,K], both k-contiguous;
+//   TN (wgrad dW = dyᵀ·x over the token axis):
+//       A[K,M], B[K,N], both m/n-contiguous, fp32 out (master grads), split-K.
+// Reference sites: the nn.Linear / in_proj / x_proj / dt_proj / out_proj / MHA
+// projections of /root/reference/mamba_decoder.py:29-43 (Mamba, MHA, FFN)
+// applied at :61-88.
+//
+// Structure (one 256x256 output tile per 512-thread workgroup, 8 waves as
+// 2 (M) x 4 (N), 128x64 per wave, v_mfma_f32_16x16x32_bf16):
+//  * a 64-deep K-tile of A and B is 64 KiB of LDS, split into four 16 KiB
+//    REGIONS by the quadrant that reads them: A0/A1 = the A rows each wave
+//    reads as its first/second 64-row half, B0/B1 = the B rows it reads as
+//    its first/second 32-column half.  Two K-tile buffers = 128 KiB, ONE
+//    __shared__ array.
+//  * a K-tile is four PHASES, one 64x32 quadrant x K=64 per wave each
+//    (16 MFMAs): (A0,B0) (A0,B1) (A1,B1) (A1,B0); A frags are read at
+//    phases 0 and 2, B frags at phases 0 and 1 and kept in registers, so each
+//    region's last LDS read is in phase 0, 0, 1 or 2.
+//  * every phase stages exactly one region (2 LDS-DMA global_load_lds_dwordx4
+//    per thread, 16 KiB per workgroup) of a LATER K-tile into a region whose
+//    last read lies at least one barrier back: phase 0 stages A1 of tile t+1,
+//    phases 1-3 stage A0, B0, B1 of tile t+2.  A region is first read 6 or 7
+//    phases after it was staged, so each phase ends with s_waitcnt vmcnt(10)
+//    (the 5 younger phases' 2 DMAs each stay in flight across the barrier) and
+//    one raw s_barrier; the last two K-tiles wait vmcnt(0).
+//  * the LDS images are lane-linear (the DMA writes base + 16*lane); bank
+//    swizzles move to the SOURCE address (k-major: 16-B chunk c of row r at
+//    c ^ ((r>>1)&7), conflict-free ds_read_b128 for 16 consecutive rows;
+//    m/n-major: 32-B granule g of k-row r at g ^ ((r&3) | ((r>>3)&1)<<2),
+//    conflict-free ds_read_b64_tr_b16 over a 32-lane half).
+//  * MFMA operands are swapped (B fragment first) so a lane's accumulator
+//    holds 4 consecutive output COLUMNS of one row: 8-byte (bf16) / 16-byte
+//    (fp32) row-major stores.
+//  * epilogues on the fp32 accumulator: + bias; GELU (exact erf) writing the
+//    pre-activation too (for the backward); GELU backward (dgrad times
+//    gelu'(pre-activation)); fp32 out with beta·C accumulate (wgrad).
+#include "common.h"
+
+#include <type_traits>
+
+namespace mtts {
+namespace {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) s16x8 lds_s16x8;
+
+constexpr int kThreads = 512;
+constexpr int kTile = 256;        // BM = BN
+constexpr int kBK = 64;
+constexpr int kRegion = 16384;    // bytes
+constexpr int kBuf = 4 * kRegion; // one K-tile: A0 A1 B0 B1
+constexpr int kLds = 2 * kBuf;    // 128 KiB
+
+enum { R_A0 = 0, R_A1 = 1, R_B0 = 2, R_B1 = 3 };
+
+struct GemmParams {
+  const bf16_t* a;
+  const bf16_t* b;
+  void* c;
+  const void* bias;
+  void* aux;
+  int64_t lda, ldb, ldc, ld_aux;
+  int64_t split_stride;  // elements between split-K output slabs (fp32 out)
+  int m, n, k;           // k: per-split K range length (multiple of 64)
+  int tiles_m, tiles_n, splits;
+  int group;             // tile rows per L2 group
+  int epi;               // MTTS_GEMM_EPI_*
+  int bias_bf16;
+  float beta;
+};
+
+// region-local row/column (0..127) -> tile row/column
+__device__ __forceinline__ int a_map(int rr, int s) { return (rr >> 6) * 128 + s * 64 + (rr & 63); }
+__device__ __forceinline__ int b_map(int rr, int s) { return (rr >> 5) * 64 + s * 32 + (rr & 31); }
+template <bool IS_A>
+__device__ __forceinline__ int rmap(int rr, int s) { return IS_A ? a_map(rr, s) : b_map(rr, s); }
+
+// 16-byte LDS-DMA with a 32-bit per-lane offset from a wave-uniform base;
+// invisible to the compiler's wait insertion (every consumer waits by hand).
+__device__ __forceinline__ void glds16(const void* base, uint32_t voff, uint32_t lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "s"(lds_base)
+               : "memory", "m0");
+#endif
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+#endif
+}
+// lgkmcnt(0) + s_barrier through the builtins (so the compiler's own wait
+// bookkeeping sees the LDS reads retired: an inline-asm wait is invisible to
+// it and it re-waits on the NEXT phase's prefetch reads), then a compiler
+// fence so no LDS access moves across.
+__device__ __forceinline__ void barrier() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0); vmcnt / expcnt untouched
+#ifndef MTTS_GEMM_DIAG_NOBAR
+  __builtin_amdgcn_s_barrier();
+#endif
+  asm volatile("" ::: "memory");
+#endif
+}
+
+__device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+// Per-thread source offsets (elements) of one region's two DMAs, relative to
+// the operand's tile origin; k-major: rows of the tile, m/n-major: k-rows.
+template <bool KMAJ, bool IS_A>
+struct Loader {
+  uint32_t off[2][2];  // [sub s][dma i], in bytes from the K-tile origin
+
+  __device__ void init(int tid, int row0, int nrows, int64_t ld) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if constexpr (KMAJ) {
+          const int rr = i * 64 + (tid >> 3), p = tid & 7;
+          const int c = p ^ ((rr >> 1) & 7);
+          int row = row0 + rmap<IS_A>(rr, s);
+          row = row < nrows ? row : nrows - 1;
+          off[s][i] = (uint32_t)((row * ld + c * 8) * 2);
+        } else {
+          const int kr = i * 32 + (tid >> 4), p = tid & 15;
+          const int f = (kr & 3) | (((kr >> 3) & 1) << 2);
+          const int c = p ^ (f << 1);                   // logical 16-B chunk (8 columns)
+          int col = row0 + rmap<IS_A>(c * 8, s);
+          col = col + 8 <= nrows ? col : ((nrows - 8) & ~7);
+          off[s][i] = (uint32_t)((kr * ld + col) * 2);
+        }
+      }
+  }
+  // stage sub-part s of K-tile `kt` (origin pointer for that K-tile) into region `lds_region`
+  __device__ __forceinline__ void stage1(const char* ktile, int s, uint32_t lds_region, int wave, int i) const {
+    glds16(ktile, off[s][i], lds_region + i * 8192 + wave * 1024);
+  }
+};
+
+// fragment for (region byte base, 16-row block at region-local row rb, k-step ks)
+template <bool KMAJ>
+__device__ __forceinline__ s16x8 frag(const char* region, int rb, int ks, int lane) {
+#ifdef MTTS_GEMM_DIAG_NOREAD
+  s16x8 z{};   // timing-only: no LDS reads
+  asm volatile("" : "+v"(z));
+  return z;
+#endif
+  if constexpr (KMAJ) {
+    const int rr = rb + (lane & 15);
+    const int c = (ks * 4 + (lane >> 4)) ^ ((rr >> 1) & 7);
+    return *(const lds_s16x8*)(region + rr * 128 + c * 16);
+  } else {
+    // two ds_read_b64_tr_b16: k-rows ks*32 + 8g + 4h + q, columns rb + 4p .. +3
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = rb + 4 * p;
+    s16x4 r[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kr = ks * 32 + 8 * g + 4 * h + q;
+      const int f = (kr & 3) | (((kr >> 3) & 1) << 2);
+      const int chunk = (col >> 3) ^ (f << 1);
+      r[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(region + kr * 256 + chunk * 16 + (col & 7) * 2));
+    }
+    return s16x8{r[0][0], r[0][1], r[0][2], r[0][3], r[1][0], r[1][1], r[1][2], r[1][3]};
+  }
+}
+
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // XCD-aware tile order: consecutive ids (one XCD's share) walk N fastest
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int split = id / tiles;
+  const int tile = id % tiles;
+  // groups of `group` tile rows walked column by column: the ~32 tiles one
+  // XCD runs at a time share a few A and B panels in its L2
+  const int gsz = p.group * p.tiles_n;
+  const int g0 = (tile / gsz) * p.group;
+  const int gr = min(p.group, p.tiles_m - g0);
+  const int tm = g0 + (tile % gsz) % gr, tn = (tile % gsz) / gr;
+#ifdef MTTS_GEMM_DIAG_SAMETILE
+  const int m0 = 0, n0 = 0;   // timing-only: every block streams tile (0, 0) (L2-resident)
+#else
+  const int m0 = tm * kTile, n0 = tn * kTile;
+#endif
+
+  // K-tile origins (bytes) for this split
+  const int64_t k0 = (int64_t)split * p.k;
+  const char* abase;
+  const char* bbase;
+  int64_t astep, bstep;  // bytes per K-tile
+  if constexpr (AK) { abase = (const char*)(p.a + k0); astep = kBK * 2; }
+  else { abase = (const char*)(p.a + k0 * p.lda); astep = kBK * p.lda * 2; }
+  if constexpr (BKM) { bbase = (const char*)(p.b + k0); bstep = kBK * 2; }
+  else { bbase = (const char*)(p.b + k0 * p.ldb); bstep = kBK * p.ldb * 2; }
+
+  Loader<AK, true> la;
+  Loader<BKM, false> lb;
+  la.init(tid, m0, p.m, p.lda);
+  lb.init(tid, n0, p.n, p.ldb);
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  auto region_addr = [&](int buf, int r) -> uint32_t { return lds0 + buf * kBuf + r * kRegion; };
+  auto stage1 = [&](int kt, int r, int i) {
+#ifdef MTTS_GEMM_DIAG_NODMA
+    if (kt >= 0) return;   // timing-only: no operand traffic
+#endif
+    const int buf = kt & 1;
+    if (r == R_A0 || r == R_A1) la.stage1(abase + kt * astep, r - R_A0, region_addr(buf, r), wave, i);
+    else lb.stage1(bbase + kt * bstep, r - R_B0, region_addr(buf, r), wave, i);
+  };
+  auto stage = [&](int kt, int r) { stage1(kt, r, 0); stage1(kt, r, 1); };
+
+  const int nk = p.k / kBK;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Global phase P = 4t + q.  Tile j's regions are staged at phases
+  // A0: 4j-9, B0: 4j-8, B1: 4j-7, A1: 4j-6 and first (and only) read — as
+  // the next phase's fragments, prefetched — at A0: 4j-2, B0: 4j-1, B1: 4j,
+  // A1: 4j+1: seven phases later for every region.  So the end of phase P
+  // retires what was staged at P-6 (read from P+1 on): vmcnt = 2 x the
+  // regions staged in phases P-5..P.  The last staged phase is 4nk-10.
+  const int lv = 4 * nk - 10;
+  auto wait_end = [&](int P) {
+    int n = (P < lv ? P : lv) - P + 6;   // regions staged in P-5..P
+    n = n < 0 ? 0 : n;
+    switch (n) {
+      case 6: wait_vm<12>(); break;
+      case 5: wait_vm<10>(); break;
+      case 4: wait_vm<8>(); break;
+      case 3: wait_vm<6>(); break;
+      case 2: wait_vm<4>(); break;
+      case 1: wait_vm<2>(); break;
+      default: wait_vm<0>(); break;
+    }
+    barrier();
+  };
+  // prologue: phases -9 .. -1
+  // (A0(2), staged at phase -1 into tile 0's buffer, waits for the reads of
+  // A0(0) and one barrier)
+  stage(0, R_A0); stage(0, R_B0); stage(0, R_B1); stage(0, R_A1);
+  if (nk > 1) { stage(1, R_A0); stage(1, R_B0); stage(1, R_B1); stage(1, R_A1); }
+  if (nk > 1) wait_vm<10>(); else wait_vm<2>();   // A0(0) B0(0) B1(0) landed
+  barrier();
+
+  const char* lbase = lds;
+  s16x8 a0[2][4], a1[2][4], b0[2][2], b1[2][2];  // [ks][block]
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) a0[ks][mb] = frag<AK>(lbase + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) b0[ks][nb] = frag<BKM>(lbase + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
+  }
+  barrier();
+  if (nk > 2) stage(2, R_A0);
+
+  // steady K-tiles (every phase stages; constant waits), then the tail.
+  // Inside a phase the two DMAs sit between MFMA groups (pinned by
+  // sched_barrier): a DMA holds its wave's issue for ~60-180 cycles, during
+  // which the SIMD's other wave keeps the matrix pipe busy.
+#define MFMA4(BF, AF, MO, NO, KS, MP)                                                         \
+  _Pragma("unroll") for (int mb_ = 2 * (MP); mb_ < 2 * (MP) + 2; ++mb_)                      \
+  _Pragma("unroll") for (int nb_ = 0; nb_ < 2; ++nb_)                                        \
+      acc[(MO) + mb_][(NO) + nb_] = mfma(BF[KS][nb_], AF[KS][mb_], acc[(MO) + mb_][(NO) + nb_]);
+#define PHASE_MFMA(BF, AF, MO, NO, DO_STAGE, KT, R)                                           \
+  __builtin_amdgcn_s_setprio(1);                                                              \
+  MFMA4(BF, AF, MO, NO, 0, 0)                                                                 \
+  __builtin_amdgcn_sched_barrier(0);                                                          \
+  if (DO_STAGE) stage1(KT, R, 0);                                                             \
+  __builtin_amdgcn_sched_barrier(0);                                                          \
+  MFMA4(BF, AF, MO, NO, 0, 1)                                                                 \
+  __builtin_amdgcn_sched_barrier(0);                                                          \
+  if (DO_STAGE) stage1(KT, R, 1);                                                             \
+  __builtin_amdgcn_sched_barrier(0);                                                          \
+  MFMA4(BF, AF, MO, NO, 1, 0)                                                                 \
+  MFMA4(BF, AF, MO, NO, 1, 1)                                                                 \
+  __builtin_amdgcn_s_setprio(0);
+  auto ktile = [&](int t, auto steady) {
+    constexpr bool ST = decltype(steady)::value;
+    const char* bufp = lbase + (t & 1) * kBuf;
+    const char* nxtp = lbase + ((t + 1) & 1) * kBuf;
+    const int P = 4 * t;
+    const bool more = ST || t + 1 < nk;
+    // ---- phase 0: A0 x B0 | prefetch B1(t) | stage B0(t+2)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b1[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
+    PHASE_MFMA(b0, a0, 0, 0, (ST || P <= lv), t + 2, R_B0)
+    if constexpr (ST) wait_vm<12>(), barrier(); else wait_end(P);
+    // ---- phase 1: A0 x B1 | prefetch A1(t) | stage B1(t+2)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) a1[ks][mb] = frag<AK>(bufp + R_A1 * kRegion, wr * 64 + mb * 16, ks, lane);
+    PHASE_MFMA(b1, a0, 0, 2, (ST || P + 1 <= lv), t + 2, R_B1)
+    if constexpr (ST) wait_vm<12>(), barrier(); else wait_end(P + 1);
+    // ---- phase 2: A1 x B1 | prefetch A0(t+1) | stage A1(t+2)
+    if (more) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) a0[ks][mb] = frag<AK>(nxtp + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
+    }
+    PHASE_MFMA(b1, a1, 4, 2, (ST || P + 2 <= lv), t + 2, R_A1)
+    if constexpr (ST) wait_vm<12>(), barrier(); else wait_end(P + 2);
+    // ---- phase 3: A1 x B0 | prefetch B0(t+1) | stage A0(t+3)
+    s16x8 b0n[2][2];
+    if (more) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) b0n[ks][nb] = frag<BKM>(nxtp + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
+    }
+    PHASE_MFMA(b0, a1, 4, 0, (ST || P + 3 <= lv), t + 3, R_A0)
+    if constexpr (ST) wait_vm<12>(), barrier(); else wait_end(P + 3);
+    if (more) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) b0[ks][nb] = b0n[ks][nb];
+    }
+  };
+#undef PHASE_MFMA
+#undef MFMA4
+  const int nsteady = nk > 3 ? nk - 3 : 0;
+  for (int t = 0; t < nsteady; ++t) ktile(t, std::true_type{});
+  for (int t = nsteady; t < nk; ++t) ktile(t, std::false_type{});
+
+  // ---- epilogue: lane holds rows m = .. + (lane&15), columns n = .. + 4*(lane>>4) + j
+  const int rl = lane & 15, cl = 4 * (lane >> 4);
+#pragma unroll
+  for (int MB = 0; MB < 8; ++MB) {
+    const int row = m0 + wr * 128 + MB * 16 + rl;
+    if (row >= p.m) continue;
+#pragma unroll
+    for (int NB = 0; NB < 4; ++NB) {
+      const int col = n0 + wc * 64 + NB * 16 + cl;
+      if (col >= p.n) continue;   // n % 4 == 0 (host check): a lane's 4 columns are all in or all out
+      f32x4 v = acc[MB][NB];
+      if constexpr (OUT_F32) {
+        float* cp = (float*)p.c + (int64_t)split * p.split_stride + (int64_t)row * p.ldc + col;
+        if (p.beta != 0.f) {
+          const f32x4 o = *(const f32x4*)cp;
+          v = v + p.beta * o;
+        }
+        *(f32x4*)cp = v;
+      } else {
+        if (EPI & MTTS_GEMM_EPI_BIAS) {
+          float bb[4];
+          if (p.bias_bf16) {
+            const uint2 raw = *(const uint2*)((const bf16_t*)p.bias + col);
+            bb[0] = __uint_as_float(raw.x << 16); bb[1] = __uint_as_float(raw.x & 0xffff0000u);
+            bb[2] = __uint_as_float(raw.y << 16); bb[3] = __uint_as_float(raw.y & 0xffff0000u);
+          } else {
+            const f32x4 b4 = *(const f32x4*)((const float*)p.bias + col);
+            bb[0] = b4[0]; bb[1] = b4[1]; bb[2] = b4[2]; bb[3] = b4[3];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += bb[j];
+        }
+        bf16_t o[4];
+        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
+          bf16_t hpre[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hpre[j] = f2bf(v[j]);
+            o[j] = f2bf(gelu_f(bf2f(hpre[j])));
+          }
+          bf16_t* ap = (bf16_t*)p.aux + (int64_t)row * p.ld_aux + col;
+          *(uint2*)ap = make_uint2(hpre[0] | ((uint32_t)hpre[1] << 16), hpre[2] | ((uint32_t)hpre[3] << 16));
+        } else if constexpr ((EPI & MTTS_GEMM_EPI_DGELU) != 0) {
+          const bf16_t* ap = (const bf16_t*)p.aux + (int64_t)row * p.ld_aux + col;
+          const uint2 raw = *(const uint2*)ap;
+          const float h[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
+                              __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(h[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+        }
+        bf16_t* cp = (bf16_t*)p.c + (int64_t)row * p.ldc + col;
+        *(uint2*)cp = make_uint2(o[0] | ((uint32_t)o[1] << 16), o[2] | ((uint32_t)o[3] << 16));
+      }
+    }
+  }
+}
+
+// out[i] = beta*out[i] + sum_s slab[s][i] (fixed order); rows x cols with row strides
+__global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ slabs, int64_t sstride, int splits,
+                                                           int rows, int cols, int64_t lds_, float* out, int64_t ldo,
+                                                           float beta) {
+  const int c4 = cols / 4;
+  const int64_t total = (int64_t)rows * c4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / c4), c = (int)(i % c4) * 4;
+    f32x4 s = *(const f32x4*)(slabs + (int64_t)r * lds_ + c);
+    for (int k = 1; k < splits; ++k) s += *(const f32x4*)(slabs + k * sstride + (int64_t)r * lds_ + c);
+    float* op = out + (int64_t)r * ldo + c;
+    if (beta != 0.f) s += beta * *(const f32x4*)op;
+    *(f32x4*)op = s;
+  }
+}
+
+template <bool AK, bool BKM, int EPI, bool F32>
+void launch(const GemmParams& p, int nwg, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
+}
+
+}  // namespace
+}  // namespace mtts
+
+using namespace mtts;
+
+extern "C" int64_t mtts_gemm_workspace(const MttsGemmArgs* a) {
+  if (!a || a->layout != MTTS_GEMM_TN || a->splits <= 1) return 0;
+  return (int64_t)a->splits * a->m * a->n * 4;
+}
+
+extern "C" int mtts_gemm(const MttsGemmArgs* a, void* stream) {
+  MTTS_CHECK(a && a->a && a->b && a->c, "gemm: null pointer");
+  const int M = a->m, N = a->n, K = a->k;
+  MTTS_CHECK(M > 0 && N > 0 && K > 0, "gemm: m=%d n=%d k=%d must be positive", M, N, K);
+  MTTS_CHECK(a->layout == MTTS_GEMM_NT || a->layout == MTTS_GEMM_TN, "gemm: layout must be NT (0) or TN (1)");
+  const bool nt = a->layout == MTTS_GEMM_NT;
+  const int splits = a->splits > 0 ? a->splits : 1;
+  MTTS_CHECK(K % (kBK * splits) == 0, "gemm: k=%d must be a multiple of 64*splits (splits=%d)", K, splits);
+  MTTS_CHECK(N % 8 == 0, "gemm: n=%d must be a multiple of 8", N);
+  MTTS_CHECK(nt || M % 8 == 0, "gemm: TN needs m=%d a multiple of 8", M);
+  MTTS_CHECK(((uintptr_t)a->a | (uintptr_t)a->b) % 16 == 0 && a->lda % 8 == 0 && a->ldb % 8 == 0,
+             "gemm: A / B must be 16-byte aligned with row strides a multiple of 8 elements");
+  MTTS_CHECK(a->ldc % 4 == 0 && (uintptr_t)a->c % 16 == 0, "gemm: C must be 16-byte aligned, ldc a multiple of 4");
+  MTTS_CHECK(nt ? (a->lda >= K && a->ldb >= K) : (a->lda >= M && a->ldb >= N), "gemm: leading dimension too small");
+  // 32-bit DMA offsets from the K-tile origin
+  const int64_t aspan = nt ? (int64_t)(M - 1) * a->lda + K : (int64_t)(kBK - 1) * a->lda + M;
+  const int64_t bspan = nt ? (int64_t)(N - 1) * a->ldb + K : (int64_t)(kBK - 1) * a->ldb + N;
+  MTTS_CHECK(aspan * 2 < (1ll << 32) && bspan * 2 < (1ll << 32), "gemm: operand span exceeds 4 GiB");
+  const int epi = a->epilogue;
+  const bool f32out = a->out_dtype == 0;
+  MTTS_CHECK(a->out_dtype == 0 || a->out_dtype == 1, "gemm: out_dtype must be 0 (f32) or 1 (bf16)");
+  MTTS_CHECK(!f32out || epi == 0, "gemm: epilogues apply to bf16 output only");
+  MTTS_CHECK(f32out || splits == 1, "gemm: split-K needs fp32 output");
+  MTTS_CHECK(!(epi & MTTS_GEMM_EPI_BIAS) || a->bias, "gemm: bias epilogue without bias");
+  MTTS_CHECK(!(epi & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) || (a->aux && a->ld_aux % 4 == 0),
+             "gemm: GELU epilogues need aux (ld_aux multiple of 4)");
+  MTTS_CHECK((epi & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) != (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU),
+             "gemm: GELU and DGELU are exclusive");
+  MTTS_CHECK(nt || (epi == 0 && f32out), "gemm: TN (weight gradient) runs fp32 out, no epilogue");
+  MTTS_CHECK(splits == 1 || a->workspace, "gemm: split-K needs the workspace (mtts_gemm_workspace bytes)");
+
+  GemmParams p{};
+  p.a = (const bf16_t*)a->a; p.b = (const bf16_t*)a->b;
+  p.bias = a->bias; p.aux = a->aux; p.bias_bf16 = a->bias_dtype == 1;
+  p.lda = a->lda; p.ldb = a->ldb; p.ld_aux = a->ld_aux;
+  p.m = M; p.n = N; p.k = K / splits;
+  p.tiles_m = (M + kTile - 1) / kTile; p.tiles_n = (N + kTile - 1) / kTile;
+  p.splits = splits; p.epi = epi;
+  p.group = std::min(p.tiles_m, 4);
+  if (const char* e = getenv("MTTS_GEMM_GROUP")) p.group = std::max(1, std::min(p.tiles_m, atoi(e)));
+  if (splits > 1) {
+    p.c = a->workspace; p.ldc = N; p.split_stride = (int64_t)M * N; p.beta = 0.f;
+  } else {
+    p.c = a->c; p.ldc = a->ldc; p.split_stride = 0; p.beta = a->beta;
+  }
+  const int nwg = p.tiles_m * p.tiles_n * splits;
+  hipStream_t st = (hipStream_t)stream;
+  if (!nt) {
+    launch<false, false, 0, true>(p, nwg, st);
+  } else if (f32out) {
+    launch<true, true, 0, true>(p, nwg, st);
+  } else {
+    switch (epi) {
+      case 0: launch<true, true, 0, false>(p, nwg, st); break;
+      case MTTS_GEMM_EPI_BIAS: launch<true, true, MTTS_GEMM_EPI_BIAS, false>(p, nwg, st); break;
+      case MTTS_GEMM_EPI_GELU: launch<true, true, MTTS_GEMM_EPI_GELU, false>(p, nwg, st); break;
+      case MTTS_GEMM_EPI_BIAS | MTTS_GEMM_EPI_GELU:
+        launch<true, true, MTTS_GEMM_EPI_BIAS | MTTS_GEMM_EPI_GELU, false>(p, nwg, st); break;
+      case MTTS_GEMM_EPI_DGELU: launch<true, true, MTTS_GEMM_EPI_DGELU, false>(p, nwg, st); break;
+      default: MTTS_CHECK(false, "gemm: unsupported epilogue combination %d", epi);
+    }
+  }
+  MTTS_LAUNCH_CHECK("gemm");
+  if (splits > 1) {
+    const int64_t total = (int64_t)M * (N / 4);
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)a->workspace,
+                       (int64_t)M * N, splits, M, N, (int64_t)N, (float*)a->c, a->ldc, a->beta);
+    MTTS_LAUNCH_CHECK("gemm split reduce");
+  }
+  return MTTS_OK;
+}

@@ -1,0 +1,98 @@
+"""Hand-written bf16 MFMA GEMMs (csrc/gemm.hip, `mtts_gemm`) for the
+decoder's training projections (reference mamba_decoder.py:29-43, applied at
+:61-88): forward x·Wᵀ and data gradient dy·W in the NT layout (both operands
+k-contiguous; the data gradient reads the cast kernel's Wᵀ copy), weight
+gradient dyᵀ·x in the TN layout straight into the fp32 master gradient.
+
+Epilogues run on the fp32 accumulator: bias, GELU (writing the bf16
+pre-activation for the backward) and the GELU backward fused into the data
+gradient of the FFN's second projection.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+
+EPI_BIAS, EPI_GELU, EPI_DGELU = 1, 2, 4
+NT, TN = 0, 1
+TILE = 256
+ENABLED = True   # routing switch for in-process A/B timing (tools/gemm_step_ab.py)
+
+
+def _rowmajor(t):
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+
+
+def nt_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Shapes/layouts the NT kernel takes: bf16, k % 64 == 0, n % 8 == 0."""
+    return (ENABLED and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.is_cuda
+            and _rowmajor(a) and _rowmajor(b)
+            and a.shape[1] == b.shape[1] and a.shape[1] % 64 == 0 and b.shape[0] % 8 == 0 and a.shape[0] > 0)
+
+
+def tn_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return (ENABLED and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.is_cuda
+            and _rowmajor(a) and _rowmajor(b)
+            and a.shape[0] == b.shape[0] and a.shape[0] % 64 == 0 and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0)
+
+
+def mm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor = None, gelu_aux: torch.Tensor = None,
+          dgelu_aux: torch.Tensor = None, out: torch.Tensor = None) -> torch.Tensor:
+    """bf16 C[m,n] = a[m,k] · b[n,k]ᵀ (+bias) with an optional GELU epilogue
+    (gelu_aux receives the pre-activation, C = gelu of it) or GELU-backward
+    epilogue (C = bf16(AB) · gelu'(dgelu_aux))."""
+    m, k = a.shape
+    n = b.shape[0]
+    if out is None:
+        out = torch.empty(m, n, device=a.device, dtype=torch.bfloat16)
+    args = L.GemmArgs()
+    args.m, args.n, args.k, args.layout, args.splits, args.out_dtype = m, n, k, NT, 1, 1
+    epi = 0
+    if bias is not None:
+        epi |= EPI_BIAS
+        args.bias, args.bias_dtype = bias.data_ptr(), L.dtype_code(bias)
+    aux = gelu_aux if gelu_aux is not None else dgelu_aux
+    if gelu_aux is not None:
+        epi |= EPI_GELU
+    if dgelu_aux is not None:
+        epi |= EPI_DGELU
+    if aux is not None:
+        args.aux, args.ld_aux = aux.data_ptr(), aux.stride(0)
+    args.epilogue = epi
+    args.lda, args.ldb, args.ldc = a.stride(0), b.stride(0), out.stride(0)
+    args.a, args.b, args.c = a.data_ptr(), b.data_ptr(), out.data_ptr()
+    L.call("mtts_gemm", args)
+    return out
+
+
+def tn_splits(m: int, n: int, k: int) -> int:
+    """Split-K factor for the weight gradient: fill >= ~256 workgroups while
+    each split keeps >= 1024 of the reduction (C2: in_proj 4, out_proj / FFN
+    8, q / o projections 16; tools/bench_mgemm.py)."""
+    tiles = -(-m // TILE) * -(-n // TILE)
+    s = 1
+    while tiles * s < 256 and k % (64 * s * 2) == 0 and k // (s * 2) >= 1024:
+        s *= 2
+    return s
+
+
+def mm_tn(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, beta: float = 0.0,
+          splits: int = None) -> torch.Tensor:
+    """fp32 C[m,n] = a[k,m]ᵀ · b[k,n] (+ beta·C): the weight gradient dyᵀ·x."""
+    k, m = a.shape
+    n = b.shape[1]
+    if out is None:
+        out = torch.empty(m, n, device=a.device, dtype=torch.float32)
+    args = L.GemmArgs()
+    s = tn_splits(m, n, k) if splits is None else splits
+    args.m, args.n, args.k, args.layout, args.splits, args.out_dtype = m, n, k, TN, s, 0
+    args.lda, args.ldb, args.ldc = a.stride(0), b.stride(0), out.stride(0)
+    args.a, args.b, args.c = a.data_ptr(), b.data_ptr(), out.data_ptr()
+    args.beta = beta
+    ws = None
+    if s > 1:
+        ws = torch.empty(L.lib().mtts_gemm_workspace(args), device=a.device, dtype=torch.uint8)
+        args.workspace = ws.data_ptr()
+    L.call("mtts_gemm", args)
+    return out

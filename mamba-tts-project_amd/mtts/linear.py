@@ -26,6 +26,7 @@ import contextlib
 import torch
 
 from . import _lib as L
+from . import gemm as G
 
 _scope = {"token": 0, "depth": 0}
 _cast_plans = {}
@@ -147,12 +148,21 @@ def colsum(x2d: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     return out
 
 
+# weight gradients with both output dims >= this run on the hand-written TN
+# kernel (mtts_gemm, csrc/gemm.hip: 0.9-1.1 PF/s on the C2 shapes vs 0.6-0.83
+# for the split-K bmm below); the skinny x_proj / dt_proj ones stay on it
+HIP_WGRAD_MIN = 256
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4, out: torch.Tensor = None) -> torch.Tensor:
     """dW = dy^T @ x in fp32; dy (M, n), x (M, k) with the same dtype.
     `out` (n, k) fp32, possibly a row slice of a larger gradient, receives it."""
     M = dy.shape[0]
     if dy.dtype == torch.float32:
         return torch.mm(dy.t(), x, out=out) if out is not None else dy.t() @ x
+    if (dy.shape[1] >= HIP_WGRAD_MIN and x.shape[1] >= HIP_WGRAD_MIN and G.tn_ok(dy, x)
+            and (out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0))):
+        return G.mm_tn(dy, x, out=out)
     if splits > 1 and M % splits == 0 and M >= 2048:
         m = M // splits
         part = torch.bmm(dy.reshape(splits, m, -1).transpose(1, 2), x.reshape(splits, m, -1),
@@ -226,3 +236,57 @@ def linear(x, weight, bias=None, rows=None):
     """Functional form; `rows=(r0, r1)` selects a row slice of weight/bias."""
     r0, r1 = (None, None) if rows is None else rows
     return LinearFn.apply(x, weight, bias, r0, r1)
+
+
+class FFNFn(torch.autograd.Function):
+    """ff(h) = gelu(h W1^T + b1) W2^T + b2 (mamba_decoder.py:39-43, 88) with
+    bf16 compute on the hand-written GEMM: bias + exact GELU fused into the
+    first projection's epilogue (the bf16 pre-activation is written beside
+    the activation for the backward), the GELU backward fused into the
+    second projection's data-gradient epilogue, both weight gradients on
+    the TN kernel straight into fp32."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, w2, b2):
+        cd = h.dtype
+        W1, B1, W2, B2 = cast_weight(w1, cd), cast_weight(b1, cd), cast_weight(w2, cd), cast_weight(b2, cd)
+        h2 = h.reshape(-1, h.shape[-1])
+        pre = torch.empty(h2.shape[0], W1.shape[0], device=h.device, dtype=cd)
+        a = G.mm_nt(h2, W1, bias=B1, gelu_aux=pre)
+        y = torch.addmm(B2, a, W2.t())
+        ctx.save_for_backward(h2, pre, a, W1, W2)
+        ctx.ws = (w1, w2)
+        ctx.meta = (h.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        return y.view(*h.shape[:-1], W2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        h2, pre, a, W1, W2 = ctx.saved_tensors
+        hshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
+        w1, w2 = ctx.ws
+        dy2 = dy.reshape(-1, dy.shape[-1]).to(W2.dtype)
+        # d(pre) = (dy W2) * gelu'(pre), one GEMM (W2^T copy: k-contiguous operand)
+        W2t = cast_weight_t(w2, W2.dtype) if _want_t(w2) else W2.t().contiguous()
+        dpre = G.mm_nt(dy2, W2t, dgelu_aux=pre)
+        dh = None
+        if ctx.needs_input_grad[0]:
+            if _want_t(w1):
+                dh = dpre @ cast_weight_t(w1, W1.dtype).t()
+            else:
+                dh = dpre @ W1
+            dh = dh.view(hshape)
+        dW1 = wgrad(dpre, h2).to(w1dt) if ctx.needs_input_grad[1] else None
+        db1 = colsum(dpre).to(b1dt) if ctx.needs_input_grad[2] else None
+        dW2 = wgrad(dy2, a).to(w2dt) if ctx.needs_input_grad[3] else None
+        db2 = colsum(dy2).to(b2dt) if ctx.needs_input_grad[4] else None
+        return dh, dW1, db1, dW2, db2
+
+
+def ffn(h, w1, b1, w2, b2):
+    """gelu(h W1^T + b1) W2^T + b2: the fused bf16 path when the shapes allow
+    it (bf16 activations, d_model / d_ff multiples of 64), else the
+    per-op path (LinearFn + F.gelu)."""
+    if (G.ENABLED and h.dtype == torch.bfloat16 and h.is_cuda and h.shape[-1] % 64 == 0 and w1.shape[0] % 64 == 0
+            and h.stride(-1) == 1 and h.is_contiguous()):
+        return FFNFn.apply(h, w1, b1, w2, b2)
+    return linear(torch.nn.functional.gelu(linear(h, w1, b1)), w2, b2)

@@ -1,0 +1,135 @@
+"""Hand-written MFMA GEMM (csrc/gemm.hip, mtts_gemm) against fp32 products of
+the same bf16 operands: NT (forward / data gradient) with bias, GELU and
+GELU-backward epilogues, TN (weight gradient) with split-K and accumulate,
+ragged and strided shapes, and the fused FFN autograd function against the
+per-op path (reference mamba_decoder.py:39-43, 88).
+
+Tolerances: bf16 outputs are checked to 1e-2 of the reference's max (bf16
+rounding is 2^-9 relative); fp32 outputs (weight gradients) to 1e-5 of max."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mtts import gemm as G
+from mtts import linear as LIN
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def rnd(*s, scale=1.0, dtype=torch.bfloat16):
+    return ((torch.rand(*s, device=dev) * 2 - 1) * scale).to(dtype)
+
+
+def rel(x, ref):
+    return ((x.float() - ref.float()).abs().max() / ref.float().abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 128), (1000, 264, 192), (300, 1032, 1024),
+                                   (16384, 1024, 1024), (1024, 2048, 1024), (37, 8, 64), (4096, 96, 2048)])
+def test_nt_plain(m, n, k):
+    torch.manual_seed(m + n + k)
+    a, b = rnd(m, k), rnd(n, k)
+    out = G.mm_nt(a, b)
+    assert rel(out, a.float() @ b.float().t()) < 1e-2
+
+
+def test_nt_strided_operands_and_output():
+    torch.manual_seed(1)
+    big_a, big_b = rnd(700, 640), rnd(520, 384)
+    a, b = big_a[:, 64:64 + 256], big_b[8:8 + 264, 128:128 + 256]   # row strides 640 / 384
+    out_full = torch.zeros(700, 300, device=dev, dtype=torch.bfloat16)
+    out = out_full[:, 8:8 + 264]
+    G.mm_nt(a, b, out=out)
+    assert rel(out, a.float() @ b.float().t()) < 1e-2
+    assert out_full[:, :8].abs().max() == 0 and out_full[:, 272:].abs().max() == 0
+
+
+@pytest.mark.parametrize("bias_dtype", [torch.float32, torch.bfloat16])
+def test_nt_bias(bias_dtype):
+    torch.manual_seed(2)
+    a, b, bias = rnd(640, 512), rnd(1024, 512), rnd(1024, dtype=bias_dtype)
+    out = G.mm_nt(a, b, bias=bias)
+    assert rel(out, a.float() @ b.float().t() + bias.float()) < 1e-2
+
+
+def test_nt_gelu_epilogue_matches_torch_exactly():
+    torch.manual_seed(3)
+    a, b, bias = rnd(2048, 1024), rnd(2048, 1024), rnd(2048)
+    pre = torch.empty(2048, 2048, device=dev, dtype=torch.bfloat16)
+    act = G.mm_nt(a, b, bias=bias, gelu_aux=pre)
+    ref_pre = torch.addmm(bias, a, b.t())
+    assert rel(pre, ref_pre) < 1e-2
+    # the activation is F.gelu of the bf16 pre-activation the kernel wrote
+    assert torch.equal(act, F.gelu(pre))
+
+
+def test_nt_dgelu_epilogue():
+    torch.manual_seed(4)
+    dy, w2t, pre = rnd(1536, 1024), rnd(2048, 1024), rnd(1536, 2048, scale=3.0)
+    g = G.mm_nt(dy, w2t, dgelu_aux=pre)
+    prod = (dy.float() @ w2t.float().t()).to(torch.bfloat16)
+    ref = torch.ops.aten.gelu_backward(prod, pre)
+    assert rel(g, ref) < 1e-2
+
+
+@pytest.mark.parametrize("m,n,k,splits", [(1024, 1024, 16384, 8), (4096, 1024, 16384, 4), (264, 520, 2048, 1),
+                                          (264, 520, 2048, 2), (96, 2048, 4096, 16), (2048, 64, 1024, 4),
+                                          (512, 512, 64, 1)])
+def test_tn_weight_gradient(m, n, k, splits):
+    torch.manual_seed(m + 7 * n + k)
+    dy, x = rnd(k, m), rnd(k, n)
+    out = G.mm_tn(dy, x, splits=splits)
+    assert rel(out, dy.float().t() @ x.float()) < 1e-5
+
+
+def test_tn_beta_accumulate_into_row_slice():
+    torch.manual_seed(5)
+    dy, x = rnd(4096, 512), rnd(4096, 768)
+    full = torch.randn(3 * 512, 768, device=dev)
+    before = full.clone()
+    G.mm_tn(dy, x, out=full[512:1024], beta=1.0, splits=4)
+    ref = before[512:1024] + dy.float().t() @ x.float()
+    assert rel(full[512:1024], ref) < 1e-5
+    assert torch.equal(full[:512], before[:512]) and torch.equal(full[1024:], before[1024:])
+
+
+def test_default_splits_fill_the_chip():
+    assert G.tn_splits(4096, 1024, 16384) * 16 * 4 >= 256
+    assert G.tn_splits(1024, 1024, 16384) == 16
+    assert G.tn_splits(256, 256, 64) == 1
+
+
+def test_refuses_unsupported_shapes():
+    a, b = rnd(256, 100), rnd(256, 100)
+    with pytest.raises(RuntimeError, match="multiple of 64"):
+        G.mm_nt(a, b)
+    a, b = rnd(256, 128), rnd(12, 128)
+    with pytest.raises(RuntimeError, match="multiple of 8"):
+        G.mm_nt(a, b)
+
+
+def test_ffn_fused_matches_per_op_path():
+    """FFNFn (GELU fused into the GEMM epilogues) vs linear + F.gelu + linear,
+    outputs and every gradient, bf16 compute with fp32 master weights."""
+    torch.manual_seed(6)
+    B, T, d, dff = 2, 512, 256, 512
+    w1 = (torch.randn(dff, d, device=dev) * d ** -0.5).requires_grad_()
+    b1 = (torch.randn(dff, device=dev) * 0.1).requires_grad_()
+    w2 = (torch.randn(d, dff, device=dev) * dff ** -0.5).requires_grad_()
+    b2 = (torch.randn(d, device=dev) * 0.1).requires_grad_()
+    h0 = torch.randn(B, T, d, device=dev).to(torch.bfloat16)
+    dy = torch.randn(B, T, d, device=dev).to(torch.bfloat16)
+    outs = []
+    for fused in (True, False):
+        h = h0.clone().requires_grad_()
+        for p in (w1, b1, w2, b2):
+            p.grad = None
+        with LIN.cast_scope([w1, b1, w2, b2], torch.bfloat16):
+            y = LIN.FFNFn.apply(h, w1, b1, w2, b2) if fused else \
+                LIN.linear(F.gelu(LIN.linear(h, w1, b1)), w2, b2)
+            y.backward(dy)
+        outs.append([y.detach(), h.grad] + [p.grad.clone() for p in (w1, b1, w2, b2)])
+    names = ["y", "dh", "dW1", "db1", "dW2", "db2"]
+    for nm, a, b in zip(names, outs[0], outs[1]):
+        assert rel(a, b) < 2e-2, nm
