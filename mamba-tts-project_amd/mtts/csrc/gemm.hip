@@ -117,9 +117,42 @@ __device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
                                                  0, 0);
 }
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// erf for the GELU epilogues without ocml's divergent branches and
+// range-reduced expf: |x| <= 0.9: x P(x^2) (degree 5 in x^2), else
+// sign(x) (1 - exp(Q(|x|) - x^2)) with Q a degree-8 fit of log erfc(t) + t^2
+// on [0.85, 4.5] (t clamped there; erf = 1 in fp32 beyond 3.92); both arms
+// computed and selected.  Max relative error 2.4e-7 (x P) / 1.1e-7 (erf arm),
+// erfc relative error 5.4e-6 (the GELU's negative side), checked in float64
+// against math.erf over the whole range (fit and check: DESIGN.md §3).
+__device__ __forceinline__ float erf_fast(float x) {
+  const float s = x * x;
+  float p = -6.175214075e-04f;
+  p = fmaf(p, s, 5.027941428e-03f);
+  p = fmaf(p, s, -2.678935602e-02f);
+  p = fmaf(p, s, 1.128241718e-01f);
+  p = fmaf(p, s, -3.761254847e-01f);
+  p = fmaf(p, s, 1.128379107e+00f);
+  const float small = x * p;
+  const float t = fminf(fabsf(x), 4.5f);
+  float q = 1.430673365e-06f;
+  q = fmaf(q, t, -4.196325972e-05f);
+  q = fmaf(q, t, 5.622986355e-04f);
+  q = fmaf(q, t, -4.598612431e-03f);
+  q = fmaf(q, t, 2.596756257e-02f);
+  q = fmaf(q, t, -1.092917621e-01f);
+  q = fmaf(q, t, 3.673504889e-01f);
+  q = fmaf(q, t, -1.129761577e+00f);
+  q = fmaf(q, t, 2.067339810e-04f);
+  const float e = __builtin_amdgcn_exp2f(fmaf(-t, t, q) * kLog2e);
+  const float big = __builtin_copysignf(1.f - e, x);
+  return fabsf(x) <= 0.9f ? small : big;
+}
+// F.gelu (approximate='none') and its derivative (torch's GeluBackward):
+// 0.5 x (1 + erf(x/sqrt2)); cdf + x exp(-x^2/2) / sqrt(2 pi)
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f));
+  return cdf + x * 0.3989422804014327f * __builtin_amdgcn_exp2f(-0.5f * x * x * kLog2e);
 }
 
 // Per-thread source offsets (elements) of one region's two DMAs, relative to
@@ -232,6 +265,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
     if (kt >= 0) return;   // timing-only: no operand traffic
 #endif
     const int buf = kt & 1;
+#ifdef MTTS_GEMM_DIAG_FIXK
+    kt = buf;   // timing-only: every K-tile re-reads K-tiles 0/1 (L2-resident, per-block addresses)
+#endif
     if (r == R_A0 || r == R_A1) la.stage1(abase + kt * astep, r - R_A0, region_addr(buf, r), wave, i);
     else lb.stage1(bbase + kt * bstep, r - R_B0, region_addr(buf, r), wave, i);
   };
@@ -360,14 +396,16 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
 
   // ---- epilogue: lane holds rows m = .. + (lane&15), columns n = .. + 4*(lane>>4) + j
   const int rl = lane & 15, cl = 4 * (lane >> 4);
+  // wave-uniform: the wave's whole 128x64 sub-tile in bounds (no per-lane masks)
+  const bool full = m0 + wr * 128 + 128 <= p.m && n0 + wc * 64 + 64 <= p.n;
 #pragma unroll
   for (int MB = 0; MB < 8; ++MB) {
     const int row = m0 + wr * 128 + MB * 16 + rl;
-    if (row >= p.m) continue;
+    if (!full && row >= p.m) continue;
 #pragma unroll
     for (int NB = 0; NB < 4; ++NB) {
       const int col = n0 + wc * 64 + NB * 16 + cl;
-      if (col >= p.n) continue;   // n % 4 == 0 (host check): a lane's 4 columns are all in or all out
+      if (!full && col >= p.n) continue;   // n % 8 == 0: a lane's 4 columns are all in or all out
       f32x4 v = acc[MB][NB];
       if constexpr (OUT_F32) {
         float* cp = (float*)p.c + (int64_t)split * p.split_stride + (int64_t)row * p.ldc + col;

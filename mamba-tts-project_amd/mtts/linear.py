@@ -286,7 +286,7 @@ def ffn(h, w1, b1, w2, b2):
     """gelu(h W1^T + b1) W2^T + b2: the fused bf16 path when the shapes allow
     it (bf16 activations, d_model / d_ff multiples of 64), else the
     per-op path (LinearFn + F.gelu)."""
-    if (G.ENABLED and h.dtype == torch.bfloat16 and h.is_cuda and h.shape[-1] % 64 == 0 and w1.shape[0] % 64 == 0
+    if (G.ENABLED and G.FFN_FUSED and h.dtype == torch.bfloat16 and h.is_cuda and h.shape[-1] % 64 == 0 and w1.shape[0] % 64 == 0
             and h.stride(-1) == 1 and h.is_contiguous()):
         return FFNFn.apply(h, w1, b1, w2, b2)
     return linear(torch.nn.functional.gelu(linear(h, w1, b1)), w2, b2)

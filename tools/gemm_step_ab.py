@@ -42,9 +42,14 @@ def timeit(n=10):
     return (time.perf_counter() - t0) / n * 1e3
 
 
-res = {"hip": [], "blaslt": []}
+if len(sys.argv) > 1:          # profile one mode: gemm_step_ab.py hip|blaslt
+    G.ENABLED = sys.argv[1] == "hip"
+    print(sys.argv[1], round(timeit(5), 2), flush=True)
+    sys.exit(0)
+res = {"hip": [], "wgrad-only": [], "blaslt": []}
 for _ in range(3):
-    for kind in ("hip", "blaslt"):
-        G.ENABLED = kind == "hip"
+    for kind in res:
+        G.ENABLED = kind != "blaslt"
+        G.FFN_FUSED = kind == "hip"
         res[kind].append(timeit())
 print({k: [round(x, 2) for x in v] for k, v in res.items()}, flush=True)
