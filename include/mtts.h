@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 1
+#define MTTS_ABI_VERSION 2
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -434,9 +434,19 @@ typedef struct {
   int64_t ld_gb;
   const void* res;           /* NULL = no residual epilogue */
   int64_t ld_res;
+  /* kgroups > 1: the K range is also split over kgroups workgroups per
+   * 32-column tile (K % (64 * kgroups) == 0, kgroups <= 32); fp32 partials
+   * go to splitk_slab (ceil(N / 32) * kgroups * 1024 floats) and the last
+   * workgroup of a tile (one ticket per tile in splitk_count, ceil(N / 32)
+   * ints that must be ZERO before the first launch; the kernel resets them)
+   * sums them in fixed order and runs the epilogue. */
+  int kgroups;
+  float* splitk_slab;
+  int* splitk_count;
 } MttsRowsArgs;
 
 int mtts_gemm_rows(const MttsRowsArgs* a, void* stream);
+
 
 /* ------------------------------------------------------------------------
  * Training-path GEMM (replaces the nn.Linear / Mamba in_proj, x_proj,

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -73,7 +73,7 @@ class RowsArgs(C.Structure):
                 ("x", vp), ("W", vp), ("bias", vp), ("y", vp),
                 ("conv_dim", i32), ("conv_state", vp), ("conv_w", vp), ("conv_b", vp), ("u", vp), ("ldu", i64),
                 ("ln_w", vp), ("ln_b", vp), ("ln_eps", f32), ("gamma", vp), ("beta", vp), ("ld_gb", i64),
-                ("res", vp), ("ld_res", i64)]
+                ("res", vp), ("ld_res", i64), ("kgroups", i32), ("splitk_slab", vp), ("splitk_count", vp)]
 
 
 class GemmArgs(C.Structure):

@@ -25,16 +25,36 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-template <int KS, int U, bool LNP>
+// SK: the K range is also split over a.kgroups workgroups per 32-column tile
+// (grid = tiles * kgroups), each writing its fp32 32x32 partial to a slab;
+// the last to arrive (agent-scope release / acquire around one ticket per
+// tile, the counter reset by it) sums the kgroups slabs in fixed order and
+// runs the epilogue.  With the LayerNorm prologue every workgroup derives
+// the full-row statistics itself from the (L2-resident) x rows.
+template <int KS, int U, bool LNP, bool SK>
 __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a) {
   __shared__ float red[KS][32][33];
-  __shared__ float psum[LNP ? KS : 1][32], psq[LNP ? KS : 1][32];
+  __shared__ float psum[LNP ? (SK ? 2 * KS : KS) : 1][32], psq[LNP ? (SK ? 2 * KS : KS) : 1][32];
   __shared__ __attribute__((aligned(16))) float slw[LNP ? 2048 : 4], slb[LNP ? 2048 : 4];
+  __shared__ int s_last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.x * 32;
+  const int KG = SK ? a.kgroups : 1;
+  int tile = blockIdx.x, kg = 0;
+  if constexpr (SK) {
+    const int tiles = gridDim.x / KG;
+    if (tiles % 8 == 0) {   // a tile's K groups on one XCD (round-robin dispatch): same-XCD slab reads
+      const int xcd = blockIdx.x % 8, q = blockIdx.x / 8;
+      tile = xcd + 8 * (q / KG);
+      kg = q % KG;
+    } else {
+      tile = blockIdx.x / KG;
+      kg = blockIdx.x % KG;
+    }
+  }
+  const int n0 = tile * 32;
   const int M = a.M, N = a.N;
-  const int kc = a.K / KS, kb = wave * kc;
+  const int kc = a.K / (KS * KG), kb = (kg * KS + wave) * kc;
   const bool rowok = i < M, colok = n0 + i < N;
   const bf16_t* xr = (const bf16_t*)a.x + (int64_t)(rowok ? i : 0) * a.ldx + kb + 8 * h;
   const bf16_t* wr = (const bf16_t*)a.W + (int64_t)(colok ? n0 + i : 0) * a.ldw + kb + 8 * h;
@@ -96,30 +116,68 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
         ba[u] = *reinterpret_cast<const s16x8*>((const bf16_t*)a.beta + ro + 16 * u);
       }
     }
-    float sx = 0.f;
+    float mean, rstd;
+    if constexpr (!SK) {
+      float sx = 0.f;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) sx += bf2f((bf16_t)xa[u][q]);
-    sx += __shfl_xor(sx, 32);
-    if (lane < 32) psum[wave][i] = sx;
-    __syncthreads();
-    float mean = 0.f;
+        for (int q = 0; q < 8; ++q) sx += bf2f((bf16_t)xa[u][q]);
+      sx += __shfl_xor(sx, 32);
+      if (lane < 32) psum[wave][i] = sx;
+      __syncthreads();
+      mean = 0.f;
 #pragma unroll
-    for (int w = 0; w < KS; ++w) mean += psum[w][i];
-    mean /= a.K;
-    float sq = 0.f;
+      for (int w = 0; w < KS; ++w) mean += psum[w][i];
+      mean /= a.K;
+      float sq = 0.f;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) { const float d = bf2f((bf16_t)xa[u][q]) - mean; sq = fmaf(d, d, sq); }
-    sq += __shfl_xor(sq, 32);
-    if (lane < 32) psq[wave][i] = sq;
-    __syncthreads();
-    float var = 0.f;
+        for (int q = 0; q < 8; ++q) { const float d = bf2f((bf16_t)xa[u][q]) - mean; sq = fmaf(d, d, sq); }
+      sq += __shfl_xor(sq, 32);
+      if (lane < 32) psq[wave][i] = sq;
+      __syncthreads();
+      float var = 0.f;
 #pragma unroll
-    for (int w = 0; w < KS; ++w) var += psq[w][i];
-    const float rstd = 1.f / sqrtf(var / a.K + a.ln_eps);
+      for (int w = 0; w < KS; ++w) var += psq[w][i];
+      rstd = 1.f / sqrtf(var / a.K + a.ln_eps);
+    } else {
+      // full-row statistics from x itself (L2-resident; the weights are
+      // already in flight): thread (row r, part p) covers K / (2 KS) columns;
+      // two passes (mean, then sum of squared deviations) as the LayerNorm
+      // kernel does, fixed-order combines through LDS
+      const int r = threadIdx.x & 31, part = threadIdx.x >> 5, np = 2 * KS;
+      const bf16_t* xrow = (const bf16_t*)a.x + (int64_t)(r < M ? r : 0) * a.ldx;
+      const int span = a.K / np;
+      float s1 = 0.f;
+#pragma unroll 4
+      for (int c = part * span; c < (part + 1) * span; c += 8) {
+        const s16x8 v = *reinterpret_cast<const s16x8*>(xrow + c);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s1 += bf2f((bf16_t)v[q]);
+      }
+      psum[part][r] = s1;
+      __syncthreads();
+      float t1 = 0.f;
+      for (int w = 0; w < np; ++w) t1 += psum[w][r];
+      const float mr = t1 / a.K;
+      float s2 = 0.f;
+#pragma unroll 4
+      for (int c = part * span; c < (part + 1) * span; c += 8) {
+        const s16x8 v = *reinterpret_cast<const s16x8*>(xrow + c);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { const float d = bf2f((bf16_t)v[q]) - mr; s2 = fmaf(d, d, s2); }
+      }
+      psq[part][r] = s2;
+      __syncthreads();
+      float t2 = 0.f;
+      mean = 0.f;
+      for (int w = 0; w < np; ++w) { mean += psum[w][i]; t2 += psq[w][i]; }
+      mean /= a.K;
+      const float var = t2 / a.K;
+      rstd = 1.f / sqrtf(var + a.ln_eps);
+    }
     // operand = bf16(LN(x) * w + b [, gamma * . + beta]) as mtts_layernorm_fwd rounds it
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -153,13 +211,56 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[wave][acc_row(r, h)][i] = acc[r];
   __syncthreads();
+  float part[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int idx = threadIdx.x + e * 64 * KS, row = idx >> 5, col = idx & 31;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < KS; ++w) s += red[w][row][col];
+    part[e] = s;
+  }
+  if constexpr (SK) {
+    if (KG > 1) {
+      // write-through (sc1) slab stores: no release fence; one relaxed
+      // agent-scope ticket; the last arriver reads every slab with sc1 loads
+      // (no acquire), all loads issued before the fixed-order sum
+      float* slab = a.splitk_slab + (int64_t)tile * KG * 1024;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        __hip_atomic_store(slab + kg * 1024 + threadIdx.x + e * 64 * KS, part[e], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(a.splitk_count + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == KG - 1;
+        if (last) __hip_atomic_store(a.splitk_count + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last;
+      }
+      __syncthreads();
+      if (!s_last) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the ticket
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        float v[32];
+#pragma unroll
+        for (int g = 0; g < 32; ++g)
+          if (g < KG) v[g] = __hip_atomic_load(slab + g * 1024 + threadIdx.x + e * 64 * KS, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        float s = 0.f;
+#pragma unroll
+        for (int g = 0; g < 32; ++g)
+          if (g < KG) s += v[g];
+        part[e] = s;
+      }
+    }
+  }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int idx = threadIdx.x + e * 64 * KS, row = idx >> 5, col = idx & 31, c = n0 + col;
     if (row >= M || c >= N) continue;
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < KS; ++w) s += red[w][row][col];
+    float s = part[e];
     s += bv[e];
     if (a.act == 1) s = 0.5f * s * (1.f + erff(s * 0.70710678118654752f));   // F.gelu (exact erf)
     const bf16_t sb = f2bf(s);
@@ -184,13 +285,17 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
 
 template <int KS, int U>
 void launch_rows(const MttsRowsArgs* a, int tiles, hipStream_t st) {
+  const bool sk = a->kgroups > 1;
+  const dim3 grid(tiles * (sk ? a->kgroups : 1));
   if constexpr (KS <= 8) {
     if (a->ln_w) {
-      hipLaunchKernelGGL((gemm_rows_kernel<KS, U, true>), dim3(tiles), dim3(64 * KS), 0, st, *a);
+      if (sk) hipLaunchKernelGGL((gemm_rows_kernel<KS, U, true, true>), grid, dim3(64 * KS), 0, st, *a);
+      else hipLaunchKernelGGL((gemm_rows_kernel<KS, U, true, false>), grid, dim3(64 * KS), 0, st, *a);
       return;
     }
   }
-  hipLaunchKernelGGL((gemm_rows_kernel<KS, U, false>), dim3(tiles), dim3(64 * KS), 0, st, *a);
+  if (sk) hipLaunchKernelGGL((gemm_rows_kernel<KS, U, false, true>), grid, dim3(64 * KS), 0, st, *a);
+  else hipLaunchKernelGGL((gemm_rows_kernel<KS, U, false, false>), grid, dim3(64 * KS), 0, st, *a);
 }
 
 }  // namespace
@@ -226,21 +331,31 @@ extern "C" int mtts_gemm_rows(const MttsRowsArgs* a, void* stream) {
   // a trip in flight.  Measured on the C4 step (tools/decode_ab.py, p50 ms):
   // ks = 8 everywhere 1.20; 4 / 8 / 16 by tile count 1.23; ks = 4 1.25;
   // ks = 2 1.44; one 8-step trip per wave with up to 16 waves 1.28.
+  const int KG = a->kgroups > 1 ? a->kgroups : 1;
+  if (KG > 1) {
+    MTTS_CHECK(a->splitk_slab && a->splitk_count && K % (64 * KG) == 0 && KG <= 32,
+               "gemm_rows: split-K over %d workgroups needs slab / counters and K %% (64 * kgroups) == 0", KG);
+    if (a->ln_w && K > 2048) {
+      set_error("gemm_rows: LayerNorm prologue needs K <= 2048 (LN parameters staged in LDS; K=%d)", K);
+      return MTTS_EUNSUPPORTED;
+    }
+  }
+  const int Kw = K / KG;   // per-workgroup K range
   int U = 4;
-  int ks = K % (64 * 8) == 0 ? 8 : K % (64 * 4) == 0 ? 4 : K % (64 * 2) == 0 ? 2 : 1;
+  int ks = Kw % (64 * 8) == 0 ? 8 : Kw % (64 * 4) == 0 ? 4 : Kw % (64 * 2) == 0 ? 2 : 1;
   if (const char* e = getenv("MTTS_ROWS_KS")) {   // tuning override
     const int f = atoi(e);
-    if ((f == 1 || f == 2 || f == 4 || f == 8 || f == 16) && K % (64 * f) == 0) ks = f;
+    if ((f == 1 || f == 2 || f == 4 || f == 8 || f == 16) && Kw % (64 * f) == 0) ks = f;
   }
   int u8 = U == 8;
-  if (a->ln_w) {   // LayerNorm prologue: exactly one trip per wave (K == ks * 16 * U), ks <= 8
+  if (a->ln_w) {   // LayerNorm prologue: exactly one trip per wave (Kw == ks * 16 * U), ks <= 8
     int f = 0;
     for (int c = 8; c >= 1 && !f; c >>= 1) {
-      if (K == c * 128) f = c, u8 = 1;
-      else if (K == c * 64) f = c, u8 = 0;
+      if (Kw == c * 64) f = c, u8 = 0;
+      else if (Kw == c * 128) f = c, u8 = 1;
     }
-    if (!f) {
-      set_error("gemm_rows: LayerNorm prologue needs K = 64 * {1,2,4,8} or 128 * {1,..,8} (K=%d)", K);
+    if (!f || (KG == 1 && K > 2048)) {
+      set_error("gemm_rows: LayerNorm prologue needs K / kgroups = 64 * {1,2,4,8} or 128 * {1,..,8} (K=%d)", K);
       return MTTS_EUNSUPPORTED;
     }
     ks = f;

@@ -510,6 +510,45 @@ def gemm_rows_ln_ok(K):
     return K in {64 * c for c in (1, 2, 4, 8)} | {128 * c for c in (1, 2, 4, 8)}
 
 
+_rows_ws = {}
+
+
+def rows_workspace(device):
+    """Per-device split-K scratch of the decode projections: fp32 partial
+    slabs and per-tile tickets (zeroed once; every launch leaves them zero).
+    Allocate outside graph capture (DecodeEngine does, before capturing)."""
+    key = torch.device(device)
+    ws = _rows_ws.get(key)
+    if ws is None:
+        ws = (torch.empty(ROWS_MAX_TILES * ROWS_MAX_KG * 1024, device=key, dtype=torch.float32),
+              torch.zeros(ROWS_MAX_TILES, device=key, dtype=torch.int32))
+        _rows_ws[key] = ws
+    return ws
+
+
+ROWS_MAX_TILES, ROWS_MAX_KG = 512, 16
+# Cross-workgroup split-K of the decode projections: built, tested and
+# measured slower on the C4 step (graph replay p50 1.39 -> 1.8-2.2 ms with
+# write-through slabs; per call 6.6-13 us vs 5.6-9 us one workgroup per
+# tile, tools/decode_ab.py shapes splitk): off.
+ROWS_SPLITK = False
+
+
+def rows_kgroups(N, K, ln):
+    """Workgroups per 32-column tile: fill ~256 workgroups, each keeping
+    >= 128 of K (one wave trip) and K / kgroups a LayerNorm-prologue size."""
+    tiles = -(-N // 32)
+    if not ROWS_SPLITK or tiles > ROWS_MAX_TILES:
+        return 1
+    kg = 1
+    while tiles * kg < 256 and kg < ROWS_MAX_KG and K % (64 * kg * 2) == 0 and K // (kg * 2) >= 128:
+        kg *= 2
+    if ln:
+        while kg > 1 and not gemm_rows_ln_ok(K // kg):
+            kg //= 2
+    return kg
+
+
 def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
     """y = act(x @ weight.t() + bias) for the decode step's skinny GEMMs
     (x: M <= 32 rows, bf16; act None or "gelu" = exact-erf F.gelu).
@@ -563,5 +602,9 @@ def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
         if res.dtype != torch.bfloat16 or res.shape != (M, N) or res.stride(1) != 1:
             raise ValueError("gemm_rows: res must be (M, N) bf16 with unit column stride")
         a.res, a.ld_res = res.data_ptr(), res.stride(0)
+    kg = rows_kgroups(N, K, ln is not None)
+    if kg > 1:
+        slab, cnt = rows_workspace(dev)
+        a.kgroups, a.splitk_slab, a.splitk_count = kg, slab.data_ptr(), cnt.data_ptr()
     L.call("mtts_gemm_rows", a)
     return out[0] if len(out) == 1 else tuple(out)

@@ -522,13 +522,69 @@ def test_gemm_rows_ln_prologue_and_residual(M, N, K, film):
     close(xs.float(), ops.gemm_rows(x, w, b).float() + res.float(), rtol=2 ** -7, name="residual")
 
 
-def test_gemm_rows_ln_prologue_rejects_multi_trip_k():
+def test_gemm_rows_ln_prologue_rejects_multi_trip_k(monkeypatch):
+    """One workgroup per tile: the LayerNorm prologue needs one trip per wave
+    (K = 4096 cannot); split over workgroups the same K is taken."""
     from mtts import ops
-    x = torch.zeros(4, 2048, device=DEV, dtype=torch.bfloat16)
-    w = torch.zeros(64, 2048, device=DEV, dtype=torch.bfloat16)
-    lw = torch.ones(2048, device=DEV)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = torch.randn(4, 4096, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(64, 4096, generator=g) / 64).to(DEV, torch.bfloat16)
+    lw, lb = torch.ones(4096, device=DEV), torch.zeros(4096, device=DEV)
+    monkeypatch.setattr(ops, "ROWS_SPLITK", False)
     with pytest.raises(RuntimeError, match="LayerNorm prologue"):
-        ops.gemm_rows(x, w, ln=(lw, lw, 1e-5))
+        ops.gemm_rows(x, w, ln=(lw, lb, 1e-5))
+    monkeypatch.setattr(ops, "ROWS_SPLITK", True)
+    with pytest.raises(RuntimeError, match="LayerNorm prologue"):   # 4096 > 2048: LDS copy of the LN params
+        ops.gemm_rows(x, w, ln=(lw, lb, 1e-5))
+    x2, w2, lw2, lb2 = x[:, :2048], w[:, :2048].contiguous(), lw[:2048], lb[:2048]
+    y = ops.gemm_rows(x2, w2, ln=(lw2, lb2, 1e-5))
+    h, _ = ops.layer_norm(x2.contiguous(), lw2, lb2, 1e-5, rows_per_group=1)
+    close(y.float(), (h.double() @ w2.double().t()).float(), rtol=2 ** -7, name="split-K LN K=2048")
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 4096, 1024), (32, 1024, 2048), (32, 1024, 1024), (32, 96, 2048),
+                                   (32, 10, 1024), (5, 2048, 1024), (3, 800, 512)])
+@pytest.mark.parametrize("mode", ["plain", "ln", "film", "res", "conv", "gelu"])
+def test_gemm_rows_split_k_matches_single_workgroup(M, N, K, mode, monkeypatch):
+    """The K range split over workgroups (fp32 partial slabs, last arriver
+    sums them in fixed order) equals one workgroup per tile up to fp32
+    summation order: within one bf16 rounding, and bit-identical across
+    repeated launches (deterministic); tickets left at zero."""
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + len(mode))
+    x = (torch.randn(M, K, generator=g) * 2 + 0.3).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    kw = {}
+    if mode in ("ln", "film"):
+        if not ops.gemm_rows_ln_ok(K):
+            pytest.skip("K not a single-workgroup LayerNorm size")
+        lw, lb = torch.randn(K, generator=g).to(DEV), torch.randn(K, generator=g).to(DEV)
+        gam = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if mode == "film" else None
+        bet = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if mode == "film" else None
+        kw["ln"] = (lw, lb, 1e-5, gam, bet)
+    if mode == "res":
+        kw["res"] = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    act = "gelu" if mode == "gelu" else None
+    C = (N // 2) // 32 * 32
+    if mode == "conv" and C == 0:
+        pytest.skip("no whole conv tile")
+    st0 = torch.randn(M, C, 4, generator=g).to(DEV) if mode == "conv" else None
+    outs = []
+    for split in (False, True, True):
+        monkeypatch.setattr(ops, "ROWS_SPLITK", split)
+        if mode == "conv":
+            st = st0.clone()
+            y, u = ops.gemm_rows(x, w, conv=(st, torch.ones(C, 4, device=DEV), None))
+            outs.append((y, u, st))
+        else:
+            outs.append((ops.gemm_rows(x, w, b, act, **kw),))
+    for a, c in zip(outs[0], outs[1]):
+        close(c.float(), a.float(), rtol=2 ** -7, name=f"split-K {mode}")
+    for a, c in zip(outs[1], outs[2]):
+        assert torch.equal(a, c)
+    if ops.rows_kgroups(N, K, "ln" in kw) > 1:
+        assert int(ops.rows_workspace(DEV)[1].abs().sum()) == 0
 
 
 def test_wgrad_split_k_matches_fp64():

@@ -43,9 +43,13 @@ def shapes():
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
         b = torch.randn(N, device=dev, dtype=torch.bfloat16)
         tr = t_us(lambda: ops.gemm_rows(x, w, b))
+        ops.ROWS_SPLITK = False
+        t1 = t_us(lambda: ops.gemm_rows(x, w, b))
+        ops.ROWS_SPLITK = True
         tb = t_us(lambda: torch.addmm(b, x, w.t()))
         gbs = N * K * 2 / tr / 1e3
-        print(f"N={N:5d} K={K:5d}  rows {tr:6.2f} us ({gbs:6.0f} GB/s)   hipBLASLt {tb:6.2f} us", flush=True)
+        print(f"N={N:5d} K={K:5d}  rows {tr:6.2f} us ({gbs:6.0f} GB/s, kgroups {ops.rows_kgroups(N, K, False)})  "
+              f"one WG/tile {t1:6.2f} us   hipBLASLt {tb:6.2f} us", flush=True)
 
 
 def step(modes=(True, False)):
@@ -93,6 +97,13 @@ if __name__ == "__main__":
             os.environ.pop(k)
     if "rowsonly" in what:
         step((True,))
+    if "splitk" in what:   # rows kernels with / without the cross-workgroup K split, interleaved
+        for _ in range(2):
+            for sk in (True, False):
+                ops.ROWS_SPLITK = sk
+                print("splitk", sk, end=" ", flush=True)
+                step((True,))
+        ops.ROWS_SPLITK = True
     if "modes" in what:
         for env in ({}, {"MTTS_ROWS_KS": "2"}, {"MTTS_ROWS_KS": "4"}, {"MTTS_ROWS_KS": "8"},
                     {"MTTS_DECODE_FUSED": "0"}, {}):
