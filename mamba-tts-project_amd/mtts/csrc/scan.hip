@@ -1887,7 +1887,7 @@ static bool wide_io_ok(const MttsScanFwdArgs* a) {
 // VMEM issue order per tile `it`: [stores of it-1] [B/C regs of it+1]
 // [DMA of it+NB-1]; waiting until only that DMA is in flight makes tile it+1
 // (B/C and the DMA issued NB-2 iterations earlier) complete.
-template <typename Tio, typename Tbc, bool SP, bool HZ, bool SPREAD>
+template <typename Tio, typename Tbc, bool SP, bool HZ>
 __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdArgs a) {
   constexpr int ES = (int)sizeof(Tio);
   constexpr int EPC = 16 / ES;            // elements per 16-byte chunk
@@ -2002,15 +2002,7 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
       if (t < L) *reinterpret_cast<uint4*>(go + (int64_t)t * a.out_ls) = v;
     }
   };
-  // SPREAD: the NDMA LDS-DMAs of tile it+NB-1 are issued one per step inside
-  // tile it's step loop (between VALU work) instead of as one burst before it
-  auto dma_one = [&](int dit, int dbuf, int q) __attribute__((always_inline)) {
-    const int k = q / NAR, ar = q % NAR;
-    const int t = min(dit * TT + k * RPD + drow, L - 1);
-    const Tio* g = ar == 0 ? gu + (int64_t)t * a.u_ls : ar == 1 ? gd + (int64_t)t * a.delta_ls : gz + (int64_t)t * a.z_ls;
-    dma16(g, &sX[wave][dbuf][ar][k * RPD * 64]);
-  };
-  auto compute_tile = [&](auto tail, int it, int buf, int bb, int dit, int dbuf) __attribute__((always_inline)) {
+  auto compute_tile = [&](auto tail, int it, int buf, int bb) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail)::value;
     const int t0 = it * TT;
     // step 0's B reads go out first (their latency hides under the scalar work);
@@ -2074,9 +2066,6 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
           *reinterpret_cast<f4*>(ck + (int64_t)((t0 + s) / kSub) * a.dim * kN + 4 * q) =
               f4{h[2 * q][0], h[2 * q][1], h[2 * q + 1][0], h[2 * q + 1][1]};
       }
-      if constexpr (SPREAD) {
-        if (s < NDMA && dit >= 0) dma_one(dit, dbuf, s);
-      }
       if (s + 1 < TT) read_row(s + 1, 0, bB[(s + 1) & 1]);
       read_row(s, 1, bC[s & 1]);
       __builtin_amdgcn_sched_barrier(0);
@@ -2109,10 +2098,9 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
     const bool more = it + 1 < nt;
     const bool ahead = it + NB - 1 < nt;
     if (more) load_bc(it + 1);
-    if (!SPREAD && ahead) dma_tile(it + NB - 1, prev);
-    const int dit = SPREAD && ahead ? it + NB - 1 : -1;
-    if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf, 0, dit, prev);
-    else compute_tile(TrueT{}, it, buf, 0, dit, prev);
+    if (ahead) dma_tile(it + NB - 1, prev);
+    if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf, 0);
+    else compute_tile(TrueT{}, it, buf, 0);
     if (more) {
 #if defined(MTTS_C1_DIAG_NODMA) || defined(MTTS_C1_DIAG_NOSTORE)
       // the hand-counted wait below assumes exactly NDMA DMAs and TT stores
@@ -2156,11 +2144,8 @@ static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream
   float* seg = (float*)a->workspace;
   if (c1_ok(a)) {
     const dim3 grid((a->dim / 64 + 3) / 4, a->batch);
-    if (getenv("MTTS_C1_SPREAD")) {
-      if (a->z) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true, true>), grid, dim3(256), 0, st, *a);
-      else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false, true>), grid, dim3(256), 0, st, *a);
-    } else if (a->z) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true, false>), grid, dim3(256), 0, st, *a);
-    else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false, false>), grid, dim3(256), 0, st, *a);
+    if (a->z) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true>), grid, dim3(256), 0, st, *a);
+    else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false>), grid, dim3(256), 0, st, *a);
     return;
   }
   if (wide_io_ok(a) && !getenv("MTTS_SCAN_FWD_V1")) {
