@@ -42,9 +42,9 @@ def timeit(n=10):
     return (time.perf_counter() - t0) / n * 1e3
 
 
-if len(sys.argv) > 1:          # profile one mode: gemm_step_ab.py hip|blaslt
+if len(sys.argv) > 1:          # profile one mode: gemm_step_ab.py hip|blaslt [steps]
     G.ENABLED = sys.argv[1] == "hip"
-    print(sys.argv[1], round(timeit(5), 2), flush=True)
+    print(sys.argv[1], round(timeit(int(sys.argv[2]) if len(sys.argv) > 2 else 5), 2), flush=True)
     sys.exit(0)
 res = {"hip": [], "wgrad-only": [], "blaslt": []}
 for _ in range(3):

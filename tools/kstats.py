@@ -2,10 +2,13 @@
 import csv
 import sys
 
-args = [a for a in sys.argv[1:] if not a.startswith("--")]
 per = 1.0
-if "--per" in sys.argv:
-    per = float(sys.argv[sys.argv.index("--per") + 1])
+argv = list(sys.argv[1:])
+if "--per" in argv:
+    i = argv.index("--per")
+    per = float(argv[i + 1])
+    del argv[i:i + 2]
+args = [a for a in argv if not a.startswith("--")]
 
 
 def load(p):
