@@ -59,7 +59,7 @@ class MambaTTSDecoderLayer(nn.Module):
             x, ff_out, new_state = self.forward_fused(x, None, text_hidden, z_style, text_mask, mamba_state)
         return x + ff_out, new_state                                          # :88-89
 
-    def forward_fused(self, x, pending, text_hidden, z_style, text_mask=None, mamba_state=None):
+    def forward_fused(self, x, pending, text_hidden, z_style, text_mask=None, mamba_state=None, kpm=None):
         """Same math as forward(); the input residual `x + pending` and the
         output residual `x + ff_out` are left to the neighbouring fused
         residual+LayerNorm kernels.  Returns (x, ff_out, new_state)."""
@@ -73,8 +73,8 @@ class MambaTTSDecoderLayer(nn.Module):
 
         # 2) x = x + h_mamba ; h = norm_cross(x)   (fused, :64-67)
         h, x = ops.layer_norm(h_mamba, self.norm_cross.weight, self.norm_cross.bias, self.norm_cross.eps, res=x)
-        key_padding_mask = None
-        if text_mask is not None:
+        key_padding_mask = kpm                     # precomputed once per decoder forward
+        if key_padding_mask is None and text_mask is not None:
             key_padding_mask = ~text_mask                                   # :68-70 (sic)
         attn_out, _ = self.cross_attn(query=h, key=text_hidden, value=text_hidden,
                                       key_padding_mask=key_padding_mask)
@@ -166,9 +166,10 @@ class MambaTTSDecoder(nn.Module):
     def _run_layers(self, x, text_hidden, z_style, text_mask, states):
         pending = None
         new_states = []
+        kpm = None if text_mask is None else ~text_mask                     # :68-70 (sic), once for all layers
         for i, layer in enumerate(self.layers):
             x, pending, st = layer.forward_fused(x, pending, text_hidden, z_style, text_mask,
-                                                 None if states is None else states[i])
+                                                 None if states is None else states[i], kpm=kpm)
             new_states.append(st)
         return x, pending, new_states
 

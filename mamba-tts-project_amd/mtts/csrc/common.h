@@ -15,6 +15,14 @@ void set_error(const char* fmt, ...);
 // out[g * out_gstride + c] = sum over partials p in [g*ppg, (g+1)*ppg) of part[p * pstride + c]
 void colsum(const float* part, int nparts, int ppg, int64_t pstride, int ncols, float* out, int64_t out_gstride,
             hipStream_t st);
+struct ColsumJob {
+  const float* part;
+  float* out;
+  int nparts, ppg;
+  int64_t out_gstride;
+};
+// up to 4 colsum jobs over slabs of one width and part stride, one launch
+void colsum_multi(const ColsumJob* jobs, int n, int ncols, int64_t pstride, hipStream_t st);
 
 #define MTTS_CHECK(cond, ...)                                                 \
   do {                                                                        \

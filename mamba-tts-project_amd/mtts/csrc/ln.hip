@@ -329,13 +329,16 @@ extern "C" int mtts_layernorm_bwd(const MttsLNBwdArgs* a, void* stream) {
   MTTS_LAUNCH_CHECK("layernorm_bwd");
   const int nblk = (f.rows + rb - 1) / rb;
   const int64_t slab = (int64_t)nblk * f.cols;
-  colsum(part, nblk, nblk, f.cols, f.cols, a->dw, 0, st);
-  colsum(part + slab, nblk, nblk, f.cols, f.cols, a->db, 0, st);
+  // dw, db (and dgamma, dbeta per FiLM row group) in one launch
+  ColsumJob jobs[4] = {{part, a->dw, nblk, nblk, 0}, {part + slab, a->db, nblk, nblk, 0}};
+  int nj = 2;
   if (f.gamma) {
     const int bpg = f.rows_per_group / rb;
-    colsum(part + 2 * slab, nblk, bpg, f.cols, f.cols, a->dgamma, f.cols, st);
-    colsum(part + 3 * slab, nblk, bpg, f.cols, f.cols, a->dbeta, f.cols, st);
+    jobs[2] = {part + 2 * slab, a->dgamma, nblk, bpg, (int64_t)f.cols};
+    jobs[3] = {part + 3 * slab, a->dbeta, nblk, bpg, (int64_t)f.cols};
+    nj = 4;
   }
+  colsum_multi(jobs, nj, f.cols, f.cols, st);
   MTTS_LAUNCH_CHECK("layernorm_bwd_reduce");
   return MTTS_OK;
 }

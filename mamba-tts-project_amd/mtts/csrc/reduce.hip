@@ -40,11 +40,106 @@ void colsum(const float* part, int nparts, int ppg, int64_t pstride, int ncols, 
                      pstride, ncols, out, out_gstride);
 }
 
+// Up to 4 column-sum jobs over slabs of the same width in ONE launch
+// (blockIdx.z = job): the LayerNorm backward's dw / db / dgamma / dbeta.
+struct ColsumJobs {
+  ColsumJob j[4];
+  int ncols;
+  int64_t pstride;
+};
+__global__ __launch_bounds__(256) void colsum_multi_kernel(const ColsumJobs J) {
+  const ColsumJob& jb = J.j[blockIdx.z];
+  const int g = blockIdx.y;
+  const int p0 = g * jb.ppg;
+  if (p0 >= jb.nparts) return;   // block-uniform: before any barrier
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int p1 = min(jb.nparts, p0 + jb.ppg);
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  if (c < J.ncols) {
+    int p = p0 + w;
+    for (; p + 28 < p1; p += 32) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += jb.part[(int64_t)(p + 4 * q) * J.pstride + c];
+    }
+    for (; p < p1; p += 4) acc[0] += jb.part[(int64_t)p * J.pstride + c];
+  }
+  const float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < J.ncols)
+    jb.out[(int64_t)g * jb.out_gstride + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+void colsum_multi(const ColsumJob* jobs, int n, int ncols, int64_t pstride, hipStream_t st) {
+  ColsumJobs J{};
+  int gmax = 1;
+  for (int i = 0; i < n; ++i) {
+    J.j[i] = jobs[i];
+    gmax = std::max(gmax, (jobs[i].nparts + jobs[i].ppg - 1) / jobs[i].ppg);
+  }
+  J.ncols = ncols;
+  J.pstride = pstride;
+  hipLaunchKernelGGL(colsum_multi_kernel, dim3((ncols + 63) / 64, gmax, n), dim3(256), 0, st, J);
+}
+
+// Stage 1 of a long column sum (bias gradients: rows = tokens): a block owns
+// 512 bf16 (256 fp32) columns as 16-byte row pieces, one per lane (a wave
+// reads 1 KiB of a row per instruction), 4 waves striding a 128-row chunk
+// with 4 rows in flight per lane; fixed-order combine of the waves in LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_rows_kernel(const T* __restrict__ in, int rows, int cols,
+                                                          int64_t ld, int rchunk, float* __restrict__ part) {
+  constexpr int EPL = 16 / (int)sizeof(T);   // columns per lane
+  constexpr int CB = 64 * EPL;               // columns per block
+  __shared__ float red[4][CB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * CB + lane * EPL;
+  const int r0 = blockIdx.y * rchunk, r1 = min(rows, r0 + rchunk);
+  float acc[EPL];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
+  auto add = [&](const uint4 v) {
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[2 * q] += __uint_as_float(x[q] << 16);
+        acc[2 * q + 1] += __uint_as_float(x[q] & 0xffff0000u);
+      }
+    } else {
+      acc[0] += __uint_as_float(v.x); acc[1] += __uint_as_float(v.y);
+      acc[2] += __uint_as_float(v.z); acc[3] += __uint_as_float(v.w);
+    }
+  };
+  if (c < cols) {
+    int r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      uint4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const uint4*>(in + (int64_t)(r + 4 * q) * ld + c);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) add(v[q]);
+    }
+    for (; r < r1; r += 4) add(*reinterpret_cast<const uint4*>(in + (int64_t)r * ld + c));
+  }
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) red[w][lane * EPL + e] = acc[e];
+  __syncthreads();
+  for (int q = threadIdx.x; q < CB; q += 256) {
+    const int cc = blockIdx.x * CB + q;
+    if (cc < cols) part[(int64_t)blockIdx.y * cols + cc] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+  }
+}
+
 }  // namespace mtts
 
 extern "C" int64_t mtts_colsum_workspace(int rows, int cols, int rows_per_group) {
-  if (rows_per_group <= 1024) return 0;
-  const int64_t chunks = (int64_t)(rows + 255) / 256;
+  if (rows_per_group <= 1024 && !(rows_per_group >= rows && rows > 1024)) return 0;
+  const int64_t chunks = (int64_t)(rows + 127) / 128;   // the 128-row single-group path needs the most
   return chunks * cols * 4 + 256;
 }
 
@@ -56,6 +151,26 @@ extern "C" int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_
   hipStream_t st = (hipStream_t)stream;
   if (rows == 0) {
     (void)hipMemsetAsync(out, 0, (size_t)cols * 4, st);
+    return MTTS_OK;
+  }
+  const int es = dtype == MTTS_F32 ? 4 : 2;
+  if (rows_per_group >= rows && rows > 1024 && cols % (16 / es) == 0 && row_stride % (16 / es) == 0 &&
+      (uintptr_t)in % 16 == 0) {
+    // one group over many rows (bias gradients): 16-byte row pieces, 128-row
+    // chunks -> fp32 partial slab -> sum of the chunks
+    MTTS_CHECK(workspace, "colsum: workspace required (mtts_colsum_workspace)");
+    const int rchunk = 128;
+    const int chunks = (rows + rchunk - 1) / rchunk;
+    float* part = (float*)workspace;
+    if (dtype == MTTS_F32)
+      hipLaunchKernelGGL(colsum_rows_kernel<float>, dim3((cols + 255) / 256, chunks), dim3(256), 0, st,
+                         (const float*)in, rows, cols, row_stride, rchunk, part);
+    else
+      hipLaunchKernelGGL(colsum_rows_kernel<bf16_t>, dim3((cols + 511) / 512, chunks), dim3(256), 0, st,
+                         (const bf16_t*)in, rows, cols, row_stride, rchunk, part);
+    MTTS_LAUNCH_CHECK("colsum rows");
+    colsum(part, chunks, chunks, cols, cols, out, out_gstride, st);
+    MTTS_LAUNCH_CHECK("colsum chunks");
     return MTTS_OK;
   }
   if (rows_per_group > 1024) {

@@ -53,14 +53,17 @@ class MambaInnerFn(torch.autograd.Function):
         y, last, ckpt = ops.scan_fwd(u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, want_last=True, want_ckpt=need)
         if need:
             ctx.save_for_backward(xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt,
-                                  conv_state_in, h0)
+                                  conv_state_in, h0, A)
         ctx.mark_non_differentiable(conv_state, last)
+        ctx.set_materialize_grads(False)   # no zero-filled grads for the unused state outputs
         return y, conv_state, last
 
     @staticmethod
     def backward(ctx, dy, _dconv, _dlast):
         (xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt,
-         conv_state_in, h0) = ctx.saved_tensors
+         conv_state_in, h0, A) = ctx.saved_tensors
+        if dy is None:   # grads are not materialised: y unused downstream
+            dy = torch.zeros(xz.shape[:-1] + (xz.shape[-1] // 2,), device=xz.device, dtype=xz.dtype)
         cd = u.dtype
         Wx, Wdt = cast_weight(W_x, cd), cast_weight(W_dt, cd)
         di = xz.shape[-1] // 2
@@ -69,7 +72,6 @@ class MambaInnerFn(torch.autograd.Function):
         Bsz, Ln, _ = xz.shape
         x, z = xz[..., :di], xz[..., di:]
         dt, Bm, Cm = x_dbl[..., :r], x_dbl[..., r:r + N], x_dbl[..., r + N:]
-        A = -torch.exp(A_log.float())
         dxz = torch.empty_like(xz)
         dx_dbl = torch.empty(Bsz, Ln, r + 2 * N, device=xz.device, dtype=torch.float32)
         need_dh0 = h0 is not None and ctx.needs_input_grad[9]
