@@ -38,9 +38,12 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_kernel(const MttsLNArgs 
       T* xs = (T*)a.x_sum + (int64_t)row * a.xsum_rs;
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        // round to the storage dtype so fwd/bwd see the same stream value
+        // round to the storage dtype (in registers) so fwd/bwd see the same stream value
         st_vec<T, VEC>(xs + (k * 64 + lane) * VEC, v[k]);
-        ld_vec<T, VEC>(xs + (k * 64 + lane) * VEC, v[k]);
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) v[k][q] = bf2f(f2bf(v[k][q]));
+        }
       }
     }
   }

@@ -1,0 +1,36 @@
+"""Causal conv1d fwd / bwd at the C2 shape (B=8, L=2048, d_inner=2048 bf16,
+x a strided view of xz as in the decoder): time and HBM rate."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mamba-tts-project_amd")]
+import torch  # noqa: E402
+from mtts import ops  # noqa: E402
+
+B, L, D = 8, 2048, 2048
+xz = torch.randn(B, L, 2 * D, device="cuda").to(torch.bfloat16)
+x = xz[..., :D]
+w = torch.randn(D, 1, 4, device="cuda") * 0.3
+bias = torch.randn(D, device="cuda") * 0.1
+du = torch.randn(B, L, D, device="cuda").to(torch.bfloat16)
+dxz = torch.empty_like(xz)
+
+
+def t(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / it * 1e3
+
+
+tf = t(lambda: ops.conv_fwd(x, w, bias, True))
+tb = t(lambda: ops.conv_bwd(x, w, bias, du, True, dx=dxz[..., :D]))
+n = B * L * D * 2
+print(f"conv fwd {tf:.1f} us ({2 * n / tf / 1e3:.0f} GB/s)   bwd {tb:.1f} us ({3 * n / tb / 1e3:.0f} GB/s)")
