@@ -74,6 +74,7 @@ struct GemmParams {
   int group;             // tile rows per L2 group
   int epi;               // MTTS_GEMM_EPI_*
   int bias_bf16;
+  int wide_out;          // bf16 out (and aux) rows 16-byte aligned: dwordx4 epilogue
   float beta;
 };
 
@@ -398,6 +399,93 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   const int rl = lane & 15, cl = 4 * (lane >> 4);
   // wave-uniform: the wave's whole 128x64 sub-tile in bounds (no per-lane masks)
   const bool full = m0 + wr * 128 + 128 <= p.m && n0 + wc * 64 + 64 <= p.n;
+  if constexpr (!OUT_F32) {
+   if (p.wide_out) {
+    // bf16 out: the 16-lane rows g and g^1 of the wave hold adjacent 4-column
+    // groups of the same output rows; one v_permlane16_swap per dword of a
+    // (NB, NB+1) pair gives each lane 8 consecutive columns, so the tile
+    // leaves as 16 dwordx4 stores per lane instead of 32 dwordx2 (the store
+    // tail is issue-bound: cdna_hip_programming.md T21).  After the swap the
+    // even rows hold block 2pr columns 8(g>>1)..+7, the odd rows block 2pr+1.
+    const int g = lane >> 4;
+    const int cw0 = n0 + wc * 64 + (g & 1) * 16 + 8 * (g >> 1);
+#pragma unroll
+    for (int MB = 0; MB < 8; ++MB) {
+      const int row = m0 + wr * 128 + MB * 16 + rl;
+      if (!full && row >= p.m) continue;   // rows g and g^1 share `row`: the swap partners skip together
+      uint32_t o2[4][2], h2[4][2];
+#pragma unroll
+      for (int NB = 0; NB < 4; ++NB) {
+        const int col = n0 + wc * 64 + NB * 16 + cl;
+        const bool cok = full || col < p.n;   // n % 8 == 0: a lane's 4 columns are all in or all out
+        f32x4 v = acc[MB][NB];
+        if (EPI & MTTS_GEMM_EPI_BIAS) {
+          float bb[4] = {0.f, 0.f, 0.f, 0.f};
+          if (cok) {
+            if (p.bias_bf16) {
+              const uint2 raw = *(const uint2*)((const bf16_t*)p.bias + col);
+              bb[0] = __uint_as_float(raw.x << 16); bb[1] = __uint_as_float(raw.x & 0xffff0000u);
+              bb[2] = __uint_as_float(raw.y << 16); bb[3] = __uint_as_float(raw.y & 0xffff0000u);
+            } else {
+              const f32x4 b4 = *(const f32x4*)((const float*)p.bias + col);
+              bb[0] = b4[0]; bb[1] = b4[1]; bb[2] = b4[2]; bb[3] = b4[3];
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += bb[j];
+        }
+        bf16_t o[4];
+        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
+          bf16_t hpre[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hpre[j] = f2bf(v[j]);
+            o[j] = f2bf(gelu_f(bf2f(hpre[j])));
+          }
+          h2[NB][0] = hpre[0] | ((uint32_t)hpre[1] << 16);
+          h2[NB][1] = hpre[2] | ((uint32_t)hpre[3] << 16);
+        } else if constexpr ((EPI & MTTS_GEMM_EPI_DGELU) != 0) {
+          uint2 raw = make_uint2(0, 0);
+          if (cok) raw = *(const uint2*)((const bf16_t*)p.aux + (int64_t)row * p.ld_aux + col);
+          const float h[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
+                              __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(h[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+        }
+        o2[NB][0] = o[0] | ((uint32_t)o[1] << 16);
+        o2[NB][1] = o[2] | ((uint32_t)o[3] << 16);
+      }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto r = __builtin_amdgcn_permlane16_swap(o2[2 * pr][d], o2[2 * pr + 1][d], false, false);
+          w[d] = r[0];
+          w[2 + d] = r[1];
+        }
+        const int cw = cw0 + pr * 32;
+        if (full || cw < p.n) {
+          *(uint4*)((bf16_t*)p.c + (int64_t)row * p.ldc + cw) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto r = __builtin_amdgcn_permlane16_swap(h2[2 * pr][d], h2[2 * pr + 1][d], false, false);
+            w[d] = r[0];
+            w[2 + d] = r[1];
+          }
+          if (full || cw < p.n)
+            *(uint4*)((bf16_t*)p.aux + (int64_t)row * p.ld_aux + cw) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+    }
+    return;
+   }
+  }
 #pragma unroll
   for (int MB = 0; MB < 8; ++MB) {
     const int row = m0 + wr * 128 + MB * 16 + rl;
@@ -532,6 +620,8 @@ extern "C" int mtts_gemm(const MttsGemmArgs* a, void* stream) {
   } else {
     p.c = a->c; p.ldc = a->ldc; p.split_stride = 0; p.beta = a->beta;
   }
+  p.wide_out = !f32out && a->ldc % 8 == 0 && (!(epi & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) || a->ld_aux % 8 == 0) &&
+               (!a->aux || (uintptr_t)a->aux % 16 == 0) && !getenv("MTTS_GEMM_NARROW_OUT");
   const int nwg = p.tiles_m * p.tiles_n * splits;
   hipStream_t st = (hipStream_t)stream;
   if (!nt) {
