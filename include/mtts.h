@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 2
+#define MTTS_ABI_VERSION 3
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -443,9 +443,25 @@ typedef struct {
   int kgroups;
   float* splitk_slab;
   int* splitk_count;
+  /* w_packed = 1: W is mtts_pack_rows_weight's image of the (N, K) weight
+   * (ldw ignored, kgroups must be <= 1): one 16-column tile per workgroup,
+   * the K range over up to 8 waves, every weight load a coalesced KiB
+   * (csrc/gemv.hip).  Needs K / 32 = KS * S, KS <= 8 a power of 2,
+   * S in {1, 2, 4, 8, 16}; the fusions above all apply, LayerNorm at any
+   * such K. */
+  int w_packed;
 } MttsRowsArgs;
 
 int mtts_gemm_rows(const MttsRowsArgs* a, void* stream);
+
+/* Packed image of a bf16 decode weight W (N, K), row stride ldw (K % 64 == 0,
+ * 16-byte aligned): for 16-column tile t and k-step s, the 64 lanes'
+ * v_mfma_f32_16x16x32_bf16 A fragments W[16t + l%16][32s + 8(l/16) .. +8]
+ * are one contiguous KiB; rows past N are zero.  out holds
+ * mtts_pack_rows_bytes(N, K) bytes (16-byte aligned).  Made once per decode
+ * context (DecodeEngine), stream-ordered. */
+int64_t mtts_pack_rows_bytes(int N, int K);
+int mtts_pack_rows_weight(const void* W, int64_t ldw, int N, int K, void* out, void* stream);
 
 
 /* ------------------------------------------------------------------------

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -73,7 +73,8 @@ class RowsArgs(C.Structure):
                 ("x", vp), ("W", vp), ("bias", vp), ("y", vp),
                 ("conv_dim", i32), ("conv_state", vp), ("conv_w", vp), ("conv_b", vp), ("u", vp), ("ldu", i64),
                 ("ln_w", vp), ("ln_b", vp), ("ln_eps", f32), ("gamma", vp), ("beta", vp), ("ld_gb", i64),
-                ("res", vp), ("ld_res", i64), ("kgroups", i32), ("splitk_slab", vp), ("splitk_count", vp)]
+                ("res", vp), ("ld_res", i64), ("kgroups", i32), ("splitk_slab", vp), ("splitk_count", vp),
+                ("w_packed", i32)]
 
 
 class GemmArgs(C.Structure):
@@ -131,6 +132,8 @@ _SIGS = {
     "mtts_selective_state_update": ([C.POINTER(StateUpdateArgs), vp], i32),
     "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
     "mtts_gemm_rows": ([C.POINTER(RowsArgs), vp], i32),
+    "mtts_pack_rows_bytes": ([i32, i32], i64),
+    "mtts_pack_rows_weight": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_gemm_workspace": ([C.POINTER(GemmArgs)], i64),
     "mtts_gemm": ([C.POINTER(GemmArgs), vp], i32),
     "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),

@@ -822,9 +822,87 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(MttsAttnFwdArgs a) {
   }
 }
 
+// Short key sides (kv_len <= U * 256 / (HD / 8); C4's 128 text keys): every
+// key of the (batch, head) in registers at once, so the softmax needs no
+// online rescaling: scores -> block max (wave shuffles + 4 LDS words) ->
+// p = exp2(s - max) -> P.V and sum(p) reduced over the wave's groups by
+// shuffles and over the 4 waves through LDS (fixed order).  All loads are
+// unconditional (clamped key index, masked afterwards).
+template <typename T, int HD, int U>
+__global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
+  constexpr int G = HD / 8, NG = 256 / G;
+  __shared__ float swm[4], swl[4], sacc[4][HD];
+  const int bh = blockIdx.x, b = bh / a.heads, hh = bh % a.heads;
+  const int g = threadIdx.x / G, gl = threadIdx.x % G, d0 = gl * 8, wave = threadIdx.x >> 6;
+  const float c = a.scale * kLog2e;
+  float q[8];
+  ld8((const T*)a.q + b * a.q_bs + hh * HD + d0, q);
+  const T* kb = (const T*)a.k + b * a.k_bs + hh * HD + d0;
+  const T* vb = (const T*)a.v + b * a.v_bs + hh * HD + d0;
+  const uint8_t* mb = a.key_padding_mask ? a.key_padding_mask + b * a.mask_bs : (const uint8_t*)a.q;
+  const uint32_t mmask = a.key_padding_mask ? 0xffu : 0u;
+  float kx[U][8], vx[U][8];
+  bool ok[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = g + u * NG;
+    const int jj = j < a.kv_len ? j : 0;
+    ld8(kb + (int64_t)jj * a.k_ls, kx[u]);
+    ld8(vb + (int64_t)jj * a.v_ls, vx[u]);
+    ok[u] = j < a.kv_len && ((uint32_t)mb[a.key_padding_mask ? jj : 0] & mmask) == 0;
+  }
+  float sc[U], m = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float sv = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sv = fmaf(q[e], kx[u][e], sv);
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) sv += __shfl_xor(sv, o);
+    sc[u] = ok[u] ? sv * c : -INFINITY;
+    m = fmaxf(m, sc[u]);
+  }
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) swm[wave] = m;
+  __syncthreads();
+  const float M = fmaxf(fmaxf(swm[0], swm[1]), fmaxf(swm[2], swm[3]));
+  float l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float p = ok[u] ? exp2f(sc[u] - M) : 0.f;
+    l += p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, vx[u][e], acc[e]);
+  }
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1) {
+    l += __shfl_xor(l, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], o);
+  }
+  if ((threadIdx.x & 63) < G) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sacc[wave][d0 + e] = acc[e];
+    if (gl == 0) swl[wave] = l;
+  }
+  __syncthreads();
+  if (threadIdx.x < HD) {
+    const float L = (swl[0] + swl[1]) + (swl[2] + swl[3]);
+    const float o = (sacc[0][threadIdx.x] + sacc[1][threadIdx.x]) + (sacc[2][threadIdx.x] + sacc[3][threadIdx.x]);
+    // fully masked: L = 0 -> 0/0 = NaN (torch MHA), lse = -inf
+    mtts::stf((T*)a.out + b * a.o_bs + hh * HD + threadIdx.x, o / L);
+    if (a.lse && threadIdx.x == 0) a.lse[(int64_t)b * a.heads + hh] = M == -INFINITY ? -INFINITY : (M + log2f(L)) * kLn2;
+  }
+}
+
 template <typename T, int HD>
 void launch_decode(const MttsAttnFwdArgs* a, hipStream_t st) {
-  hipLaunchKernelGGL((attn_decode_kernel<T, HD>), dim3(a->batch * a->heads), dim3(256), 0, st, *a);
+  constexpr int NG = 256 / (HD / 8);
+  const dim3 grid(a->batch * a->heads);
+  if (a->kv_len <= 4 * NG) hipLaunchKernelGGL((attn_decode1_kernel<T, HD, 4>), grid, dim3(256), 0, st, *a);
+  else if (a->kv_len <= 8 * NG) hipLaunchKernelGGL((attn_decode1_kernel<T, HD, 8>), grid, dim3(256), 0, st, *a);
+  else hipLaunchKernelGGL((attn_decode_kernel<T, HD>), grid, dim3(256), 0, st, *a);
 }
 
 template <typename T>

@@ -41,6 +41,9 @@ void colsum_multi(const ColsumJob* jobs, int n, int ncols, int64_t pstride, hipS
     }                                                                         \
   } while (0)
 
+// decode projections on packed weights (gemv.hip), called by mtts_gemm_rows
+int launch_gemv_packed(const MttsRowsArgs* a, hipStream_t st);
+
 // ---------------------------------------------------------------- dtypes
 typedef uint16_t bf16_t;
 

@@ -309,7 +309,7 @@ extern "C" int mtts_gemm_rows(const MttsRowsArgs* a, void* stream) {
   MTTS_CHECK(M >= 0 && M <= 32 && N > 0 && K > 0, "gemm_rows: M=%d must be in [0, 32], N, K > 0", M);
   MTTS_CHECK(K % 64 == 0, "gemm_rows: K=%d must be a multiple of 64", K);
   MTTS_CHECK(a->act == 0 || a->act == 1, "gemm_rows: act must be 0 (none) or 1 (gelu)");
-  MTTS_CHECK(((uintptr_t)a->x | (uintptr_t)a->W) % 16 == 0 && a->ldx % 8 == 0 && a->ldw % 8 == 0,
+  MTTS_CHECK(((uintptr_t)a->x | (uintptr_t)a->W) % 16 == 0 && a->ldx % 8 == 0 && (a->w_packed || a->ldw % 8 == 0),
              "gemm_rows: x / W must be 16-byte aligned with 16-byte row strides");
   MTTS_CHECK(a->conv_dim >= 0 && a->conv_dim <= N && a->conv_dim % 32 == 0,
              "gemm_rows: conv_dim=%d must be a multiple of 32 in [0, N]", a->conv_dim);
@@ -323,6 +323,11 @@ extern "C" int mtts_gemm_rows(const MttsRowsArgs* a, void* stream) {
                "gemm_rows: LayerNorm prologue operands must be 16-byte aligned");
   }
   MTTS_CHECK(!a->res || a->conv_dim == 0, "gemm_rows: residual and conv epilogues are exclusive");
+  if (a->w_packed) {
+    MTTS_CHECK(a->kgroups <= 1, "gemm_rows: packed weights take no split-K");
+    if (M == 0) return MTTS_OK;
+    return launch_gemv_packed(a, (hipStream_t)stream);
+  }
   if (M == 0) return MTTS_OK;
   hipStream_t st = (hipStream_t)stream;
   const int tiles = (N + 31) / 32;

@@ -129,6 +129,20 @@ class DecodeEngine:
                 return False
         return m.norm_out.weight.dtype == torch.float32
 
+    _PACKED = ("Win", "Wx", "Wout", "Wq", "Wo", "W1", "W2")
+
+    def _pack_ctx(self):
+        """Packed (MFMA-fragment order) images of the step's projection
+        weights for csrc/gemv.hip, made once per context; shapes the packed
+        kernel does not take keep the row-major weight."""
+        c = self.ctx
+        for p in c["layers"]:
+            for k in self._PACKED:
+                if ops.gemv_split_ok(p[k].shape[1], ln=k in ("Win", "Wq", "W1")):
+                    p[k + "_p"] = ops.pack_rows_weight(p[k])
+        if ops.gemv_split_ok(c["Wh"].shape[1], ln=True):
+            c["Wh_p"] = ops.pack_rows_weight(c["Wh"])
+
     # -- one step, fused epilogues (bf16, <= 32 sequences) ---------------------
     def _step_rows(self, tok, pos, states):
         """Per layer, 9 launches and no LayerNorm kernel (csrc/rows.hip):
@@ -146,26 +160,30 @@ class DecodeEngine:
         def ln(norm, gamma=None, beta=None):
             return (norm.weight, norm.bias, norm.eps, gamma, beta)
 
+        def w(p, k):   # packed image when there is one (csrc/gemv.hip)
+            return p.get(k + "_p", p[k])
+
         fuse_conv = os.environ.get("MTTS_DECODE_FUSE_CONV", "1") != "0"
         for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
             conv_state, ssm_state = states[i]
             mm = l.mamba
             di, N, r = mm.d_inner, mm.d_state, mm.dt_rank
             if fuse_conv:
-                xz, u = ops.gemm_rows(x, p["Win"], conv=(conv_state, p["conv_w"], p["conv_b"]), ln=ln(l.norm_mamba))
+                xz, u = ops.gemm_rows(x, w(p, "Win"), conv=(conv_state, p["conv_w"], p["conv_b"]),
+                                      ln=ln(l.norm_mamba))
             else:
-                xz = ops.gemm_rows(x, p["Win"], ln=ln(l.norm_mamba))
+                xz = ops.gemm_rows(x, w(p, "Win"), ln=ln(l.norm_mamba))
                 u = ops.conv_update(xz[:, :di], conv_state, p["conv_w"], p["conv_b"], True)
-            x_dbl = ops.gemm_rows(u, p["Wx"])
+            x_dbl = ops.gemm_rows(u, w(p, "Wx"))
             y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
                                  xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"])
-            x = ops.gemm_rows(y, p["Wout"], res=x)
-            q = ops.gemm_rows(x, p["Wq"], p["bq"], ln=ln(l.norm_cross))
+            x = ops.gemm_rows(y, w(p, "Wout"), res=x)
+            q = ops.gemm_rows(x, w(p, "Wq"), p["bq"], ln=ln(l.norm_cross))
             o = attention(q[:, None], p["k"], p["v"], l.cross_attn.num_heads, c["kpm"])[:, 0]
-            x = ops.gemm_rows(o, p["Wo"], p["bo"], res=x)
-            f = ops.gemm_rows(x, p["W1"], p["b1"], "gelu", ln=ln(l.norm_ff, p["gamma"], p["beta"]))
-            x = ops.gemm_rows(f, p["W2"], p["b2"], res=x)
-        return ops.gemm_rows(x, c["Wh"], c["bh"], ln=ln(m.norm_out))[:, None]
+            x = ops.gemm_rows(o, w(p, "Wo"), p["bo"], res=x)
+            f = ops.gemm_rows(x, w(p, "W1"), p["b1"], "gelu", ln=ln(l.norm_ff, p["gamma"], p["beta"]))
+            x = ops.gemm_rows(f, w(p, "W2"), p["b2"], res=x)
+        return ops.gemm_rows(x, w(c, "Wh"), c["bh"], ln=ln(m.norm_out))[:, None]
 
     # -- one step, eager -----------------------------------------------------
     def _step(self, tok, pos, states):
@@ -214,6 +232,8 @@ class DecodeEngine:
             self.ctx_refs = conds                  # strong references (see _same_ctx)
             self.ctx_versions = tuple(None if t is None else t._version for t in conds)
             self.fused = self._fused_ok(cd, last_token.shape[0])
+            if self.fused and os.environ.get("MTTS_DECODE_PACKED", "1") != "0":
+                self._pack_ctx()
             self.graph = None
             self.states = None
         B = last_token.shape[0]

@@ -497,8 +497,55 @@ def length_regulate(hidden, durations, max_len=None):
 GEMM_ROWS_MAX = 32
 
 
+class PackedRows:
+    """A bf16 decode weight (N, K) re-laid by mtts_pack_rows_weight into
+    MFMA-fragment order (csrc/gemv.hip): every weight load of the packed
+    projection kernel is one coalesced KiB.  `data` is the packed image."""
+
+    __slots__ = ("data", "N", "K", "dtype")
+
+    def __init__(self, data, N, K):
+        self.data, self.N, self.K, self.dtype = data, N, K, torch.bfloat16
+
+    @property
+    def shape(self):
+        return (self.N, self.K)
+
+
+def gemv_split_ok(K, ln=False):
+    """K values the packed kernel takes: K / 32 = KS * S, KS <= 8 a power
+    of two, S in {1, 2, 4, 8, 16}; with the LayerNorm prologue K <= 2048
+    (host mirror of gemv_split / launch_gemv_packed)."""
+    if ln and K > 2048:
+        return False
+    if K <= 0 or K % 64:
+        return False
+    n, ks = K // 32, 1
+    while ks < 8 and n % (2 * ks) == 0:
+        ks *= 2
+    return n // ks in (1, 2, 4, 8, 16)
+
+
+def pack_rows_weight(w):
+    """PackedRows image of a contiguous-rows bf16 weight (N, K) (one launch)."""
+    _check_cuda(w)
+    if w.dtype != torch.bfloat16 or w.dim() != 2 or w.stride(1) != 1:
+        raise ValueError("pack_rows_weight: weight must be 2-D bf16 with unit column stride")
+    N, K = w.shape
+    if not gemv_split_ok(K):
+        raise ValueError(f"pack_rows_weight: K={K} unsupported by the packed kernel")
+    nbytes = L.lib().mtts_pack_rows_bytes(N, K)
+    out = torch.empty(nbytes // 2, device=w.device, dtype=torch.bfloat16)
+    L.call_raw("mtts_pack_rows_weight", w.data_ptr(), w.stride(0), N, K, out.data_ptr())
+    return PackedRows(out, N, K)
+
+
 def gemm_rows_ok(x, weight):
     """True when mtts_gemm_rows_bf16 takes y = x @ weight.t() as given."""
+    if isinstance(weight, PackedRows):
+        return (x.dtype == torch.bfloat16 and x.dim() == 2 and 0 < x.shape[0] <= GEMM_ROWS_MAX
+                and x.shape[1] == weight.K and x.stride(1) == 1 and x.stride(0) % 8 == 0
+                and x.data_ptr() % 16 == 0)
     return (x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and x.dim() == 2
             and 0 < x.shape[0] <= GEMM_ROWS_MAX and x.shape[1] % 64 == 0 and x.stride(1) == 1
             and weight.stride(1) == 1 and x.stride(0) % 8 == 0 and weight.stride(0) % 8 == 0
@@ -560,10 +607,11 @@ def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
         the fly, exactly as ops.layer_norm would produce it.
     res: (M, N) bf16; y = bf16(y + res) (the residual stream after the add).
     """
-    _check_cuda(x, weight, bias)
+    packed = isinstance(weight, PackedRows)
+    _check_cuda(x, weight.data if packed else weight, bias)
     if not gemm_rows_ok(x, weight):
         raise ValueError(f"gemm_rows: unsupported operands x{tuple(x.shape)}/{x.stride()} "
-                         f"w{tuple(weight.shape)}/{weight.stride()} {x.dtype}")
+                         f"w{tuple(weight.shape)}/{'packed' if packed else weight.stride()} {x.dtype}")
     M, K = x.shape
     N = weight.shape[0]
     if weight.shape[1] != K:
@@ -576,8 +624,9 @@ def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     a = L.RowsArgs()
     a.M, a.N, a.K, a.act = M, N, K, {None: 0, "gelu": 1}[act]
-    a.ldx, a.ldw, a.ldy = x.stride(0), weight.stride(0), y.stride(0)
-    a.x, a.W, a.bias, a.y = x.data_ptr(), weight.data_ptr(), L.ptr(bias), y.data_ptr()
+    a.ldx, a.ldw, a.ldy = x.stride(0), 0 if packed else weight.stride(0), y.stride(0)
+    a.x, a.W, a.bias, a.y = x.data_ptr(), (weight.data if packed else weight).data_ptr(), L.ptr(bias), y.data_ptr()
+    a.w_packed = int(packed)
     out = [y]
     if conv is not None:
         cs, cw, cb = conv
@@ -602,7 +651,7 @@ def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
         if res.dtype != torch.bfloat16 or res.shape != (M, N) or res.stride(1) != 1:
             raise ValueError("gemm_rows: res must be (M, N) bf16 with unit column stride")
         a.res, a.ld_res = res.data_ptr(), res.stride(0)
-    kg = rows_kgroups(N, K, ln is not None)
+    kg = 1 if packed else rows_kgroups(N, K, ln is not None)
     if kg > 1:
         slab, cnt = rows_workspace(dev)
         a.kgroups, a.splitk_slab, a.splitk_count = kg, slab.data_ptr(), cnt.data_ptr()

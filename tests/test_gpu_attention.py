@@ -63,6 +63,12 @@ CASES = [  # B, T, S, H, hd
     (2, 1, 5, 2, 32),
     (1, 1, 300, 2, 64),
     (32, 1, 1000, 8, 128),
+    # single-pass decode kernel (attn_decode1_kernel, all keys in registers): U = 4 and 8
+    (32, 1, 128, 16, 64),
+    (4, 1, 200, 4, 64),
+    (2, 1, 60, 2, 128),
+    (3, 1, 100, 2, 128),
+    (2, 1, 33, 4, 16),
 ]
 
 
@@ -83,6 +89,21 @@ def test_forward_matches_reference(case, dtype):
 def test_fully_masked_rows_are_nan_and_others_exact():
     from mtts import attn_kernels as A
     B, T, S, H, hd = 3, 40, 24, 4, 16
+    q, kv, kpm = make(B, T, S, H, hd, torch.float32, full_mask_batch=1)
+    d = H * hd
+    out, lse = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+    assert torch.isnan(out[1]).all()
+    assert torch.isinf(lse[1]).all() and (lse[1] < 0).all()
+    ref, _ = ref_attention(q, kv[..., :d], kv[..., d:], H, kpm)
+    close(out[[0, 2]], ref[[0, 2]], 2e-5)
+
+
+@pytest.mark.parametrize("S", [24, 128, 200, 1000])
+def test_decode_fully_masked_rows_are_nan(S):
+    """q_len = 1 (both decode kernels): a fully masked key side gives NaN rows
+    and -inf lse like torch MHA; the other batch rows match the reference."""
+    from mtts import attn_kernels as A
+    B, T, H, hd = 3, 1, 4, 64
     q, kv, kpm = make(B, T, S, H, hd, torch.float32, full_mask_batch=1)
     d = H * hd
     out, lse = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)

@@ -598,3 +598,62 @@ def test_wgrad_split_k_matches_fp64():
     wgrad(dy, x, out=big[1024:2048])
     close(big[1024:2048], ref, rtol=1e-5, name="wgrad row slice")
     assert big[:1024].abs().max().item() == 0 and big[2048:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 4096, 1024), (32, 1024, 2048), (32, 1024, 4096), (32, 96, 2048),
+                                   (32, 10, 1024), (5, 2048, 1024), (3, 800, 512), (17, 64, 64), (16, 48, 192)])
+@pytest.mark.parametrize("mode", ["plain", "ln", "film", "res", "conv", "gelu"])
+def test_gemm_rows_packed_matches_row_major(M, N, K, mode):
+    """Packed decode weights (mtts_pack_rows_weight + csrc/gemv.hip: 16-column
+    tiles, coalesced KiB weight loads, K over up to 8 waves) equal the
+    row-major skinny GEMM up to fp32 summation order (one bf16 rounding,
+    bound 2^-7 relative), bit-identical across repeated launches; the packed
+    image holds exactly the weight's fragments (zero-padded columns)."""
+    from mtts import ops
+    if not ops.gemv_split_ok(K, ln=mode in ("ln", "film")):
+        pytest.skip("K not taken by the packed kernel")
+    g = torch.Generator(device="cpu").manual_seed(M * 3 + N + K + len(mode))
+    x = (torch.randn(M, K, generator=g) * 2 + 0.3).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    wp = ops.pack_rows_weight(w)
+    # the image: tile t, step s, lane l holds W[16t + l%16, 32s + 8(l/16) : +8]
+    Np = -(-N // 16) * 16
+    wpad = torch.zeros(Np, K, device=DEV, dtype=torch.bfloat16)
+    wpad[:N] = w
+    img = wpad.view(Np // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1)
+    assert torch.equal(wp.data, img)
+    kw, act = {}, None
+    if mode in ("ln", "film"):
+        lw, lb = torch.randn(K, generator=g).to(DEV), torch.randn(K, generator=g).to(DEV)
+        gam = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if mode == "film" else None
+        bet = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if mode == "film" else None
+        kw["ln"] = (lw, lb, 1e-5, gam, bet)
+    if mode == "res":
+        kw["res"] = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    if mode == "gelu":
+        act = "gelu"
+    C = (N // 2) // 32 * 32
+    if mode == "conv":
+        if C == 0:
+            pytest.skip("no whole conv tile")
+        st0 = torch.randn(M, C, 4, generator=g).to(DEV)
+        cw, cb = torch.randn(C, 4, generator=g).to(DEV), torch.randn(C, generator=g).to(DEV)
+        outs = []
+        for wt in (w, wp, wp):
+            st = st0.clone()
+            y, u = ops.gemm_rows(x, wt, conv=(st, cw, cb))
+            outs.append((y, u, st))
+    elif "ln" in kw and not ops.gemm_rows_ln_ok(K):   # row-major prologue cannot: LayerNorm kernel + GEMM
+        h, _ = ops.layer_norm(x, kw["ln"][0], kw["ln"][1], 1e-5, gamma=kw["ln"][3], beta=kw["ln"][4],
+                              rows_per_group=1)
+        outs = [(ops.gemm_rows(h, w, b),)] + [(ops.gemm_rows(x, wp, b, **kw),) for _ in range(2)]
+    else:
+        outs = [(ops.gemm_rows(x, wt, b, act, **kw),) for wt in (w, wp, wp)]
+    for a_, c_ in zip(outs[0], outs[1]):
+        close(c_.float(), a_.float(), rtol=2 ** -7, name=f"packed {mode}")
+    for a_, c_ in zip(outs[1], outs[2]):
+        assert torch.equal(a_, c_)
+    if mode == "plain":
+        ref = x.double() @ w.double().t() + b.double()
+        close(outs[1][0], ref, rtol=2 ** -8, name="packed vs float64")

@@ -42,14 +42,13 @@ def shapes():
         x = torch.randn(32, K, device=dev, dtype=torch.bfloat16)
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
         b = torch.randn(N, device=dev, dtype=torch.bfloat16)
-        tr = t_us(lambda: ops.gemm_rows(x, w, b))
-        ops.ROWS_SPLITK = False
+        wp = ops.pack_rows_weight(w)
+        tp = t_us(lambda: ops.gemm_rows(x, wp, b))
         t1 = t_us(lambda: ops.gemm_rows(x, w, b))
-        ops.ROWS_SPLITK = True
         tb = t_us(lambda: torch.addmm(b, x, w.t()))
-        gbs = N * K * 2 / tr / 1e3
-        print(f"N={N:5d} K={K:5d}  rows {tr:6.2f} us ({gbs:6.0f} GB/s, kgroups {ops.rows_kgroups(N, K, False)})  "
-              f"one WG/tile {t1:6.2f} us   hipBLASLt {tb:6.2f} us", flush=True)
+        gbs = N * K * 2 / tp / 1e3
+        print(f"N={N:5d} K={K:5d}  packed {tp:6.2f} us ({gbs:6.0f} GB/s)  rows {t1:6.2f} us   "
+              f"hipBLASLt {tb:6.2f} us", flush=True)
 
 
 def step(modes=(True, False)):
@@ -97,6 +96,13 @@ if __name__ == "__main__":
             os.environ.pop(k)
     if "rowsonly" in what:
         step((True,))
+    if "packed" in what:   # packed-weight projections (csrc/gemv.hip) vs row-major, interleaved
+        for _ in range(2):
+            for pk in ("1", "0"):
+                os.environ["MTTS_DECODE_PACKED"] = pk
+                print("packed", pk, end=" ", flush=True)
+                step((True,))
+        os.environ.pop("MTTS_DECODE_PACKED")
     if "splitk" in what:   # rows kernels with / without the cross-workgroup K split, interleaved
         for _ in range(2):
             for sk in (True, False):
