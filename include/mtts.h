@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 3
+#define MTTS_ABI_VERSION 4
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -192,6 +192,10 @@ typedef struct {
    * dt_w (D, dt_rank) row-major, dtype_io. */
   int dt_rank;
   const void* dt_w;
+  /* optional: out also written as a packed activation image (xpk_index;
+   * batch <= 32, dim % 32 == 0, bf16) for the out_proj projection; out may
+   * then be NULL */
+  void* out_packed;
 } MttsStateUpdateArgs;
 
 int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* stream);
@@ -224,6 +228,12 @@ typedef struct {
 } MttsLNArgs;
 
 int mtts_layernorm_fwd(const MttsLNArgs* a, void* stream);
+
+/* Decode-step LayerNorm(+FiLM) of <= 32 rows straight into the packed
+ * activation image of the next projection (csrc/gemv.hip): y_packed =
+ * image of bf16(LN(x) * w + b [, gamma * . + beta]) (bf16 x, gamma, beta;
+ * rows_per_group 1; cols % 32 == 0; a->y / res / mean / rstd unused). */
+int mtts_layernorm_rows_packed(const MttsLNArgs* a, void* y_packed, void* stream);
 
 /* Backward: dy (M, N) -> dx (M, N) [+= dx_acc if given: dx = dx_acc + LN'],
  * dw, db (N) fp32, dgamma/dbeta (G, N) fp32 (when gamma).  Uses the saved
@@ -281,6 +291,10 @@ typedef struct {
   const uint8_t* key_padding_mask;
   void* out;
   float* lse;                /* may be NULL (inference) */
+  /* q_len == 1 only, optional: out also written as a packed activation
+   * image of (batch, heads * head_dim) (xpk_index; batch <= 32, bf16) for
+   * the output projection; out may then be NULL */
+  void* out_packed;
 } MttsAttnFwdArgs;
 
 int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream);
@@ -450,6 +464,18 @@ typedef struct {
    * S in {1, 2, 4, 8, 16}; the fusions above all apply, LayerNorm at any
    * such K. */
   int w_packed;
+  /* Packed activations (csrc/common.h xpk_index: the B-fragment order of the
+   * packed kernel, 32 * K elements, M <= 32, K % 32 == 0):
+   *  x_packed = 1: x is such an image (ldx ignored; w_packed required)
+   *                -> coalesced KiB operand loads; with the LayerNorm
+   *                prologue the FiLM gamma / beta are images too (ld_gb
+   *                ignored);
+   *  y_packed != NULL: y is also written as an image of (M, N) (N % 32 == 0;
+   *                y may then be NULL), for the next projection;
+   *  u_packed != NULL: u of the conv epilogue also written as an image. */
+  int x_packed;
+  void* y_packed;
+  void* u_packed;
 } MttsRowsArgs;
 
 int mtts_gemm_rows(const MttsRowsArgs* a, void* stream);

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -65,7 +65,7 @@ class StateUpdateArgs(C.Structure):
                 ("dt_softplus", i32),
                 ("x_bs", i64), ("dt_bs", i64), ("z_bs", i64), ("out_bs", i64), ("B_bs", i64), ("C_bs", i64),
                 ("state", vp), ("x", vp), ("dt", vp), ("A", vp), ("Bm", vp), ("Cm", vp), ("D", vp), ("z", vp),
-                ("dt_bias", vp), ("out", vp), ("dt_rank", i32), ("dt_w", vp)]
+                ("dt_bias", vp), ("out", vp), ("dt_rank", i32), ("dt_w", vp), ("out_packed", vp)]
 
 
 class RowsArgs(C.Structure):
@@ -74,7 +74,7 @@ class RowsArgs(C.Structure):
                 ("conv_dim", i32), ("conv_state", vp), ("conv_w", vp), ("conv_b", vp), ("u", vp), ("ldu", i64),
                 ("ln_w", vp), ("ln_b", vp), ("ln_eps", f32), ("gamma", vp), ("beta", vp), ("ld_gb", i64),
                 ("res", vp), ("ld_res", i64), ("kgroups", i32), ("splitk_slab", vp), ("splitk_count", vp),
-                ("w_packed", i32)]
+                ("w_packed", i32), ("x_packed", i32), ("y_packed", vp), ("u_packed", vp)]
 
 
 class GemmArgs(C.Structure):
@@ -101,7 +101,8 @@ class AttnFwdArgs(C.Structure):
                 ("dtype", i32), ("scale", f32),
                 ("q_bs", i64), ("q_ls", i64), ("k_bs", i64), ("k_ls", i64), ("v_bs", i64), ("v_ls", i64),
                 ("o_bs", i64), ("o_ls", i64), ("mask_bs", i64),
-                ("q", vp), ("k", vp), ("v", vp), ("key_padding_mask", vp), ("out", vp), ("lse", vp)]
+                ("q", vp), ("k", vp), ("v", vp), ("key_padding_mask", vp), ("out", vp), ("lse", vp),
+                ("out_packed", vp)]
 
 
 class AttnBwdArgs(C.Structure):
@@ -133,6 +134,7 @@ _SIGS = {
     "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
     "mtts_gemm_rows": ([C.POINTER(RowsArgs), vp], i32),
     "mtts_pack_rows_bytes": ([i32, i32], i64),
+    "mtts_layernorm_rows_packed": ([C.POINTER(LNArgs), vp, vp], i32),
     "mtts_pack_rows_weight": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_gemm_workspace": ([C.POINTER(GemmArgs)], i64),
     "mtts_gemm": ([C.POINTER(GemmArgs), vp], i32),

@@ -63,6 +63,25 @@ def _mask_u8(kpm, B, S):
     return kpm.view(torch.uint8)
 
 
+def attention_decode_packed(q, k, v, n_heads, kpm=None):
+    """Single-query attention (q (B, d), decode step) returning the output
+    as the packed activation image of the output projection (ops.PackedAct;
+    csrc/attn.hip single-pass decode kernel)."""
+    from .ops import PackedAct
+    B, d = q.shape
+    q3 = q[:, None]
+    k, v = _prep(k), _prep(v)
+    if not _aligned(q3):
+        q3 = q3.contiguous()
+    m = _mask_u8(kpm, B, k.shape[1])
+    out = torch.empty(B, 1, d, device=q.device, dtype=q.dtype)
+    yp = PackedAct.empty(B, d, q.device)
+    a = _fwd_args(q3, k, v, n_heads, m, out, None)
+    a.out_packed = yp.data.data_ptr()
+    L.call("mtts_attention_fwd", a)
+    return yp
+
+
 def attention_fwd(q, k, v, n_heads, kpm=None, want_lse=False):
     """Returns (out (B, T, d) in q's dtype, lse (B, H, T) fp32 or None)."""
     for t in (q, k, v):

@@ -891,7 +891,10 @@ __global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
     const float L = (swl[0] + swl[1]) + (swl[2] + swl[3]);
     const float o = (sacc[0][threadIdx.x] + sacc[1][threadIdx.x]) + (sacc[2][threadIdx.x] + sacc[3][threadIdx.x]);
     // fully masked: L = 0 -> 0/0 = NaN (torch MHA), lse = -inf
-    mtts::stf((T*)a.out + b * a.o_bs + hh * HD + threadIdx.x, o / L);
+    if (a.out) mtts::stf((T*)a.out + b * a.o_bs + hh * HD + threadIdx.x, o / L);
+    if constexpr (sizeof(T) == 2) {   // packed activation image for the output projection
+      if (a.out_packed) ((mtts::bf16_t*)a.out_packed)[mtts::xpk_index(b, hh * HD + threadIdx.x)] = mtts::f2bf(o / L);
+    }
     if (a.lse && threadIdx.x == 0) a.lse[(int64_t)b * a.heads + hh] = M == -INFINITY ? -INFINITY : (M + log2f(L)) * kLn2;
   }
 }
@@ -1010,6 +1013,11 @@ void dispatch_bwd(const BwdParams& p, bool split, hipStream_t st) {
 extern "C" int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream) {
   int rc = check_fwd(a, "attention_fwd");
   if (rc) return rc;
+  // the packed image is written by the single-pass decode kernel only
+  MTTS_CHECK(!a->out_packed || (a->q_len == 1 && a->dtype == MTTS_BF16 && a->batch <= 32 &&
+                                (a->heads * a->head_dim) % 32 == 0 && a->kv_len <= 8 * (256 / (a->head_dim / 8)) &&
+                                !getenv("MTTS_ATTN_DECODE_OFF")),
+             "attention_fwd: packed output needs q_len 1, bf16, batch <= 32, kv_len <= %d", 8 * (256 / (a->head_dim / 8)));
   if (a->batch == 0 || a->q_len == 0) return MTTS_OK;
   hipStream_t st = (hipStream_t)stream;
   const bool one = a->q_len == 1 && !getenv("MTTS_ATTN_DECODE_OFF");   // decode step: single-query kernel

@@ -44,6 +44,17 @@ void colsum_multi(const ColsumJob* jobs, int n, int ncols, int64_t pstride, hipS
 // decode projections on packed weights (gemv.hip), called by mtts_gemm_rows
 int launch_gemv_packed(const MttsRowsArgs* a, hipStream_t st);
 
+// Packed ACTIVATION image of a decode-step operand (<= 32 rows, K columns,
+// K % 32 == 0): the v_mfma_f32_16x16x32_bf16 B fragments of the packed
+// projection kernel in load order, so its operand loads are coalesced KiB
+// like the weights': element (m, k) lives at
+//   ((k / 32 * 2 + m / 16) * 64 + (k / 8 % 4) * 16 + m % 16) * 8 + k % 8.
+// 32 * K elements; rows >= M are never written (they only feed output rows
+// that are never stored).
+__host__ __device__ __forceinline__ int64_t xpk_index(int m, int k) {
+  return ((int64_t)((k >> 5) * 2 + (m >> 4)) * 64 + ((k >> 3) & 3) * 16 + (m & 15)) * 8 + (k & 7);
+}
+
 // ---------------------------------------------------------------- dtypes
 typedef uint16_t bf16_t;
 

@@ -60,9 +60,10 @@ __device__ __forceinline__ float gelu_erf(float s) { return 0.5f * s * (1.f + er
 // S: k-steps per wave (K = 32 * S * KS, KS = blockDim.x / 64); LNM:
 // 0 none, 1 LayerNorm prologue, 2 LayerNorm + FiLM; CONV: conv-update
 // epilogue operands present
-template <int S, int LNM, bool CONV>
+template <int S, int LNM, bool CONV, bool XP>
 __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs a) {
   constexpr bool LNP = LNM > 0, FILM = LNM == 2;
+
   __shared__ __attribute__((aligned(16))) f32x4 red[kMaxKS][2][64];
   __shared__ float psum[LNP ? kMaxKS : 1][32], psq[LNP ? kMaxKS : 1][32];
   const int KS = blockDim.x >> 6;
@@ -82,8 +83,19 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
   s16x8 xf0[S], xf1[S];
 #pragma unroll
   for (int j = 0; j < S; ++j) {
-    xf0[j] = *reinterpret_cast<const s16x8*>(x0 + 32 * j);
-    xf1[j] = *reinterpret_cast<const s16x8*>(x1 + 32 * j);   // unconditional: a branch here drains vmcnt
+#ifdef GEMV_DIAG_NOX   // timing-only build: no x operand loads
+    xf0[j] = s16x8{(short)j, 1, 2, 3, 4, 5, 6, (short)r};
+    xf1[j] = xf0[j];
+#else
+    if constexpr (XP) {   // packed image: the two halves of k-step s0 + j are consecutive KiB
+      const s16x8* xp = reinterpret_cast<const s16x8*>(a.x) + (int64_t)(s0 + j) * 128 + lane;
+      xf0[j] = xp[0];
+      xf1[j] = xp[64];
+    } else {
+      xf0[j] = *reinterpret_cast<const s16x8*>(x0 + 32 * j);
+      xf1[j] = *reinterpret_cast<const s16x8*>(x1 + 32 * j);   // unconditional: a branch here drains vmcnt
+    }
+#endif
   }
 
   // ---- LayerNorm parameters / FiLM rows, also ahead of the weights: vmcnt
@@ -95,13 +107,28 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
     const bf16_t* gp = (const bf16_t*)a.gamma;
     const bf16_t* bp = (const bf16_t*)a.beta;
     const int64_t o0 = (int64_t)(r < M ? r : 0) * a.ld_gb + kx, o1 = (int64_t)(16 + r < M ? 16 + r : 0) * a.ld_gb + kx;
+#ifdef GEMV_DIAG_NOLNP   // timing-only build: no LayerNorm parameter / FiLM loads
+    const float4 one4 = make_float4(1.f, 1.f, 1.f, (float)r);
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      lw[j][0] = lw[j][1] = lb[j][0] = lb[j][1] = one4;
+      if constexpr (FILM) ga0[j] = ba0[j] = ga1[j] = ba1[j] = s16x8{1, 2, 3, 4, 5, 6, 7, (short)j};
+    }
+    if (false)
+#endif
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       lw[j][0] = *reinterpret_cast<const float4*>(a.ln_w + kx + 32 * j);
       lw[j][1] = *reinterpret_cast<const float4*>(a.ln_w + kx + 32 * j + 4);
       lb[j][0] = *reinterpret_cast<const float4*>(a.ln_b + kx + 32 * j);
       lb[j][1] = *reinterpret_cast<const float4*>(a.ln_b + kx + 32 * j + 4);
-      if constexpr (FILM) {
+      if constexpr (FILM && XP) {   // packed FiLM images: coalesced KiB like x
+        const int64_t o = (int64_t)(s0 + j) * 128 * 8 + lane * 8;
+        ga0[j] = *reinterpret_cast<const s16x8*>(gp + o);
+        ba0[j] = *reinterpret_cast<const s16x8*>(bp + o);
+        ga1[j] = *reinterpret_cast<const s16x8*>(gp + o + 512);
+        ba1[j] = *reinterpret_cast<const s16x8*>(bp + o + 512);
+      } else if constexpr (FILM) {
         ga0[j] = *reinterpret_cast<const s16x8*>(gp + o0 + 32 * j);
         ba0[j] = *reinterpret_cast<const s16x8*>(bp + o0 + 32 * j);
         ga1[j] = *reinterpret_cast<const s16x8*>(gp + o1 + 32 * j);
@@ -114,7 +141,11 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
   s16x8 wf[S];
 #pragma unroll
   for (int j = 0; j < S; ++j) {
+#ifdef GEMV_DIAG_NOW   // timing-only build (tools/diag_build.sh): no weight stream
+    wf[j] = xf0[j];
+#else
     wf[j] = wp[j * 64];   // (non-temporal loads measured equal)
+#endif
   }
   // ---- epilogue operands, fetched before the product (threads < 128:
   // half = row block, 4 consecutive columns nb..nb+3 of row m)
@@ -156,6 +187,9 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
     // mtts_layernorm_fwd rounds it; statistics of the full row from the
     // wave's registers (lanes r, r+16, r+32, r+48 share row r), then over the
     // KS waves in fixed order; two passes (mean, then squared deviations)
+#ifdef GEMV_DIAG_NOSTATS   // timing-only build: no row statistics (no barriers)
+    const float ma = 0.f, mb = 0.f, ra = 1.f, rb = 1.f;
+#else
     float sa = 0.f, sb = 0.f;
 #pragma unroll
     for (int j = 0; j < S; ++j)
@@ -188,6 +222,7 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
     float va = 0.f, vb = 0.f;
     for (int w = 0; w < KS; ++w) { va += psq[w][r]; vb += psq[w][16 + r]; }
     const float ra = 1.f / sqrtf(va / a.K + a.ln_eps), rb = 1.f / sqrtf(vb / a.K + a.ln_eps);
+#endif
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const float w8[8] = {lw[j][0].x, lw[j][0].y, lw[j][0].z, lw[j][0].w, lw[j][1].x, lw[j][1].y, lw[j][1].z, lw[j][1].w};
@@ -232,16 +267,24 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
     yv[q] = bf2f(sb);
     out[q] = a.res ? f2bf(yv[q] + rv[q]) : sb;
   }
-  bf16_t* yrow = (bf16_t*)a.y + (int64_t)m * a.ldy;
-  if (nb + 3 < N && ((uintptr_t)(yrow + nb) & 7) == 0) {
+  if (a.y) {
+    bf16_t* yrow = (bf16_t*)a.y + (int64_t)m * a.ldy;
+    if (nb + 3 < N && ((uintptr_t)(yrow + nb) & 7) == 0) {
+      uint2 w2;
+      w2.x = (uint32_t)out[0] | ((uint32_t)out[1] << 16);
+      w2.y = (uint32_t)out[2] | ((uint32_t)out[3] << 16);
+      *reinterpret_cast<uint2*>(yrow + nb) = w2;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (nb + q < N) yrow[nb + q] = out[q];
+    }
+  }
+  if (a.y_packed) {   // N % 32 == 0: columns nb..nb+3 are 4 consecutive elements of the image
     uint2 w2;
     w2.x = (uint32_t)out[0] | ((uint32_t)out[1] << 16);
     w2.y = (uint32_t)out[2] | ((uint32_t)out[3] << 16);
-    *reinterpret_cast<uint2*>(yrow + nb) = w2;
-  } else {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (nb + q < N) yrow[nb + q] = out[q];
+    *reinterpret_cast<uint2*>((bf16_t*)a.y_packed + xpk_index(m, nb)) = w2;
   }
   if (conv_tile) {   // causal_conv1d_update (width 4) + SiLU on the bf16-rounded column
 #pragma unroll
@@ -251,15 +294,27 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
       *reinterpret_cast<float4*>(a.conv_state + ((int64_t)m * a.conv_dim + c) * 4) = st;
       const float4 w = cwv[q];
       const float v = fmaf(w.x, st.x, fmaf(w.y, st.y, fmaf(w.z, st.z, fmaf(w.w, st.w, cbv[q]))));
-      ((bf16_t*)a.u)[(int64_t)m * a.ldu + c] = f2bf(silu_f(v));
+      out[q] = f2bf(silu_f(v));
+      ((bf16_t*)a.u)[(int64_t)m * a.ldu + c] = out[q];
+    }
+    if (a.u_packed) {
+      uint2 w2;
+      w2.x = (uint32_t)out[0] | ((uint32_t)out[1] << 16);
+      w2.y = (uint32_t)out[2] | ((uint32_t)out[3] << 16);
+      *reinterpret_cast<uint2*>((bf16_t*)a.u_packed + xpk_index(m, nb)) = w2;
     }
   }
 }
 
 template <int S, int LNM>
 void launch_gemv2(const MttsRowsArgs* a, const dim3 grid, const dim3 block, hipStream_t st) {
-  if (a->conv_dim > 0) hipLaunchKernelGGL((gemv16_kernel<S, LNM, true>), grid, block, 0, st, *a);
-  else hipLaunchKernelGGL((gemv16_kernel<S, LNM, false>), grid, block, 0, st, *a);
+  if (a->x_packed) {
+    if (a->conv_dim > 0) hipLaunchKernelGGL((gemv16_kernel<S, LNM, true, true>), grid, block, 0, st, *a);
+    else hipLaunchKernelGGL((gemv16_kernel<S, LNM, false, true>), grid, block, 0, st, *a);
+    return;
+  }
+  if (a->conv_dim > 0) hipLaunchKernelGGL((gemv16_kernel<S, LNM, true, false>), grid, block, 0, st, *a);
+  else hipLaunchKernelGGL((gemv16_kernel<S, LNM, false, false>), grid, block, 0, st, *a);
 }
 
 template <int S>
@@ -273,6 +328,75 @@ void launch_gemv(const MttsRowsArgs* a, int ks, hipStream_t st) {
     }
   }
   launch_gemv2<S, 0>(a, grid, block, st);
+}
+
+// One wave per row (<= 32 rows): two-pass statistics over the row in
+// registers, the same arithmetic and summation order as ln_fwd_kernel
+// (csrc/ln.hip, VEC 8), so bf16(LN(x) * w + b [, gamma * . + beta]) is bit
+// identical to mtts_layernorm_fwd's y; written as 16-byte pieces of the
+// packed activation image.
+template <bool FILM, int NC>
+__global__ __launch_bounds__(256) void ln_rows_packed_kernel(const MttsLNArgs a, bf16_t* __restrict__ yp) {
+  // NC 16-byte chunks per lane (cols <= 512 NC); every load is issued up
+  // front and unconditionally (clamped chunk index, masked afterwards):
+  // branches around loads would drain vmcnt between them
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int C = a.cols;
+  const bf16_t* x = (const bf16_t*)a.x + (int64_t)row * a.x_rs;
+  float v[NC][8], w[NC][8], b[NC][8], gm[FILM ? NC : 1][8], bt[FILM ? NC : 1][8];
+  bool ok[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int k0 = 8 * (lane + 64 * i);
+    ok[i] = k0 < C;
+    const int k = ok[i] ? k0 : 0;
+    ld_vec<bf16_t, 8>(x + k, v[i]);
+    ld_vec<float, 4>(a.w + k, *reinterpret_cast<float(*)[4]>(w[i]));
+    ld_vec<float, 4>(a.w + k + 4, *reinterpret_cast<float(*)[4]>(w[i] + 4));
+    ld_vec<float, 4>(a.b + k, *reinterpret_cast<float(*)[4]>(b[i]));
+    ld_vec<float, 4>(a.b + k + 4, *reinterpret_cast<float(*)[4]>(b[i] + 4));
+    if constexpr (FILM) {
+      ld_vec<bf16_t, 8>((const bf16_t*)a.gamma + (int64_t)row * a.gb_rs + k, gm[i]);
+      ld_vec<bf16_t, 8>((const bf16_t*)a.beta + (int64_t)row * a.gb_rs + k, bt[i]);
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += ok[i] ? v[i][q] : 0.f;
+  const float mean = wave_sum(s) / C;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { const float d = ok[i] ? v[i][q] - mean : 0.f; sq = fmaf(d, d, sq); }
+  const float rstd = 1.f / sqrtf(wave_sum(sq) / C + a.eps);
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    float o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[q] = fmaf((v[i][q] - mean) * rstd, w[i][q], b[i][q]);
+      if constexpr (FILM) o[q] = fmaf(gm[i][q], o[q], bt[i][q]);
+    }
+    if (ok[i]) st_vec<bf16_t, 8>(yp + xpk_index(row, 8 * (lane + 64 * i)), o);
+  }
+}
+
+template <bool FILM>
+void launch_ln_rows(const MttsLNArgs* a, bf16_t* yp, hipStream_t st) {
+  const dim3 grid((a->rows + 3) / 4), block(256);
+  const int nc = (a->cols + 511) / 512;
+  switch (nc) {
+    case 1: hipLaunchKernelGGL((ln_rows_packed_kernel<FILM, 1>), grid, block, 0, st, *a, yp); break;
+    case 2: hipLaunchKernelGGL((ln_rows_packed_kernel<FILM, 2>), grid, block, 0, st, *a, yp); break;
+    case 3:
+    case 4: hipLaunchKernelGGL((ln_rows_packed_kernel<FILM, 4>), grid, block, 0, st, *a, yp); break;
+    default: hipLaunchKernelGGL((ln_rows_packed_kernel<FILM, 8>), grid, block, 0, st, *a, yp); break;
+  }
 }
 
 }  // namespace
@@ -299,6 +423,10 @@ int launch_gemv_packed(const MttsRowsArgs* a, hipStream_t st) {
     set_error("gemm_rows: packed weights need K %% 64 == 0 and K / 32 = KS * S with KS <= 8 a power of 2, "
               "S in {1, 2, 4, 8, 16} (K=%d)", a->K);
     return MTTS_EUNSUPPORTED;
+  }
+  if ((a->y_packed && a->N % 32) || (a->x_packed && a->K % 32) || (!a->y && !a->y_packed)) {
+    set_error("gemm_rows: packed activation images need N / K %% 32 == 0 (N=%d K=%d), and some output", a->N, a->K);
+    return MTTS_EINVAL;
   }
   if (a->ln_w && s > 8) {
     set_error("gemm_rows: packed weights with the LayerNorm prologue need K <= 2048 (K=%d)", a->K);
@@ -334,5 +462,21 @@ extern "C" int mtts_pack_rows_weight(const void* W, int64_t ldw, int N, int K, v
   hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)((total + threads - 1) / threads)), dim3(threads), 0,
                      (hipStream_t)stream, (const bf16_t*)W, ldw, N, K, (uint4*)out, total);
   MTTS_LAUNCH_CHECK("pack_rows_weight");
+  return MTTS_OK;
+}
+
+extern "C" int mtts_layernorm_rows_packed(const MttsLNArgs* a, void* y_packed, void* stream) {
+  MTTS_CHECK(a && a->x && a->w && a->b && y_packed, "layernorm_rows_packed: null pointer");
+  MTTS_CHECK(a->rows > 0 && a->rows <= 32 && a->cols > 0 && a->cols % 32 == 0 && a->cols <= 4096,
+             "layernorm_rows_packed: rows=%d must be in [1, 32], cols=%d a multiple of 32 <= 4096", a->rows, a->cols);
+  MTTS_CHECK(a->dtype == MTTS_BF16 && (!a->gamma || (a->beta && a->gb_dtype == MTTS_BF16 && a->rows_per_group <= 1)),
+             "layernorm_rows_packed: bf16 rows, FiLM rows bf16 with one row per group");
+  MTTS_CHECK(((uintptr_t)a->x | (uintptr_t)a->w | (uintptr_t)a->b | (uintptr_t)y_packed) % 16 == 0 &&
+                 a->x_rs % 8 == 0 && (!a->gamma || (((uintptr_t)a->gamma | (uintptr_t)a->beta) % 16 == 0 &&
+                                                    a->gb_rs % 8 == 0)),
+             "layernorm_rows_packed: operands must be 16-byte aligned with 16-byte row strides");
+  if (a->gamma) launch_ln_rows<true>(a, (bf16_t*)y_packed, (hipStream_t)stream);
+  else launch_ln_rows<false>(a, (bf16_t*)y_packed, (hipStream_t)stream);
+  MTTS_LAUNCH_CHECK("layernorm_rows_packed");
   return MTTS_OK;
 }

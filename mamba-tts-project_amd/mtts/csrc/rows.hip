@@ -304,7 +304,7 @@ void launch_rows(const MttsRowsArgs* a, int tiles, hipStream_t st) {
 using namespace mtts;
 
 extern "C" int mtts_gemm_rows(const MttsRowsArgs* a, void* stream) {
-  MTTS_CHECK(a && a->x && a->W && a->y, "gemm_rows: null pointer");
+  MTTS_CHECK(a && a->x && a->W && (a->y || (a->w_packed && a->y_packed)), "gemm_rows: null pointer");
   const int M = a->M, N = a->N, K = a->K;
   MTTS_CHECK(M >= 0 && M <= 32 && N > 0 && K > 0, "gemm_rows: M=%d must be in [0, 32], N, K > 0", M);
   MTTS_CHECK(K % 64 == 0, "gemm_rows: K=%d must be a multiple of 64", K);

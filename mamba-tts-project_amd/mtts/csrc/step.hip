@@ -99,7 +99,10 @@ __global__ void state_update_kernel(const MttsStateUpdateArgs a) {
   if (!ok || j != 0) return;
   if (a.D) y = fmaf(a.D[c], x, y);
   if (a.z) y *= silu_f(ldf((const Tio*)a.z + (int64_t)b * a.z_bs + c));
-  stf((Tio*)a.out + (int64_t)b * a.out_bs + c, y);
+  if (a.out) stf((Tio*)a.out + (int64_t)b * a.out_bs + c, y);
+  if constexpr (sizeof(Tio) == 2) {   // packed activation image for out_proj (csrc/common.h)
+    if (a.out_packed) ((bf16_t*)a.out_packed)[xpk_index(b, c)] = f2bf(y);
+  }
 }
 
 }  // namespace mtts
@@ -123,7 +126,7 @@ extern "C" int mtts_causal_conv1d_update(const MttsConvUpdateArgs* a, void* stre
 }
 
 extern "C" int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* stream) {
-  MTTS_CHECK(a && a->state && a->x && a->dt && a->A && a->Bm && a->Cm && a->out, "state_update: null tensor");
+  MTTS_CHECK(a && a->state && a->x && a->dt && a->A && a->Bm && a->Cm, "state_update: null tensor");
   MTTS_CHECK(a->batch > 0 && a->dim > 0, "state_update: bad sizes");
   MTTS_CHECK(a->dt_rank >= 0 && (a->dt_rank == 0 || a->dt_w), "state_update: dt_rank > 0 needs dt_w");
   if (a->dstate != 16) {
@@ -131,6 +134,9 @@ extern "C" int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* s
     return MTTS_EUNSUPPORTED;
   }
   MTTS_CHECK((uintptr_t)a->state % 16 == 0 && (uintptr_t)a->A % 16 == 0, "state_update: state/A alignment");
+  MTTS_CHECK(a->out || a->out_packed, "state_update: no output");
+  MTTS_CHECK(!a->out_packed || (a->dtype_io == MTTS_BF16 && a->batch <= 32 && a->dim % 32 == 0),
+             "state_update: packed output needs bf16, batch <= 32, dim %% 32 == 0");
   const int64_t n = (int64_t)a->batch * a->dim * 4;   // four lanes per (batch, channel)
   hipStream_t st = (hipStream_t)stream;
   dim3 g((n + 255) / 256), blk(256);

@@ -32,7 +32,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops
-from .attn_kernels import attention
+from .attn_kernels import attention, attention_decode_packed
 from .linear import cast_weight
 
 
@@ -71,6 +71,7 @@ class DecodeEngine:
         self.reset()
 
     def reset(self):
+        self.xpk = False
         self.ctx_key = None
         self.ctx_refs = None
         self.ctx_versions = None
@@ -163,6 +164,9 @@ class DecodeEngine:
         def w(p, k):   # packed image when there is one (csrc/gemv.hip)
             return p.get(k + "_p", p[k])
 
+        if self.xpk:
+            return self._step_xpk(x, states, ln)
+
         fuse_conv = os.environ.get("MTTS_DECODE_FUSE_CONV", "1") != "0"
         for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
             conv_state, ssm_state = states[i]
@@ -184,6 +188,58 @@ class DecodeEngine:
             f = ops.gemm_rows(x, w(p, "W1"), p["b1"], "gelu", ln=ln(l.norm_ff, p["gamma"], p["beta"]))
             x = ops.gemm_rows(f, w(p, "W2"), p["b2"], res=x)
         return ops.gemm_rows(x, w(c, "Wh"), c["bh"], ln=ln(m.norm_out))[:, None]
+
+    def _xpk_ok(self):
+        """Every projection packed and every operand shape the packed
+        activation images take (K, N % 32; short key side): the step of
+        _step_xpk applies."""
+        if os.environ.get("MTTS_DECODE_XPACKED", "1") == "0":
+            return False
+        c = self.ctx
+        names = self._PACKED
+        if not all(k + "_p" in p for p in c["layers"] for k in names) or "Wh_p" not in c:
+            return False
+        for l, p in zip(self.m.layers, c["layers"]):
+            ca = l.cross_attn
+            hd = ca.embed_dim // ca.num_heads
+            if (any(p[k].shape[0] % 32 or p[k].shape[1] % 32 for k in names)
+                    or p["k"].shape[1] > 8 * (256 // (hd // 8)) or l.mamba.d_inner % 32):
+                return False
+        for p in c["layers"]:   # FiLM rows as packed images (per-context constants)
+            if "gamma_p" not in p:
+                p["gamma_p"] = ops.PackedAct.pack(p["gamma"])
+                p["beta_p"] = ops.PackedAct.pack(p["beta"])
+        return True
+
+    def _step_xpk(self, x, states, ln):
+        """_step_rows with packed activations (csrc/gemv.hip, common.h
+        xpk_index): every producer writes the packed image of what the next
+        projection reads (residual epilogues the residual stream besides its
+        row-major copy, the conv-update u for x_proj, the state-update y for
+        out_proj, attention o, FFN-up f) and the FiLM rows are packed once
+        per context, so every projection loads its operands as coalesced KiB
+        like its weights; the LayerNorm(+FiLM) prologues run on the packed
+        rows.  9 launches per layer, as _step_rows."""
+        m, c = self.m, self.ctx
+        xp = None   # packed image of the residual stream (none before layer 0)
+        for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
+            conv_state, ssm_state = states[i]
+            mm = l.mamba
+            di, N, r = mm.d_inner, mm.d_state, mm.dt_rank
+            xz, u, up = ops.gemm_rows(x if xp is None else xp, p["Win_p"],
+                                      conv=(conv_state, p["conv_w"], p["conv_b"]), ln=ln(l.norm_mamba),
+                                      u_packed=True)
+            x_dbl = ops.gemm_rows(up, p["Wx_p"])
+            y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
+                                 xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"], packed_out=True)
+            x, xp = ops.gemm_rows(y, p["Wout_p"], res=x, packed_out="also")
+            q = ops.gemm_rows(xp, p["Wq_p"], p["bq"], ln=ln(l.norm_cross))
+            o = attention_decode_packed(q, p["k"], p["v"], l.cross_attn.num_heads, c["kpm"])
+            x, xp = ops.gemm_rows(o, p["Wo_p"], p["bo"], res=x, packed_out="also")
+            f = ops.gemm_rows(xp, p["W1_p"], p["b1"], "gelu", ln=ln(l.norm_ff, p["gamma_p"], p["beta_p"]),
+                              packed_out="only")
+            x, xp = ops.gemm_rows(f, p["W2_p"], p["b2"], res=x, packed_out="also")
+        return ops.gemm_rows(xp, c["Wh_p"], c["bh"], ln=ln(m.norm_out))[:, None]
 
     # -- one step, eager -----------------------------------------------------
     def _step(self, tok, pos, states):
@@ -234,6 +290,7 @@ class DecodeEngine:
             self.fused = self._fused_ok(cd, last_token.shape[0])
             if self.fused and os.environ.get("MTTS_DECODE_PACKED", "1") != "0":
                 self._pack_ctx()
+            self.xpk = self.fused and self._xpk_ok()
             self.graph = None
             self.states = None
         B = last_token.shape[0]

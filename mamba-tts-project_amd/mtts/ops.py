@@ -13,6 +13,8 @@ Public op API mirroring [upstream] mamba-ssm (layout (B, D, L)):
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from . import _lib as L
@@ -261,30 +263,37 @@ def conv_update(x, conv_state, w, bias=None, silu=True, out=None):
     return out
 
 
-def state_update(state, x, dt, A, Bm, Cm, D=None, z=None, dt_bias=None, softplus=True, out=None, dt_w=None):
+def state_update(state, x, dt, A, Bm, Cm, D=None, z=None, dt_bias=None, softplus=True, out=None, dt_w=None,
+                 packed_out=False):
     """state (B, D, N) fp32 updated IN PLACE; x/z (B, D); Bm/Cm (B, N) with
     unit element stride; dt (B, D) raw delta, or with dt_w (D, R) given the
-    (B, R) low-rank input of dt_proj (fused: delta = dt @ dt_w.t())."""
+    (B, R) low-rank input of dt_proj (fused: delta = dt @ dt_w.t()).
+    packed_out: y is returned ONLY as a PackedAct (out_proj's operand)."""
     _check_cuda(state, x, dt, A, Bm, Cm, dt_w)
     for t in (Bm, Cm, dt):
         if t.stride(-1) != 1:
             raise ValueError("state_update: B / C / dt need unit element stride")
     Bsz, Dm = x.shape
-    out = torch.empty(Bsz, Dm, device=x.device, dtype=x.dtype) if out is None else out
+    yp = PackedAct.empty(Bsz, Dm, x.device) if packed_out else None
+    if not packed_out:
+        out = torch.empty(Bsz, Dm, device=x.device, dtype=x.dtype) if out is None else out
     a = L.StateUpdateArgs()
     a.batch, a.dim, a.dstate = Bsz, Dm, state.shape[-1]
     a.dtype_io, a.dtype_bc, a.dt_softplus = L.dtype_code(x), L.dtype_code(Bm), int(softplus)
-    a.x_bs, a.dt_bs, a.out_bs, a.B_bs, a.C_bs = x.stride(0), dt.stride(0), out.stride(0), Bm.stride(0), Cm.stride(0)
+    a.x_bs, a.dt_bs, a.B_bs, a.C_bs = x.stride(0), dt.stride(0), Bm.stride(0), Cm.stride(0)
+    a.out_bs = 0 if out is None else out.stride(0)
     if z is not None:
         a.z_bs = z.stride(0)
     a.state, a.x, a.dt, a.A, a.Bm, a.Cm = state.data_ptr(), x.data_ptr(), dt.data_ptr(), A.data_ptr(), Bm.data_ptr(), Cm.data_ptr()
-    a.D, a.z, a.dt_bias, a.out = L.ptr(D), L.ptr(z), L.ptr(dt_bias), out.data_ptr()
+    a.D, a.z, a.dt_bias, a.out = L.ptr(D), L.ptr(z), L.ptr(dt_bias), L.ptr(out)
+    if yp is not None:
+        a.out_packed = yp.data.data_ptr()
     if dt_w is not None:
         if dt_w.dtype != x.dtype or dt_w.shape != (Dm, dt.shape[1]) or not dt_w.is_contiguous() or dt.dtype != x.dtype:
             raise ValueError("state_update: dt_w must be a contiguous (D, R) tensor of x's dtype")
         a.dt_rank, a.dt_w = dt_w.shape[1], dt_w.data_ptr()
     L.call("mtts_selective_state_update", a)
-    return out
+    return out if yp is None else yp
 
 
 def causal_conv1d_update(x, conv_state, weight, bias=None, activation=None):
@@ -512,6 +521,68 @@ class PackedRows:
         return (self.N, self.K)
 
 
+class PackedAct:
+    """A decode-step activation (M <= 32 rows, K columns, bf16) as the packed
+    image the projection kernel loads in coalesced KiB (csrc/common.h
+    xpk_index: 32 * K elements, rows >= M unused).  Made by the producers'
+    epilogues (projections, state update, decode attention) and by
+    ln_rows_packed."""
+
+    __slots__ = ("data", "M", "K")
+
+    def __init__(self, data, M, K):
+        self.data, self.M, self.K = data, M, K
+
+    @property
+    def shape(self):
+        return (self.M, self.K)
+
+    @staticmethod
+    def empty(M, K, device):
+        if M > GEMM_ROWS_MAX or K % 32:
+            raise ValueError(f"PackedAct: M={M} must be <= {GEMM_ROWS_MAX}, K={K} a multiple of 32")
+        return PackedAct(torch.empty(32 * K, device=device, dtype=torch.bfloat16), M, K)
+
+    @staticmethod
+    def pack(x):
+        """Packed image of a row-major bf16 (M, K) tensor (setup-time helper:
+        per-context constants such as the FiLM rows)."""
+        M, K = x.shape
+        out = PackedAct.empty(M, K, x.device)
+        img = torch.zeros(32, K, device=x.device, dtype=torch.bfloat16)
+        img[:M] = x
+        out.data.copy_(img.view(2, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).reshape(-1))
+        return out
+
+    def unpack(self):
+        """Row-major (M, K) copy (tests / debugging)."""
+        img = self.data.view(self.K // 32, 2, 4, 16, 8)            # s, half, g, r, q
+        return img.permute(1, 3, 0, 2, 4).reshape(32, self.K)[:self.M]
+
+
+def ln_rows_packed(x, w, b, eps, gamma=None, beta=None):
+    """bf16(LN(x) * w + b [, gamma * . + beta]) of <= 32 bf16 rows as the
+    packed image of the next projection (mtts_layernorm_rows_packed): the
+    same values as layer_norm's y, bit for bit."""
+    _check_cuda(x, w, b, gamma, beta)
+    M, K = x.shape
+    if x.dtype != torch.bfloat16 or x.stride(1) != 1:
+        raise ValueError("ln_rows_packed: x must be bf16 (M, K) with unit column stride")
+    out = PackedAct.empty(M, K, x.device)
+    a = L.LNArgs()
+    a.rows, a.cols, a.dtype, a.rows_per_group, a.eps = M, K, L.dtype_code(x), 1, float(eps)
+    a.x, a.x_rs = x.data_ptr(), x.stride(0)
+    wf, bf = _f32c(w), _f32c(b)
+    a.w, a.b = wf.data_ptr(), bf.data_ptr()
+    if gamma is not None:
+        if gamma.dtype != torch.bfloat16 or gamma.shape != (M, K) or gamma.stride() != beta.stride() \
+                or gamma.stride(1) != 1:
+            raise ValueError("ln_rows_packed: FiLM gamma / beta must be (M, K) bf16 with equal strides")
+        a.gamma, a.beta, a.gb_rs, a.gb_dtype = gamma.data_ptr(), beta.data_ptr(), gamma.stride(0), L.dtype_code(gamma)
+    L.call_raw("mtts_layernorm_rows_packed", C.byref(a), out.data.data_ptr())
+    return out
+
+
 def gemv_split_ok(K, ln=False):
     """K values the packed kernel takes: K / 32 = KS * S, KS <= 8 a power
     of two, S in {1, 2, 4, 8, 16}; with the LayerNorm prologue K <= 2048
@@ -542,6 +613,8 @@ def pack_rows_weight(w):
 
 def gemm_rows_ok(x, weight):
     """True when mtts_gemm_rows_bf16 takes y = x @ weight.t() as given."""
+    if isinstance(x, PackedAct):
+        return isinstance(weight, PackedRows) and x.K == weight.K
     if isinstance(weight, PackedRows):
         return (x.dtype == torch.bfloat16 and x.dim() == 2 and 0 < x.shape[0] <= GEMM_ROWS_MAX
                 and x.shape[1] == weight.K and x.stride(1) == 1 and x.stride(0) % 8 == 0
@@ -596,7 +669,7 @@ def rows_kgroups(N, K, ln):
     return kg
 
 
-def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
+def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None, packed_out=None, u_packed=False):
     """y = act(x @ weight.t() + bias) for the decode step's skinny GEMMs
     (x: M <= 32 rows, bf16; act None or "gelu" = exact-erf F.gelu).
 
@@ -606,12 +679,17 @@ def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
     ln = (w, b, eps[, gamma, beta]): the x operand is LayerNorm'd (+FiLM) on
         the fly, exactly as ops.layer_norm would produce it.
     res: (M, N) bf16; y = bf16(y + res) (the residual stream after the add).
+    x may be a PackedAct (with a PackedRows weight): coalesced operand loads.
+    packed_out "only" / "also": y comes back as a PackedAct (instead of /
+        besides the row-major tensor: (y, y_packed)) for the next projection.
+    u_packed: with conv, also a PackedAct of u (returned last).
     """
     packed = isinstance(weight, PackedRows)
-    _check_cuda(x, weight.data if packed else weight, bias)
+    xpk = isinstance(x, PackedAct)
+    _check_cuda(x.data if xpk else x, weight.data if packed else weight, bias)
     if not gemm_rows_ok(x, weight):
-        raise ValueError(f"gemm_rows: unsupported operands x{tuple(x.shape)}/{x.stride()} "
-                         f"w{tuple(weight.shape)}/{'packed' if packed else weight.stride()} {x.dtype}")
+        raise ValueError(f"gemm_rows: unsupported operands x{tuple(x.shape)}/{'packed' if xpk else x.stride()} "
+                         f"w{tuple(weight.shape)}/{'packed' if packed else weight.stride()}")
     M, K = x.shape
     N = weight.shape[0]
     if weight.shape[1] != K:
@@ -620,14 +698,18 @@ def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
         bias = bias.to(torch.bfloat16).contiguous()
         if bias.numel() != N:
             raise ValueError("gemm_rows: bias size")
-    dev = x.device
-    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    dev = x.data.device if xpk else x.device
+    y = None if packed_out == "only" else torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    yp = PackedAct.empty(M, N, dev) if packed_out else None
     a = L.RowsArgs()
     a.M, a.N, a.K, a.act = M, N, K, {None: 0, "gelu": 1}[act]
-    a.ldx, a.ldw, a.ldy = x.stride(0), 0 if packed else weight.stride(0), y.stride(0)
-    a.x, a.W, a.bias, a.y = x.data_ptr(), (weight.data if packed else weight).data_ptr(), L.ptr(bias), y.data_ptr()
-    a.w_packed = int(packed)
-    out = [y]
+    a.ldx, a.ldw, a.ldy = 0 if xpk else x.stride(0), 0 if packed else weight.stride(0), N if y is None else y.stride(0)
+    a.x, a.W, a.bias, a.y = (x.data if xpk else x).data_ptr(), (weight.data if packed else weight).data_ptr(), \
+        L.ptr(bias), L.ptr(y)
+    a.w_packed, a.x_packed = int(packed), int(xpk)
+    if yp is not None:
+        a.y_packed = yp.data.data_ptr()
+    out = [yp] if y is None else ([y, yp] if yp is not None else [y])
     if conv is not None:
         cs, cw, cb = conv
         C = cw.shape[0]
@@ -637,6 +719,10 @@ def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
         a.conv_dim, a.conv_state, a.conv_w, a.conv_b = C, cs.data_ptr(), cw.data_ptr(), L.ptr(cb)
         a.u, a.ldu = u.data_ptr(), u.stride(0)
         out.append(u)
+        if u_packed:
+            up = PackedAct.empty(M, C, dev)
+            a.u_packed = up.data.data_ptr()
+            out.append(up)
     if ln is not None:
         lw, lb, eps = ln[0], ln[1], ln[2]
         if lw.dtype != torch.float32 or lb.dtype != torch.float32 or lw.numel() != K or not lw.is_contiguous():
@@ -644,9 +730,14 @@ def gemm_rows(x, weight, bias=None, act=None, conv=None, ln=None, res=None):
         a.ln_w, a.ln_b, a.ln_eps = lw.data_ptr(), lb.data_ptr(), float(eps)
         if len(ln) > 3 and ln[3] is not None:
             g, be = ln[3], ln[4]
-            if g.dtype != torch.bfloat16 or g.stride() != be.stride() or g.shape != (M, K):
-                raise ValueError("gemm_rows: FiLM gamma / beta must be (M, K) bf16 with equal strides")
-            a.gamma, a.beta, a.ld_gb = g.data_ptr(), be.data_ptr(), g.stride(0)
+            if xpk:   # packed x: FiLM rows as packed images too
+                if not (isinstance(g, PackedAct) and isinstance(be, PackedAct) and g.shape == be.shape == (M, K)):
+                    raise ValueError("gemm_rows: with a packed x, FiLM gamma / beta must be PackedAct (M, K)")
+                a.gamma, a.beta, a.ld_gb = g.data.data_ptr(), be.data.data_ptr(), 0
+            else:
+                if g.dtype != torch.bfloat16 or g.stride() != be.stride() or g.shape != (M, K):
+                    raise ValueError("gemm_rows: FiLM gamma / beta must be (M, K) bf16 with equal strides")
+                a.gamma, a.beta, a.ld_gb = g.data_ptr(), be.data_ptr(), g.stride(0)
     if res is not None:
         if res.dtype != torch.bfloat16 or res.shape != (M, N) or res.stride(1) != 1:
             raise ValueError("gemm_rows: res must be (M, N) bf16 with unit column stride")

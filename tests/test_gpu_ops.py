@@ -657,3 +657,106 @@ def test_gemm_rows_packed_matches_row_major(M, N, K, mode):
     if mode == "plain":
         ref = x.double() @ w.double().t() + b.double()
         close(outs[1][0], ref, rtol=2 ** -8, name="packed vs float64")
+
+
+@pytest.mark.parametrize("M,K", [(32, 1024), (5, 256), (17, 2048)])
+@pytest.mark.parametrize("film", [False, True])
+def test_ln_rows_packed_equals_layer_norm(M, K, film):
+    """mtts_layernorm_rows_packed: the packed image of LN(+FiLM) equals
+    mtts_layernorm_fwd's y bit for bit (same arithmetic and order)."""
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(M + K + film)
+    x = (torch.randn(M, K, generator=g) * 3 + 0.5).to(DEV, torch.bfloat16)
+    lw, lb = torch.randn(K, generator=g).to(DEV), torch.randn(K, generator=g).to(DEV)
+    gam = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if film else None
+    bet = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if film else None
+    hp = ops.ln_rows_packed(x, lw, lb, 1e-5, gam, bet)
+    h, _ = ops.layer_norm(x, lw, lb, 1e-5, gamma=gam, beta=bet, rows_per_group=1)
+    assert torch.equal(hp.unpack(), h)
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 1024, 2048), (32, 4096, 1024), (7, 96, 512), (20, 64, 64)])
+def test_gemm_rows_packed_activations(M, N, K):
+    """Packed activation images (csrc/common.h xpk_index) in and out of the
+    packed projection kernel: x as an image gives the row-major result bit
+    for bit; the y / u images unpack to the row-major y / u; state update and
+    decode attention images unpack to their row-major outputs."""
+    from mtts import ops
+    from mtts.attn_kernels import attention_decode_packed, attention_fwd
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    wp = ops.pack_rows_weight(w)
+    xp = ops.PackedAct.empty(M, K, DEV)
+    xp.data.view(-1)[:] = 0
+    # build the image through a producer: y of an identity-free GEMM is awkward, so scatter directly
+    img = torch.zeros(32, K, device=DEV, dtype=torch.bfloat16)
+    img[:M] = x
+    xp.data.copy_(img.view(2, 16, K // 32, 4, 8).permute(2, 0, 3, 1, 4).reshape(-1))
+    assert torch.equal(xp.unpack(), x)
+    y_ref = ops.gemm_rows(x, wp, b, res=None)
+    y2, yp = ops.gemm_rows(xp, wp, b, packed_out="also")
+    assert torch.equal(y2, y_ref)
+    assert torch.equal(yp.unpack(), y_ref)
+    yo = ops.gemm_rows(xp, wp, b, "gelu", packed_out="only")
+    assert torch.equal(yo.unpack(), ops.gemm_rows(x, wp, b, "gelu"))
+    if N % 64 == 0:   # conv epilogue with a packed u
+        C = N // 2
+        st0 = torch.randn(M, C, 4, generator=g).to(DEV)
+        cw, cb = torch.randn(C, 4, generator=g).to(DEV), torch.randn(C, generator=g).to(DEV)
+        s1, s2 = st0.clone(), st0.clone()
+        ya, ua = ops.gemm_rows(xp, wp, conv=(s1, cw, cb))
+        yb, ub, upk = ops.gemm_rows(x, wp, conv=(s2, cw, cb), u_packed=True)
+        assert torch.equal(ya, yb) and torch.equal(ua, ub) and torch.equal(s1, s2)
+        assert torch.equal(upk.unpack(), ub)
+    if K % 32 == 0 and M <= 32:   # state update image
+        D, Nst = K, 16
+        st = torch.randn(M, D, Nst, generator=g).to(DEV)
+        u = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
+        z = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
+        dt = torch.randn(M, D, generator=g).to(DEV, torch.bfloat16)
+        Bm = torch.randn(M, Nst, generator=g).to(DEV, torch.bfloat16)
+        Cm = torch.randn(M, Nst, generator=g).to(DEV, torch.bfloat16)
+        A = -torch.rand(D, Nst, generator=g).to(DEV) - 0.5
+        Dv = torch.randn(D, generator=g).to(DEV)
+        s1, s2 = st.clone(), st.clone()
+        y1 = ops.state_update(s1, u, dt, A, Bm, Cm, Dv, z, None, True)
+        y2p = ops.state_update(s2, u, dt, A, Bm, Cm, Dv, z, None, True, packed_out=True)
+        assert torch.equal(s1, s2) and torch.equal(y2p.unpack(), y1)
+    if K in (512, 1024, 2048):   # decode attention image
+        H = K // 128 if K >= 1024 else K // 64
+        q = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+        kv = torch.randn(M, 77, 2 * K, generator=g).to(DEV, torch.bfloat16)
+        kpm = torch.zeros(M, 77, dtype=torch.bool, device=DEV)
+        kpm[:, 70:] = True
+        o, _ = attention_fwd(q[:, None], kv[..., :K], kv[..., K:], H, kpm)
+        op = attention_decode_packed(q, kv[..., :K], kv[..., K:], H, kpm)
+        assert torch.equal(op.unpack(), o[:, 0])
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 4096, 1024), (9, 1024, 512)])
+@pytest.mark.parametrize("film", [False, True])
+def test_gemm_rows_ln_prologue_on_packed_x(M, N, K, film):
+    """LayerNorm(+FiLM) prologue on a packed x (FiLM rows packed too) equals
+    the same prologue on the row-major x bit for bit (same registers, same
+    order), and the residual epilogue's packed copy of y unpacks to y."""
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + film)
+    x = (torch.randn(M, K, generator=g) * 2 + 0.3).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    lw, lb = torch.randn(K, generator=g).to(DEV), torch.randn(K, generator=g).to(DEV)
+    gam = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if film else None
+    bet = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16) if film else None
+    wp = ops.pack_rows_weight(w)
+    y1 = ops.gemm_rows(x, wp, b, ln=(lw, lb, 1e-5, gam, bet))
+    xp = ops.PackedAct.pack(x)
+    gp = ops.PackedAct.pack(gam) if film else None
+    bp = ops.PackedAct.pack(bet) if film else None
+    y2 = ops.gemm_rows(xp, wp, b, ln=(lw, lb, 1e-5, gp, bp))
+    assert torch.equal(y1, y2)
+    res = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    y3, y3p = ops.gemm_rows(xp, wp, b, res=res, packed_out="also")
+    assert torch.equal(y3p.unpack(), y3)
+    assert torch.equal(y3, ops.gemm_rows(x, wp, b, res=res))

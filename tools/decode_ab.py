@@ -103,6 +103,13 @@ if __name__ == "__main__":
                 print("packed", pk, end=" ", flush=True)
                 step((True,))
         os.environ.pop("MTTS_DECODE_PACKED")
+    if "xpacked" in what:   # packed activation images (csrc/gemv.hip) vs row-major operands, interleaved
+        for _ in range(2):
+            for pk in ("1", "0"):
+                os.environ["MTTS_DECODE_XPACKED"] = pk
+                print("xpacked", pk, end=" ", flush=True)
+                step((True,))
+        os.environ.pop("MTTS_DECODE_XPACKED")
     if "splitk" in what:   # rows kernels with / without the cross-workgroup K split, interleaved
         for _ in range(2):
             for sk in (True, False):
