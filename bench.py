@@ -91,6 +91,7 @@ def make_batch(c, dev, seed):
 def train_bench(args, rank, world, dev):
     import mamba_decoder
     from mtts.optim import FusedClipAdam
+    from mtts.loss import cross_entropy
     c = dict(C2)
     torch.manual_seed(0)
     model = mamba_decoder.MambaTTSDecoder(c["vocab"], d_model=c["d_model"], n_layers=c["n_layers"],
@@ -107,8 +108,7 @@ def train_bench(args, rank, world, dev):
 
     def step():
         logits = model(tokens, text, z, text_mask=mask)
-        loss = torch.nn.functional.cross_entropy(logits.float().view(-1, c["vocab"]), tokens.view(-1),
-                                                 ignore_index=0)
+        loss = cross_entropy(logits.view(-1, c["vocab"]), tokens.view(-1), ignore_index=0)   # csrc/loss.hip
         if dp is not None:
             dp.zero_grad()         # grads are views into the flat all-reduce buffer
         else:

@@ -480,6 +480,35 @@ typedef struct {
 
 int mtts_gemm_rows(const MttsRowsArgs* a, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Codec-token cross-entropy with ignore index: replaces train.py:31-42
+ * codec_ce_loss = F.cross_entropy(logits.view(B*T, V), targets.view(B*T),
+ * ignore_index=pad_id) (mean over the non-ignored rows; NaN when all are
+ * ignored, as torch).  logits (rows, vocab) with row stride ld, F32 or BF16;
+ * targets int64 (rows).  Forward: loss[0] = mean loss, loss[1] = count,
+ * lse (rows) fp32 saved; workspace mtts_cross_entropy_workspace(rows) bytes.
+ * Backward: dlogits = (softmax - onehot) * grad_loss[0] / count on the
+ * non-ignored rows, 0 elsewhere (grad_loss read on the device). fp32 math,
+ * fixed-order reductions (deterministic).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int64_t rows;
+  int vocab;
+  int dtype;                 /* MTTS_F32 / MTTS_BF16 logits (and dlogits) */
+  int64_t ld;
+  const void* logits;
+  const int64_t* targets;
+  int ignore_index;
+  float* loss;               /* 2 floats: mean loss, non-ignored count */
+  float* lse;                /* rows */
+  float* workspace;
+} MttsCrossEntropyArgs;
+
+int64_t mtts_cross_entropy_workspace(int64_t rows);
+int mtts_cross_entropy_fwd(const MttsCrossEntropyArgs* a, void* stream);
+int mtts_cross_entropy_bwd(const MttsCrossEntropyArgs* a, const float* grad_loss, void* dlogits, int64_t ld_dlogits,
+                           void* stream);
+
 /* Packed image of a bf16 decode weight W (N, K), row stride ldw (K % 64 == 0,
  * 16-byte aligned): for 16-column tile t and k-step s, the 64 lanes'
  * v_mfma_f32_16x16x32_bf16 A fragments W[16t + l%16][32s + 8(l/16) .. +8]

@@ -29,6 +29,10 @@ def codec_ce_loss(logits: torch.Tensor, targets: torch.Tensor, pad_id: int = 0) 
     """Cross-entropy over flattened codec tokens; logits (B, T, V), targets
     (B, T) long; targets == pad_id are ignored; targets are NOT shifted."""
     B, T, V = logits.shape
+    if logits.is_cuda:   # csrc/loss.hip: the .float() upcast happens in registers
+        from mtts.loss import cross_entropy
+        x = logits.reshape(B * T, V)
+        return cross_entropy(x if x.stride(1) == 1 else x.contiguous(), targets.reshape(B * T), ignore_index=pad_id)
     return F.cross_entropy(logits.reshape(B * T, V).float(), targets.reshape(B * T), ignore_index=pad_id)
 
 

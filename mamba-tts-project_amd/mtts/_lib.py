@@ -77,6 +77,11 @@ class RowsArgs(C.Structure):
                 ("w_packed", i32), ("x_packed", i32), ("y_packed", vp), ("u_packed", vp)]
 
 
+class CrossEntropyArgs(C.Structure):
+    _fields_ = [("rows", i64), ("vocab", i32), ("dtype", i32), ("ld", i64), ("logits", vp), ("targets", vp),
+                ("ignore_index", i32), ("loss", vp), ("lse", vp), ("workspace", vp)]
+
+
 class GemmArgs(C.Structure):
     _fields_ = [("m", i32), ("n", i32), ("k", i32), ("layout", i32), ("splits", i32), ("epilogue", i32),
                 ("out_dtype", i32), ("bias_dtype", i32), ("lda", i64), ("ldb", i64), ("ldc", i64), ("ld_aux", i64),
@@ -134,6 +139,9 @@ _SIGS = {
     "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
     "mtts_gemm_rows": ([C.POINTER(RowsArgs), vp], i32),
     "mtts_pack_rows_bytes": ([i32, i32], i64),
+    "mtts_cross_entropy_workspace": ([i64], i64),
+    "mtts_cross_entropy_fwd": ([C.POINTER(CrossEntropyArgs), vp], i32),
+    "mtts_cross_entropy_bwd": ([C.POINTER(CrossEntropyArgs), vp, vp, i64, vp], i32),
     "mtts_layernorm_rows_packed": ([C.POINTER(LNArgs), vp, vp], i32),
     "mtts_pack_rows_weight": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_gemm_workspace": ([C.POINTER(GemmArgs)], i64),

@@ -1883,10 +1883,15 @@ static bool wide_io_ok(const MttsScanFwdArgs* a) {
 // One wave per SIMD (the block's LDS makes a block of 4 waves own its CU);
 // the waves are independent: each runs its own LDS-DMA ring of u/delta/z
 // tiles NB-1 tiles ahead and its own B/C staging, with no workgroup barrier.
-// Outputs replace u in the tile image and leave as 16-byte row chunks.
-// VMEM issue order per tile `it`: [stores of it-1] [B/C regs of it+1]
-// [DMA of it+NB-1]; waiting until only that DMA is in flight makes tile it+1
-// (B/C and the DMA issued NB-2 iterations earlier) complete.
+// Outputs leave straight from registers (MTTS_C1_DIRECT_STORE, default): one
+// 4- (2-) byte store per lane and step, a wave writing 256 (128) B of one row
+// per instruction.  VMEM issue order per tile `it`: [B/C regs of it+1] [DMA
+// of it+NB-1] [checkpoint stores of tile it, when any] [TT y stores of tile
+// it]; waiting until at most NDMA + TT operations are in flight therefore
+// retires the B/C load and every older DMA, i.e. tile it+1 is complete (the
+// checkpoint stores only make the wait stricter).  With DIRECT_STORE 0 the
+// outputs replace u in the tile image and leave as 16-byte row chunks
+// ([stores of it-1] first, wait for NDMA).
 template <typename Tio, typename Tbc, bool SP, bool HZ>
 __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdArgs a) {
   constexpr int ES = (int)sizeof(Tio);
