@@ -828,12 +828,44 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(MttsAttnFwdArgs a) {
 // p = exp2(s - max) -> P.V and sum(p) reduced over the wave's groups by
 // shuffles and over the 4 waves through LDS (fixed order).  All loads are
 // unconditional (clamped key index, masked afterwards).
+// wave-level reductions of the single-pass decode kernel with DPP / permlane
+// forms instead of ds_bpermute shuffles (no LDS round trip per stage):
+// group_sum over the G consecutive lanes of a key group (G | 16), groups_sum /
+// groups_max over the 64 / G groups of the wave (lane bits log2 G .. 5)
+template <int G>
+__device__ __forceinline__ float group_sum(float v, int lane) {
+  if constexpr (G >= 2) v += mtts::dpp<mtts::kQuadXor1>(v);
+  if constexpr (G >= 4) v += mtts::dpp<mtts::kQuadXor2>(v);
+  if constexpr (G >= 8) v += mtts::xor4(v, lane);
+  if constexpr (G >= 16) v += mtts::xor8(v);
+  return v;
+}
+template <int G>
+__device__ __forceinline__ float groups_sum(float v, int lane) {
+  if constexpr (G <= 1) v += mtts::dpp<mtts::kQuadXor1>(v);
+  if constexpr (G <= 2) v += mtts::dpp<mtts::kQuadXor2>(v);
+  if constexpr (G <= 4) v += mtts::xor4(v, lane);
+  if constexpr (G <= 8) v += mtts::xor8(v);
+  v = mtts::sum_xor16(v);
+  return mtts::sum_xor32(v);
+}
+template <int G>
+__device__ __forceinline__ float groups_max(float v, int lane) {
+  if constexpr (G <= 1) v = fmaxf(v, mtts::dpp<mtts::kQuadXor1>(v));
+  if constexpr (G <= 2) v = fmaxf(v, mtts::dpp<mtts::kQuadXor2>(v));
+  if constexpr (G <= 4) v = fmaxf(v, mtts::xor4(v, lane));
+  if constexpr (G <= 8) v = fmaxf(v, mtts::xor8(v));
+  v = fmaxf(v, mtts::xor16(v, lane));
+  return fmaxf(v, mtts::xor32(v, lane));
+}
+
 template <typename T, int HD, int U>
 __global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
   constexpr int G = HD / 8, NG = 256 / G;
   __shared__ float swm[4], swl[4], sacc[4][HD];
   const int bh = blockIdx.x, b = bh / a.heads, hh = bh % a.heads;
   const int g = threadIdx.x / G, gl = threadIdx.x % G, d0 = gl * 8, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   const float c = a.scale * kLog2e;
   float q[8];
   ld8((const T*)a.q + b * a.q_bs + hh * HD + d0, q);
@@ -857,13 +889,11 @@ __global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
     float sv = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) sv = fmaf(q[e], kx[u][e], sv);
-#pragma unroll
-    for (int o = 1; o < G; o <<= 1) sv += __shfl_xor(sv, o);
+    sv = group_sum<G>(sv, lane);
     sc[u] = ok[u] ? sv * c : -INFINITY;
     m = fmaxf(m, sc[u]);
   }
-#pragma unroll
-  for (int o = G; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+  m = groups_max<G>(m, lane);
   if ((threadIdx.x & 63) == 0) swm[wave] = m;
   __syncthreads();
   const float M = fmaxf(fmaxf(swm[0], swm[1]), fmaxf(swm[2], swm[3]));
@@ -875,12 +905,9 @@ __global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, vx[u][e], acc[e]);
   }
+  l = groups_sum<G>(l, lane);
 #pragma unroll
-  for (int o = G; o < 64; o <<= 1) {
-    l += __shfl_xor(l, o);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], o);
-  }
+  for (int e = 0; e < 8; ++e) acc[e] = groups_sum<G>(acc[e], lane);
   if ((threadIdx.x & 63) < G) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) sacc[wave][d0 + e] = acc[e];
