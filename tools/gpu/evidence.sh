@@ -5,7 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r2p
+O=$R/gpurun_out/evidence
 mkdir -p $O/pmc
 PT="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
 [ -n "$SKIP_TESTS" ] || timeout -k 10 900 $PT tests -m gpu > $O/tests.log 2>&1; rc=$?

@@ -3,7 +3,7 @@
 # breakdown and MFMA activity per kernel
 set -o pipefail
 export TMPDIR=/tmp
-O=$GRAFT_REPO_ROOT/gpurun_out/r2m
+O=$GRAFT_REPO_ROOT/gpurun_out/pmc_c2
 mkdir -p $O
 cd /tmp
 timeout -s KILL 60 rocprofv3 -L > $O/avail.txt 2>&1 || true

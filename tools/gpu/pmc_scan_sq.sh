@@ -2,7 +2,7 @@
 # SQ issue / stall PMC pass over the north-star scan forward (c1, fp32 and bf16)
 set -o pipefail
 export TMPDIR=/tmp
-O=$GRAFT_REPO_ROOT/gpurun_out/r2ad
+O=$GRAFT_REPO_ROOT/gpurun_out/pmc_scan
 mkdir -p $O
 cd /tmp
 for dt in fp32 bf16; do

@@ -2,7 +2,7 @@
 # rocprofv3 kernel stats of the default bench command and of 60 decode steps
 set -o pipefail
 export TMPDIR=/tmp
-O=$GRAFT_REPO_ROOT/gpurun_out/r2ae
+O=$GRAFT_REPO_ROOT/gpurun_out/prof
 mkdir -p $O
 cd /tmp
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/bench -o b -- python3 $GRAFT_REPO_ROOT/bench.py > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
