@@ -31,7 +31,9 @@ import os
 import torch
 import torch.nn.functional as F
 
+from . import _lib as L
 from . import ops
+from .embed import _err_flag
 from .attn_kernels import attention, attention_decode_packed
 from .linear import cast_weight
 
@@ -110,7 +112,11 @@ class DecodeEngine:
                 A=(-torch.exp(mm.A_log.detach().float())).contiguous(), D=mm.D.detach().float().contiguous(),
                 dt_bias=mm.dt_proj.bias.detach().float().contiguous(),
             ))
+        dev = text_hidden.device
         return dict(B=B, kpm=kpm, layers=layers, cd=cd,
+                    tok_w=m.token_embed.weight.detach().float().contiguous(),
+                    pos_w=m.pos_embed.weight.detach().float().contiguous(),
+                    q0_w=torch.zeros(1, d, device=dev), q0_id=torch.zeros(1, device=dev, dtype=torch.int32),
                     Wh=cast_weight(m.head.weight, cd), bh=cast_weight(m.head.bias, cd))
 
     def _fused_ok(self, cd, B):
@@ -129,6 +135,22 @@ class DecodeEngine:
                     or any(n.weight.dtype != torch.float32 for n in (l.norm_mamba, l.norm_cross, l.norm_ff))):
                 return False
         return m.norm_out.weight.dtype == torch.float32
+
+    def _embed(self, tok):
+        """token_embed(last_token) + pos_embed(step_index) in the compute dtype
+        (mamba_decoder.py:188-256; no quant_embed in decode_step) as ONE
+        mtts_embed_sum launch (a zero quantizer row, the step's position id
+        from the int32 buffer pos32) instead of two gathers, an add and a
+        cast."""
+        m, c = self.m, self.ctx
+        B = c["B"]
+        d = m.token_embed.weight.shape[1]
+        out = torch.empty(B, d, device=tok.device, dtype=c["cd"])
+        tw, pw = c["tok_w"], c["pos_w"]
+        L.call_raw("mtts_embed_sum", tok.data_ptr(), tok.stride(0), c["q0_id"].data_ptr(), self.pos32.data_ptr(),
+                   tw.data_ptr(), c["q0_w"].data_ptr(), pw.data_ptr(), B, 1, d, tw.shape[0], out.data_ptr(),
+                   L.dtype_code(out), out.stride(0), _err_flag(tok.device).data_ptr())
+        return out
 
     _PACKED = ("Win", "Wx", "Wout", "Wq", "Wo", "W1", "W2")
 
@@ -155,8 +177,7 @@ class DecodeEngine:
         x_sum of the generic step."""
         m, c = self.m, self.ctx
         cd = c["cd"]
-        x = (F.embedding(tok, m.token_embed.weight) + F.embedding(pos, m.pos_embed.weight)[None]).to(cd)
-        x = x.view(c["B"], -1)
+        x = self._embed(tok)
 
         def ln(norm, gamma=None, beta=None):
             return (norm.weight, norm.bias, norm.eps, gamma, beta)
@@ -303,6 +324,7 @@ class DecodeEngine:
                                     torch.zeros(B, mm.d_inner, mm.d_state, device=dev)))
             self.tok_buf = torch.zeros(B, 1, dtype=torch.long, device=dev)
             self.pos_buf = torch.zeros(1, dtype=torch.long, device=dev)
+            self.pos32 = torch.zeros(1, dtype=torch.int32, device=dev)
         # adopt the caller's states (None = start of sequence)
         for i, st in enumerate(self.states):
             given = None if mamba_states is None else mamba_states[i]
@@ -313,7 +335,10 @@ class DecodeEngine:
                 st[0].copy_(given[0])
                 st[1].copy_(given[1])
         self.tok_buf.copy_(last_token)
+        if not 0 <= int(step_index) < m.pos_embed.num_embeddings:   # pos_embed(step_index) raises (:226)
+            raise IndexError("index out of range in self")
         self.pos_buf.fill_(int(step_index))
+        self.pos32.fill_(int(step_index))
         step = self._step_rows if self.fused else self._step
         if not self.use_graph:
             logits = step(self.tok_buf, self.pos_buf, self.states)
