@@ -159,9 +159,11 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
   // compiler drain vmcnt, i.e. wait for the weights in flight
   // (a select after the load is sunk into a branch by the compiler: the
   // absent operands are masked bitwise instead)
+  // (dummy: the output row 0 / its packed image, valid for every column < N)
   const int mc = m < M ? m : M - 1;
-  const bf16_t* bias = a.bias ? (const bf16_t*)a.bias : (const bf16_t*)a.x;
-  const bf16_t* res = a.res ? (const bf16_t*)a.res + (int64_t)mc * a.ld_res : (const bf16_t*)a.x;
+  const bf16_t* dummy = (const bf16_t*)(a.y ? a.y : a.y_packed);
+  const bf16_t* bias = a.bias ? (const bf16_t*)a.bias : dummy;
+  const bf16_t* res = a.res ? (const bf16_t*)a.res + (int64_t)mc * a.ld_res : dummy;
   const uint32_t bmask = a.bias ? 0xffff0000u : 0u, rmask = a.res ? 0xffff0000u : 0u;
   float bv[4], rv[4];
   float4 cst[4], cwv[4];
