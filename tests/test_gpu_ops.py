@@ -760,3 +760,18 @@ def test_gemm_rows_ln_prologue_on_packed_x(M, N, K, film):
     y3, y3p = ops.gemm_rows(xp, wp, b, res=res, packed_out="also")
     assert torch.equal(y3p.unpack(), y3)
     assert torch.equal(y3, ops.gemm_rows(x, wp, b, res=res))
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 64), (3, 2048, 64)])
+def test_gemm_rows_packed_no_bias_wide_n_small_k(M, N, K):
+    """Packed projection without bias / residual where N far exceeds the x
+    operand's size (the absent operands' dummy loads must stay inside an
+    allocation): equals the float64 product within one bf16 rounding."""
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    y = ops.gemm_rows(x, ops.pack_rows_weight(w))
+    close(y, x.double() @ w.double().t(), rtol=2 ** -8, name="packed no-bias")
+    yp = ops.gemm_rows(ops.PackedAct.pack(x), ops.pack_rows_weight(w), packed_out="only")
+    assert torch.equal(yp.unpack(), y)
