@@ -431,7 +431,8 @@ int launch_gemv_packed(const MttsRowsArgs* a, hipStream_t st) {
     return MTTS_EINVAL;
   }
   if (a->ln_w && s > 8) {
-    set_error("gemm_rows: packed weights with the LayerNorm prologue need K <= 2048 (K=%d)", a->K);
+    set_error("gemm_rows: packed weights with the LayerNorm prologue need at most 8 k-steps per wave, "
+              "K <= 256 * waves = 2048 (K=%d, %d waves)", a->K, ks);
     return MTTS_EUNSUPPORTED;
   }
   switch (s) {
