@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 4
+#define MTTS_ABI_VERSION 5
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -295,6 +295,11 @@ typedef struct {
    * image of (batch, heads * head_dim) (xpk_index; batch <= 32, bf16) for
    * the output projection; out may then be NULL */
   void* out_packed;
+  /* q_len == 1 only, optional: element stride between heads of k / v
+   * (0 = head_dim, heads contiguous inside a row).  With k / v stored
+   * head-major (B, H, S, hd): k_bs = v_bs = H*S*hd, k_ls = v_ls = hd,
+   * kv_hs = S*hd, so each (batch, head) reads one contiguous K and V block. */
+  int64_t kv_hs;
 } MttsAttnFwdArgs;
 
 int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream);

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -107,7 +107,7 @@ class AttnFwdArgs(C.Structure):
                 ("q_bs", i64), ("q_ls", i64), ("k_bs", i64), ("k_ls", i64), ("v_bs", i64), ("v_ls", i64),
                 ("o_bs", i64), ("o_ls", i64), ("mask_bs", i64),
                 ("q", vp), ("k", vp), ("v", vp), ("key_padding_mask", vp), ("out", vp), ("lse", vp),
-                ("out_packed", vp)]
+                ("out_packed", vp), ("kv_hs", i64)]
 
 
 class AttnBwdArgs(C.Structure):

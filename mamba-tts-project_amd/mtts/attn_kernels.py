@@ -66,13 +66,27 @@ def _mask_u8(kpm, B, S):
 def attention_decode_packed(q, k, v, n_heads, kpm=None):
     """Single-query attention (q (B, d), decode step) returning the output
     as the packed activation image of the output projection (ops.PackedAct;
-    csrc/attn.hip single-pass decode kernel)."""
+    csrc/attn.hip single-pass decode kernel).  k / v: (B, S, d) channel-last,
+    or HEAD-MAJOR (B, H, S, hd) contiguous (the decode engine's per-context
+    copies): one contiguous K and V block per (batch, head)."""
     from .ops import PackedAct
     B, d = q.shape
     q3 = q[:, None]
-    k, v = _prep(k), _prep(v)
     if not _aligned(q3):
         q3 = q3.contiguous()
+    if k.dim() == 4:   # head-major
+        H, S, hd = k.shape[1:]
+        if H != n_heads or H * hd != d or not (k.is_contiguous() and v.is_contiguous()):
+            raise ValueError("attention_decode_packed: head-major k / v must be contiguous (B, H, S, hd)")
+        m = _mask_u8(kpm, B, S)
+        out = torch.empty(B, 1, d, device=q.device, dtype=q.dtype)
+        yp = PackedAct.empty(B, d, q.device)
+        a = _fwd_args(q3, k.view(B, H * S, hd), v.view(B, H * S, hd), n_heads, m, out, None)
+        a.kv_len, a.k_ls, a.v_ls, a.kv_hs = S, hd, hd, S * hd
+        a.out_packed = yp.data.data_ptr()
+        L.call("mtts_attention_fwd", a)
+        return yp
+    k, v = _prep(k), _prep(v)
     m = _mask_u8(kpm, B, k.shape[1])
     out = torch.empty(B, 1, d, device=q.device, dtype=q.dtype)
     yp = PackedAct.empty(B, d, q.device)

@@ -774,8 +774,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(MttsAttnFwdArgs a) {
   ld8((const T*)a.q + b * a.q_bs + hh * HD + d0, q);
 #pragma unroll
   for (int e = 0; e < 8; ++e) q[e] *= c;
-  const T* kb = (const T*)a.k + b * a.k_bs + hh * HD + d0;
-  const T* vb = (const T*)a.v + b * a.v_bs + hh * HD + d0;
+  const int64_t hs = a.kv_hs ? a.kv_hs : HD;
+  const T* kb = (const T*)a.k + b * a.k_bs + hh * hs + d0;
+  const T* vb = (const T*)a.v + b * a.v_bs + hh * hs + d0;
   float m = -INFINITY, l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j0 = g; j0 < a.kv_len; j0 += NG * U) {
     float kx[U][8], vx[U][8];
@@ -869,8 +870,9 @@ __global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
   const float c = a.scale * kLog2e;
   float q[8];
   ld8((const T*)a.q + b * a.q_bs + hh * HD + d0, q);
-  const T* kb = (const T*)a.k + b * a.k_bs + hh * HD + d0;
-  const T* vb = (const T*)a.v + b * a.v_bs + hh * HD + d0;
+  const int64_t hs = a.kv_hs ? a.kv_hs : HD;
+  const T* kb = (const T*)a.k + b * a.k_bs + hh * hs + d0;
+  const T* vb = (const T*)a.v + b * a.v_bs + hh * hs + d0;
   const uint8_t* mb = a.key_padding_mask ? a.key_padding_mask + b * a.mask_bs : (const uint8_t*)a.q;
   const uint32_t mmask = a.key_padding_mask ? 0xffu : 0u;
   float kx[U][8], vx[U][8];
@@ -1040,6 +1042,8 @@ void dispatch_bwd(const BwdParams& p, bool split, hipStream_t st) {
 extern "C" int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream) {
   int rc = check_fwd(a, "attention_fwd");
   if (rc) return rc;
+  MTTS_CHECK(a->kv_hs == 0 || (a->q_len == 1 && a->kv_hs % 8 == 0 && !getenv("MTTS_ATTN_DECODE_OFF")),
+             "attention_fwd: a k / v head stride is taken by the single-query kernels only (q_len 1)");
   // the packed image is written by the single-pass decode kernel only
   MTTS_CHECK(!a->out_packed || (a->q_len == 1 && a->dtype == MTTS_BF16 && a->batch <= 32 &&
                                 (a->heads * a->head_dim) % 32 == 0 && a->kv_len <= 8 * (256 / (a->head_dim / 8)) &&

@@ -226,6 +226,11 @@ class DecodeEngine:
             if (any(p[k].shape[0] % 32 or p[k].shape[1] % 32 for k in names)
                     or p["k"].shape[1] > 8 * (256 // (hd // 8)) or l.mamba.d_inner % 32):
                 return False
+        for l, p in zip(self.m.layers, c["layers"]):   # head-major K / V: one contiguous block per (b, h)
+            H = l.cross_attn.num_heads
+            Bk, S, d = p["k"].shape
+            p["khm"] = p["k"].reshape(Bk, S, H, d // H).permute(0, 2, 1, 3).contiguous()
+            p["vhm"] = p["v"].reshape(Bk, S, H, d // H).permute(0, 2, 1, 3).contiguous()
         for p in c["layers"]:   # FiLM rows as packed images (per-context constants)
             if "gamma_p" not in p:
                 p["gamma_p"] = ops.PackedAct.pack(p["gamma"])
@@ -255,7 +260,7 @@ class DecodeEngine:
                                  xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"], packed_out=True)
             x, xp = ops.gemm_rows(y, p["Wout_p"], res=x, packed_out="also")
             q = ops.gemm_rows(xp, p["Wq_p"], p["bq"], ln=ln(l.norm_cross))
-            o = attention_decode_packed(q, p["k"], p["v"], l.cross_attn.num_heads, c["kpm"])
+            o = attention_decode_packed(q, p["khm"], p["vhm"], l.cross_attn.num_heads, c["kpm"])
             x, xp = ops.gemm_rows(o, p["Wo_p"], p["bo"], res=x, packed_out="also")
             f = ops.gemm_rows(xp, p["W1_p"], p["b1"], "gelu", ln=ln(l.norm_ff, p["gamma_p"], p["beta_p"]),
                               packed_out="only")

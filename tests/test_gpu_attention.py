@@ -242,3 +242,23 @@ def test_single_query_fully_masked_and_generic_agree(dtype, monkeypatch):
     monkeypatch.setenv("MTTS_ATTN_DECODE_OFF", "1")
     out2, _ = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
     close(out[keep], out2[keep].double(), tol)
+
+
+@pytest.mark.parametrize("B,S,H,hd", [(32, 128, 8, 128), (3, 77, 4, 64), (2, 200, 2, 64)])
+def test_decode_head_major_kv_matches_channel_last(B, S, H, hd):
+    """Single-query attention reading head-major (B, H, S, hd) K / V copies
+    (kv_hs head stride; the decode engine's per-context layout) equals the
+    channel-last call bit for bit (same kernel arithmetic)."""
+    from mtts.attn_kernels import attention_decode_packed
+    g = torch.Generator(device="cpu").manual_seed(B + S + H)
+    d = H * hd
+    q = torch.randn(B, d, generator=g).to("cuda", torch.bfloat16)
+    kv = torch.randn(B, S, 2 * d, generator=g).to("cuda", torch.bfloat16)
+    kpm = torch.zeros(B, S, dtype=torch.bool, device="cuda")
+    kpm[:, S - 5:] = True
+    k, v = kv[..., :d], kv[..., d:]
+    a = attention_decode_packed(q, k, v, H, kpm)
+    khm = k.reshape(B, S, H, hd).permute(0, 2, 1, 3).contiguous()
+    vhm = v.reshape(B, S, H, hd).permute(0, 2, 1, 3).contiguous()
+    b = attention_decode_packed(q, khm, vhm, H, kpm)
+    assert torch.equal(a.unpack(), b.unpack())
