@@ -342,8 +342,10 @@ class DecodeEngine:
         self.tok_buf.copy_(last_token)
         if not 0 <= int(step_index) < m.pos_embed.num_embeddings:   # pos_embed(step_index) raises (:226)
             raise IndexError("index out of range in self")
-        self.pos_buf.fill_(int(step_index))
-        self.pos32.fill_(int(step_index))
+        if self.fused:   # the fused step embeds through mtts_embed_sum (int32 position id)
+            self.pos32.fill_(int(step_index))
+        else:
+            self.pos_buf.fill_(int(step_index))
         step = self._step_rows if self.fused else self._step
         if not self.use_graph:
             logits = step(self.tok_buf, self.pos_buf, self.states)
