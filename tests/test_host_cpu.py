@@ -58,3 +58,24 @@ def test_text_processor_batching():
     assert [s.tolist() for s in seqs] == [[vocab.index("HH")], [vocab.index("L"), vocab.index("OW1")]] and mask is None
     tab = tp.create_positional_encoding(10, 8)
     assert tab.shape == (10, 8) and float(tab[tp.padding_id].abs().sum()) == 0.0
+
+
+def test_packed_activation_layout_roundtrip_and_split_rules():
+    """Host side of the packed decode operands (csrc/common.h xpk_index): the
+    PackedAct image built by pack() holds element (m, k) at
+    ((k/32*2 + m/16)*64 + (k/8%4)*16 + m%16)*8 + k%8 and unpacks to the rows;
+    gemv_split_ok mirrors the kernel's wave split (K/32 = KS*S, KS <= 8,
+    S <= 16; <= 8 with the LayerNorm prologue)."""
+    from mtts import ops
+    M, K = 20, 96
+    x = torch.arange(M * K, dtype=torch.float32).view(M, K).to(torch.bfloat16)
+    p = ops.PackedAct.pack(x)
+    assert p.data.numel() == 32 * K and p.shape == (M, K)
+    flat = p.data
+    for m, k in [(0, 0), (5, 7), (19, 95), (16, 32), (3, 40)]:
+        idx = (((k >> 5) * 2 + (m >> 4)) * 64 + ((k >> 3) & 3) * 16 + (m & 15)) * 8 + (k & 7)
+        assert flat[idx] == x[m, k]
+    assert torch.equal(p.unpack(), x)
+    assert ops.gemv_split_ok(1024) and ops.gemv_split_ok(2048) and ops.gemv_split_ok(4096)
+    assert ops.gemv_split_ok(64) and not ops.gemv_split_ok(96) and not ops.gemv_split_ok(8192)
+    assert ops.gemv_split_ok(2048, ln=True) and not ops.gemv_split_ok(4096, ln=True)
