@@ -144,7 +144,10 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
 #ifdef GEMV_DIAG_NOW   // timing-only build (tools/diag_build.sh): no weight stream
     wf[j] = xf0[j];
 #else
-    wf[j] = wp[j * 64];   // (non-temporal loads measured equal)
+    // non-temporal: every weight byte is read once per step and the step's
+    // ~0.4 GB of weights exceed the Infinity Cache (decode p50 0.775 ->
+    // 0.755 ms, C4, three interleaved rounds; hot-cache per-call timings equal)
+    wf[j] = __builtin_nontemporal_load(wp + j * 64);
 #endif
   }
   // ---- epilogue operands, fetched before the product (threads < 128:
