@@ -739,7 +739,9 @@ __device__ __forceinline__ void dma16(const void* g, void* lds) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t l = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+  // nt: the u / delta / z tiles are read once (north-star fp32 fwd 2.185 ->
+  // 2.160 ms over three interleaved rounds; C2 shapes and bwd unchanged)
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(l) : "memory", "m0");
 #endif
 }
 // W-dword global load into registers, invisible to the compiler's wait
