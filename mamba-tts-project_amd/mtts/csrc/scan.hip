@@ -1924,10 +1924,18 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int c0 = (blockIdx.x * 4 + wave) * 64;
+  // XCD-aware: the gridDim.x blocks of one batch row (which share its B/C
+  // rows) on one XCD (dispatch assigns linear id % 8 to XCDs round-robin);
+  // bf16 north-star 1.993 -> 1.980 ms over three interleaved rounds, fp32 equal
+  int bx = blockIdx.x, b = blockIdx.y;
+  if ((gridDim.y & 7) == 0) {
+    const int id = blockIdx.x + gridDim.x * blockIdx.y, j = id >> 3;
+    b = (id & 7) * (gridDim.y >> 3) + j / gridDim.x;
+    bx = j % gridDim.x;
+  }
+  const int c0 = (bx * 4 + wave) * 64;
   if (c0 >= a.dim) return;  // dim % 64 == 0 (host); no barrier anywhere below
   const int c = c0 + lane;
-  const int b = blockIdx.y;
   const int L = a.seqlen;
   const int nt = (L + TT - 1) / TT;
 
