@@ -557,6 +557,7 @@ def main():
         f"(one fixed batch; the decoder's unshifted targets, SURVEY quirk 4, make it learn the identity fast)")
     rec = {
         "metric": "audio tokens/sec (teacher-forced fwd+bwd) per GPU; decode_step p50 latency",
+        "value_meaning": "whole job: tokens of all ranks / max-over-ranks time (value_per_gpu = value / n_gpus)",
         "value": tps, "value_per_gpu": tps / world, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",

@@ -29,11 +29,14 @@ def codec_ce_loss(logits: torch.Tensor, targets: torch.Tensor, pad_id: int = 0) 
     """Cross-entropy over flattened codec tokens; logits (B, T, V), targets
     (B, T) long; targets == pad_id are ignored; targets are NOT shifted."""
     B, T, V = logits.shape
-    if logits.is_cuda:   # csrc/loss.hip: the .float() upcast happens in registers
+    x = logits.reshape(B * T, V)
+    if logits.is_cuda and logits.dtype in (torch.float32, torch.bfloat16) and x.stride(1) == 1:
+        # csrc/loss.hip (fp32 / bf16 logits, unit column stride): the fp32
+        # upcast happens in registers
         from mtts.loss import cross_entropy
-        x = logits.reshape(B * T, V)
-        return cross_entropy(x if x.stride(1) == 1 else x.contiguous(), targets.reshape(B * T), ignore_index=pad_id)
-    return F.cross_entropy(logits.reshape(B * T, V).float(), targets.reshape(B * T), ignore_index=pad_id)
+        return cross_entropy(x, targets.reshape(B * T), ignore_index=pad_id)
+    # any other dtype / layout: F.cross_entropy exactly as train.py:38-42
+    return F.cross_entropy(x, targets.reshape(B * T), ignore_index=pad_id)
 
 
 def flatten_codec_tokens(codec_tokens: torch.Tensor):

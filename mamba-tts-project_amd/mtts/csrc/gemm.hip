@@ -599,6 +599,11 @@ extern "C" int mtts_gemm(const MttsGemmArgs* a, void* stream) {
   MTTS_CHECK(!f32out || epi == 0, "gemm: epilogues apply to bf16 output only");
   MTTS_CHECK(f32out || splits == 1, "gemm: split-K needs fp32 output");
   MTTS_CHECK(!(epi & MTTS_GEMM_EPI_BIAS) || a->bias, "gemm: bias epilogue without bias");
+  // the epilogue reads the bias as f32x4 (fp32) / uint2 (bf16) and aux as uint2 / uint4
+  MTTS_CHECK(!(epi & MTTS_GEMM_EPI_BIAS) || (uintptr_t)a->bias % (a->bias_dtype == 1 ? 8 : 16) == 0,
+             "gemm: bias must be %d-byte aligned", a->bias_dtype == 1 ? 8 : 16);
+  MTTS_CHECK(!(epi & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) || (uintptr_t)a->aux % 8 == 0,
+             "gemm: aux must be 8-byte aligned");
   MTTS_CHECK(!(epi & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) || (a->aux && a->ld_aux % 4 == 0),
              "gemm: GELU epilogues need aux (ld_aux multiple of 4)");
   MTTS_CHECK((epi & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) != (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU),

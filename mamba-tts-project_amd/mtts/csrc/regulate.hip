@@ -237,14 +237,21 @@ __global__ __launch_bounds__(256) void embed_sum_kernel(const int64_t* __restric
   const int l0 = blockIdx.x * rpb;
   for (int l = l0 + w; l < min(L, l0 + rpb); l += 4) {
     const int64_t t = tok[b * tok_bs + l];
+    T* __restrict__ o = out + b * o_bs + (int64_t)l * d;
     if (t < 0 || t >= V) {
-      if (lane == 0) err[0] = 1;  // nn.Embedding would raise; the host checks the flag
+      // nn.Embedding would raise; the host checks the flag (mtts.embed.check_errors,
+      // the decode engine once per step).  The row is written as zeros so no
+      // uninitialised memory flows on.
+      if (lane == 0) err[0] = 1;
+      for (int c = lane; c < d / 4; c += 64) {
+        if constexpr (sizeof(T) == 4) reinterpret_cast<float4*>(o)[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        else reinterpret_cast<uint2*>(o)[c] = make_uint2(0u, 0u);
+      }
       continue;
     }
     const float4* __restrict__ a = reinterpret_cast<const float4*>(tw + t * d);
     const float4* __restrict__ q = reinterpret_cast<const float4*>(qw + (int64_t)qid[l] * d);
     const float4* __restrict__ p = reinterpret_cast<const float4*>(pw + (int64_t)pid[l] * d);
-    T* __restrict__ o = out + b * o_bs + (int64_t)l * d;
     for (int c = lane; c < d / 4; c += 64) {
       const float4 x = a[c], y = q[c], z = p[c];
       const float s0 = (x.x + z.x) + y.x, s1 = (x.y + z.y) + y.y, s2 = (x.z + z.z) + y.z, s3 = (x.w + z.w) + y.w;

@@ -222,9 +222,10 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
   }
   if constexpr (SK) {
     if (KG > 1) {
-      // write-through (sc1) slab stores: no release fence; one relaxed
-      // agent-scope ticket; the last arriver reads every slab with sc1 loads
-      // (no acquire), all loads issued before the fixed-order sum
+      // write-through (sc1) slab stores, drained by every wave, then ONE
+      // agent-scope RELEASE ticket per workgroup; the last arriver runs an
+      // agent-scope ACQUIRE fence before it reads the slabs (HIP memory model;
+      // the sc1 loads alone would rest on hardware behaviour)
       float* slab = a.splitk_slab + (int64_t)tile * KG * 1024;
 #pragma unroll
       for (int e = 0; e < E; ++e)
@@ -233,14 +234,15 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
-        const int old = __hip_atomic_fetch_add(a.splitk_count + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int old = __hip_atomic_fetch_add(a.splitk_count + tile, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == KG - 1;
         if (last) __hip_atomic_store(a.splitk_count + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = last;
       }
       __syncthreads();
       if (!s_last) return;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the ticket
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // invalidates this CU's L1: other CUs' slabs
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         float v[32];

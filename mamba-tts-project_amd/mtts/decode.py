@@ -73,6 +73,8 @@ class DecodeEngine:
         self.reset()
 
     def reset(self):
+        self._err_host = None
+        self._err_ev = None
         self.xpk = False
         self.ctx_key = None
         self.ctx_refs = None
@@ -300,11 +302,31 @@ class DecodeEngine:
         h, _ = ops.layer_norm(pending, m.norm_out.weight, m.norm_out.bias, m.norm_out.eps, res=x)
         return mm_(h, c["Wh"], c["bh"])[:, None]
 
+    # -- out-of-range token ids --------------------------------------------------
+    def _check_token_flag(self, dev):
+        """The fused step embeds through mtts_embed_sum, which zero-fills and
+        flags a row whose token id is outside token_embed (nn.Embedding raises
+        there, mamba_decoder.py:217).  The flag of an earlier step is read from
+        a pinned copy once its event has completed (no host sync), so a bad id
+        raises IndexError at the next decode_step call at the latest."""
+        if self._err_ev is not None and self._err_ev.query() and int(self._err_host[0]) != 0:
+            self._err_host.zero_()
+            _err_flag(dev).zero_()
+            raise IndexError("decode_step: last_token id out of range of token_embed (index out of range in self)")
+
+    def _post_token_flag(self, dev):
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._err_ev = torch.cuda.Event()
+        self._err_host.copy_(_err_flag(dev), non_blocking=True)
+        self._err_ev.record()
+
     # -- public ----------------------------------------------------------------
     @torch.no_grad()
     def step(self, last_token, text_hidden, z_style, mamba_states, step_index, text_mask=None, ref_hidden=None,
              ref_mask=None):
         m = self.m
+        self._check_token_flag(last_token.device)
         cd = m._cd()
         conds = (text_hidden, z_style, text_mask, ref_hidden, ref_mask)
         key = (cd, tuple(last_token.shape))
@@ -349,6 +371,8 @@ class DecodeEngine:
         step = self._step_rows if self.fused else self._step
         if not self.use_graph:
             logits = step(self.tok_buf, self.pos_buf, self.states)
+            if self.fused:
+                self._post_token_flag(dev)
             return logits, list(self.states)
         if self.graph is None:
             saved = [(a.clone(), b.clone()) for a, b in self.states]
@@ -369,4 +393,6 @@ class DecodeEngine:
                 b.copy_(sb)
             self.graph = g
         self.graph.replay()
+        if self.fused:
+            self._post_token_flag(dev)
         return self.out_buf.clone(), list(self.states)

@@ -10,7 +10,16 @@ into buckets of `bucket_mb`.  A post-accumulate-grad hook counts finished
 parameters per bucket; a full bucket is all-reduced asynchronously while the
 backward continues (overlap), and `finish()` waits for the stragglers and
 applies the 1/world averaging.  Large buckets (default 128 MB) suit xGMI's
-point-to-point links: few, large ring collectives.
+point-to-point links: few, large ring collectives.  The FIRST bucket (the
+parameters whose gradients the backward finishes first: the head and the
+last layer) is capped at `first_bucket_mb` so the first all-reduce starts
+early in the backward.
+
+`comm_dtype=torch.bfloat16` all-reduces a bf16 image of each bucket (half
+the bytes on the links; the fp32 gradients are rounded once to bf16 before
+the sum and the bf16 sum is widened back into the fp32 buffer before the
+averaging), the gradient-compression option for xGMI-bound steps.  The
+default is fp32 (exact sums up to the collective's order).
 """
 from __future__ import annotations
 
@@ -19,7 +28,8 @@ import torch.distributed as dist
 
 
 class GradAllReduce:
-    def __init__(self, params, bucket_mb: float = 128.0, group=None):
+    def __init__(self, params, bucket_mb: float = 128.0, group=None, first_bucket_mb: float = 8.0,
+                 comm_dtype: torch.dtype = None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.params = [p for p in params if p.requires_grad]
@@ -28,7 +38,11 @@ class GradAllReduce:
         dtype = order[0].dtype
         total = sum(p.numel() for p in order)
         self.flat = torch.zeros(total, device=dev, dtype=dtype)
-        cap = max(1, int(bucket_mb * 1024 * 1024 // self.flat.element_size()))
+        cap_rest = max(1, int(bucket_mb * 1024 * 1024 // self.flat.element_size()))
+        cap = max(1, int(min(first_bucket_mb, bucket_mb) * 1024 * 1024 // self.flat.element_size()))
+        if comm_dtype is not None and comm_dtype not in (torch.bfloat16, dtype):
+            raise TypeError("GradAllReduce: comm_dtype must be None, the parameter dtype or torch.bfloat16")
+        self.comm_dtype = None if comm_dtype in (None, dtype) else comm_dtype
         self.buckets = []        # (start, end, n_params)
         self.bucket_of = {}
         off, start, count = 0, 0, 0
@@ -45,8 +59,10 @@ class GradAllReduce:
             if off - start >= cap:
                 self.buckets.append([start, off, count])
                 start, count = off, 0
+                cap = cap_rest
         if count:
             self.buckets.append([start, off, count])
+        self.cbuf = None if self.comm_dtype is None else torch.empty(total, device=dev, dtype=self.comm_dtype)
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
@@ -72,17 +88,27 @@ class GradAllReduce:
         b = self.bucket_of[p]
         self.pending[b] += 1
         if self.pending[b] == self.buckets[b][2]:
-            s, e, _ = self.buckets[b]
+            self._launch(b)
+
+    def _launch(self, b):
+        s, e, _ = self.buckets[b]
+        if self.cbuf is None:
             self.handles[b] = dist.all_reduce(self.flat[s:e], group=self.group, async_op=True)
+        else:
+            self.cbuf[s:e].copy_(self.flat[s:e])          # one rounding to the wire dtype
+            self.handles[b] = dist.all_reduce(self.cbuf[s:e], group=self.group, async_op=True)
 
     def finish(self):
         """Wait for every bucket (launching any whose hooks did not all fire,
         e.g. unused parameters) and average over ranks."""
-        for b, (s, e, _) in enumerate(self.buckets):
+        for b in range(len(self.buckets)):
             if self.handles[b] is None:
-                self.handles[b] = dist.all_reduce(self.flat[s:e], group=self.group, async_op=True)
-        for h in self.handles:
+                self._launch(b)
+        for b, h in enumerate(self.handles):
             h.wait()
+            if self.cbuf is not None:
+                s, e, _ = self.buckets[b]
+                self.flat[s:e].copy_(self.cbuf[s:e])
         for p, v in self.views.items():
             if p.grad is not None and p.grad is not v and p.grad.data_ptr() != v.data_ptr():
                 raise RuntimeError("GradAllReduce: a gradient left the flat buffer after its hook; "

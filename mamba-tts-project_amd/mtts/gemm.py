@@ -34,6 +34,17 @@ def nt_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
             and a.shape[1] == b.shape[1] and a.shape[1] % 64 == 0 and b.shape[0] % 8 == 0 and a.shape[0] > 0)
 
 
+def epi_ok(bias: torch.Tensor = None, aux: torch.Tensor = None) -> bool:
+    """Epilogue operand alignment the kernel reads with (mirrors mtts_gemm's
+    checks): fp32 bias 16-byte, bf16 bias 8-byte aligned; the GELU /
+    GELU-backward aux rows 8-byte aligned with ld_aux % 4 == 0."""
+    if bias is not None and bias.data_ptr() % (16 if bias.dtype == torch.float32 else 8) != 0:
+        return False
+    if aux is not None and (aux.data_ptr() % 8 != 0 or aux.stride(0) % 4 != 0 or aux.stride(-1) != 1):
+        return False
+    return True
+
+
 def tn_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
     return (ENABLED and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.is_cuda
             and _rowmajor(a) and _rowmajor(b)
@@ -47,6 +58,8 @@ def mm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor = None, gelu_aux:
     epilogue (C = bf16(AB) · gelu'(dgelu_aux))."""
     m, k = a.shape
     n = b.shape[0]
+    if not epi_ok(bias, gelu_aux if gelu_aux is not None else dgelu_aux):
+        raise ValueError("mm_nt: bias / aux not aligned for the epilogue's vector accesses (gemm.epi_ok)")
     if out is None:
         out = torch.empty(m, n, device=a.device, dtype=torch.bfloat16)
     args = L.GemmArgs()
