@@ -30,9 +30,10 @@ Also reported on rank 0 at N = 1 (same JSON line):
   roofline_bf16 the same with bf16 I/O (VALU-bound: DESIGN.md section 3)
   step_mfma     the step's algorithmic FLOPs / step time vs dense bf16 peak
   decode        decode_step p50/p90 latency (C4, B=32, 12L)
-  c5_decoder    the decoder step at train.py's shape:
-                T_audio = 5x1024 flattened codec streams, voice prompt as
-                5120 reference keys (T_kv = 5248), tokens/s and TFLOP/s
+  c5_step       BASELINE configs[4]: the whole train.py step (text encoder,
+                duration loss, style pipeline, voice-prompt reference, 8L
+                d_model=512 decoder at T_audio = 5x1024, 3-term loss, clip +
+                Adam) on synthetic batches, B=8 per rank, every N
   text_encoder  TextEncoder + DurationPredictor fwd+bwd
   style         style pipeline: HIP length regulator
                 roofline, StyleConditioningPipeline eval / train times
@@ -306,55 +307,50 @@ def style_bench(B=8, T_text=128, d_model=1024, d_style=256, iters=20):
             "pipeline_eval_ms": eval_ms, "pipeline_train_fwd_bwd_ms": train_ms}
 
 
-def c5_decoder_bench(B=4, Q=5, T_frames=1024, T_text=128, steps=3):
-    """SURVEY §8f row 3 / configs[4]'s decoder: the train.py shape -- 5 FACodec
-    streams of 1024 frames flattened to T_audio = 5120, the voice prompt
-    embedded as reference (embed_codec_tokens, 5120 keys) in front of the
-    text (T_kv = 5248), codec_ce_loss, fused clip + Adam; 12L d=1024 bf16."""
-    import mamba_decoder
-    import codec_tokens as ct
-    from mtts.optim import FusedClipAdam
-    dev = "cuda"
+def c5_step_bench(rank, world, dev, B=8, T_text=128, T_codec=1024, T_ref=1024, steps=3, warmup=2):
+    """BASELINE configs[4] (C5): one train.py step (train.py:168-241) on
+    synthetic batches through train_harness.TrainStep at train.py's widths
+    (build_models: d_model 512, d_style 256, 8-layer decoder, 5 FACodec
+    streams of 1024 frames flattened to T_audio = 5120, the voice prompt as
+    5120 reference keys + 128 text keys, text encoder 4 FFT blocks, duration
+    predictor, style pipeline (dead output, as in train.py), 3-term loss,
+    clip (decoder) + Adam), decoder in bf16, dropout 0.1 as train.py, B per
+    rank; with N ranks the gradients of every trainable parameter are
+    all-reduced over RCCL before the optimizer (batch DP, weak scaling).
+    Timed like the headline: barrier + synchronize on both sides, max over
+    ranks; tokens = audio tokens (B * 5120) of all ranks."""
+    import train_harness as th
     torch.manual_seed(0)
-    m = mamba_decoder.MambaTTSDecoder(10, d_model=1024, n_layers=12, n_heads=8, d_ff=2048, d_style=256,
-                                      num_quantizers=Q).to(dev)
-    m.compute_dtype = torch.bfloat16
-    g = torch.Generator(device=dev).manual_seed(5)
-    codec = torch.randint(0, 10, (B, T_frames, Q), device=dev, generator=g)
-    voice = torch.randint(0, 10, (B, T_frames, Q), device=dev, generator=g)
-    text = torch.randn(B, T_text, 1024, device=dev, generator=g)
-    z = torch.randn(B, 256, device=dev, generator=g)
-    tmask = torch.ones(B, T_text, dtype=torch.bool, device=dev)
-    audio, _, _ = ct.flatten_codec_tokens(codec)
-    _, v3, _ = ct.flatten_codec_tokens(voice)
-    params = list(m.parameters())
-    opt = FusedClipAdam(params, lr=1e-4, max_grad_norm=1.0)
-
-    def step():
-        ref, vmask = ct.embed_codec_tokens(v3, m)
-        logits = m(audio, text, z, text_mask=tmask, ref_hidden=ref, ref_mask=vmask)
-        loss = ct.codec_ce_loss(logits, audio)
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        opt.step()
-        return loss
-    for _ in range(2):
-        step()
+    models = th.build_models(dev, compute_dtype=torch.bfloat16)
+    dp = None
+    if world > 1:
+        from mtts.dp import GradAllReduce
+        trainable = [p for m in (models.text_encoder, models.dur_predictor, models.decoder)
+                     for p in m.parameters() if p.requires_grad]
+        dp = GradAllReduce(trainable, bucket_mb=128)
+    step = th.TrainStep(models, lr=1e-4, grad_allreduce=dp)
+    batch = th.synthetic_batch(B, dev, T_text=T_text, T_codec=T_codec, T_ref=T_ref, seed=77 + rank)
+    for _ in range(warmup):
+        first = step(batch)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        loss = step()
+        out = step(batch)
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / steps * 1e3
-    T = Q * T_frames
-    T_kv = Q * T_frames + T_text
-    c = dict(C2, B=B, T=T, T_text=T_kv)
-    fl = flops_per_step(c)
-    attn_fl = 3 * 12 * 4 * B * T * T_kv * 1024
-    del m, opt
+    if world > 1:
+        dist.barrier()
+    dt = _max_over_ranks(time.perf_counter() - t0, world, dev)
+    ms = dt / steps * 1e3
+    T_audio = T_codec * th.CODEC_STREAMS
+    res = {"B_per_rank": B, "T_audio": T_audio, "T_kv": T_ref * th.CODEC_STREAMS + T_text, "T_text": T_text,
+           "n_gpus": world, "ms_per_step": ms, "tokens_per_s": world * B * T_audio / dt * steps,
+           "dtype": "decoder bf16, text encoder / duration predictor / style pipeline fp32",
+           "losses_first_last": [float(first["loss_total"]), float(out["loss_total"])]}
+    del models, step, dp
     torch.cuda.empty_cache()
-    return {"B": B, "T_audio": T, "T_kv": T_kv, "ms_per_step": ms, "tokens_per_s": B * T / ms * 1e3,
-            "tflops": fl / ms / 1e9, "attention_share_of_flops": attn_fl / fl, "loss": float(loss.item())}
+    return res
 
 
 def text_bench(B=8, T_text=128, d_model=512, iters=10):
@@ -590,9 +586,10 @@ def main():
             rec["roofline_bf16"] = {"bound": "hbm (VALU-limited, DESIGN.md section 3)", "achieved": sbw / 1e9,
                                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": sbw / HBM_PEAK, "ms": sms,
                                     "algorithmic_bytes": sb, "traffic": pmc_traffic("bf16")}
+    if not args.skip_extras:
+        rec["c5_step"] = c5_step_bench(rank, world, dev)
+        log(f"[bench] c5 step {rec['c5_step']}")
     if rank == 0 and world == 1 and not args.skip_extras:
-        rec["c5_decoder"] = c5_decoder_bench()
-        log(f"[bench] c5 decoder {rec['c5_decoder']}")
         rec["text_encoder"] = text_bench()
         log(f"[bench] text encoder {rec['text_encoder']}")
         rec["style"] = style_bench()

@@ -355,3 +355,95 @@ def decode_step_ref(p, n_layers, n_heads, last_token, text_hidden, z_style, stat
         new_states.append(s)
     x = layer_norm_ref(x, p["norm_out.weight"], p["norm_out.bias"])
     return x @ p["head.weight"].T + p["head.bias"], new_states
+
+
+# --------------------------------------------------------------------------
+# Style pipeline and the train.py step (SURVEY §8f rows 1-4, configs[4] = C5)
+# --------------------------------------------------------------------------
+
+def style_pipeline_ref(p, text_hidden, style_emb, durations, n_heads, max_len=None):
+    """Restates StyleConditioningPipeline.forward (style_cross_attention.py:316-354)
+    with dropout off: StyleProjection (:49-66: Linear -> LayerNorm, unsqueezed
+    to one token), the two cross-attention blocks (:112-141 / :258-286:
+    x = LN(x + MHA(x, K, V)); x = LN(x + W2 GELU(W1 x)) ) around the
+    LengthRegulator (:156-198).  p keys as the pipeline's state_dict."""
+    def proj(pre):
+        h = style_emb @ p[pre + ".0.weight"].T + p[pre + ".0.bias"]
+        return layer_norm_ref(h, p[pre + ".1.weight"], p[pre + ".1.bias"])[:, None]
+
+    K, V = proj("style_proj.key_proj"), proj("style_proj.value_proj")
+
+    def block(pre, x):
+        a = _mha_kv_ref(x, K, V, p[pre + ".cross_attn.in_proj_weight"], p[pre + ".cross_attn.in_proj_bias"],
+                        p[pre + ".cross_attn.out_proj.weight"], p[pre + ".cross_attn.out_proj.bias"], n_heads)
+        x = layer_norm_ref(x + a, p[pre + ".norm.weight"], p[pre + ".norm.bias"])
+        f = F.gelu(x @ p[pre + ".ffn.0.weight"].T + p[pre + ".ffn.0.bias"]) @ p[pre + ".ffn.3.weight"].T \
+            + p[pre + ".ffn.3.bias"]
+        return layer_norm_ref(x + f, p[pre + ".ffn_norm.weight"], p[pre + ".ffn_norm.bias"])
+
+    styled = block("cross_attn_1", text_hidden)
+    up, lengths = length_regulator_ref(styled, durations, max_len)
+    return block("cross_attn_2", up), lengths, K, V
+
+
+def _mha_kv_ref(q_in, k_in, v_in, in_w, in_b, out_w, out_b, n_heads):
+    """nn.MultiheadAttention(query, key, value) with distinct key / value inputs."""
+    Bsz, T, d = q_in.shape
+    S = k_in.shape[1]
+    hd = d // n_heads
+    q = (q_in @ in_w[:d].T + in_b[:d]).view(Bsz, T, n_heads, hd).transpose(1, 2)
+    k = (k_in @ in_w[d:2 * d].T + in_b[d:2 * d]).view(Bsz, S, n_heads, hd).transpose(1, 2)
+    v = (v_in @ in_w[2 * d:].T + in_b[2 * d:]).view(Bsz, S, n_heads, hd).transpose(1, 2)
+    pr = torch.softmax((q @ k.transpose(-1, -2)) / math.sqrt(hd), dim=-1)
+    return (pr @ v).transpose(1, 2).reshape(Bsz, T, d) @ out_w.T + out_b
+
+
+def heuristic_durations_ref(text_mask, target_frames):
+    """Restates train.py:84-97 (the per-row Python loop as written there)."""
+    B, T = text_mask.shape
+    lengths = (~text_mask).sum(dim=1).clamp(min=1)
+    per_ph = torch.div(target_frames, lengths, rounding_mode="floor").clamp(min=1)
+    durations = torch.zeros_like(text_mask, dtype=torch.float)
+    for b in range(B):
+        durations[b, : lengths[b]] = per_ph[b]
+    return durations
+
+
+def duration_loss_ref(log_duration_pred, duration_target, mask=None):
+    """Restates DurationPredictor.compute_loss (text_encoder.py:183-209): MSE in
+    the log domain, masked mean over non-pad phonemes."""
+    log_t = torch.log(duration_target.to(log_duration_pred.dtype) + 1e-8)
+    loss = F.mse_loss(log_duration_pred, log_t, reduction="none")
+    if mask is not None:
+        return loss.masked_fill(mask, 0.0).sum() / (~mask).sum().to(loss.dtype)
+    return loss.mean()
+
+
+def train_step_losses_ref(p_te, p_dur, p_dec, batch, te_cfg, dec_cfg, w_codec=1.0, w_dur=0.1, w_smsd=0.5):
+    """Restates the loss of one train.py step (train.py:168-230) on a synthetic
+    batch, dropout off, SMSD absent (spk_embs None -> loss_smsd = 0, :192;
+    z_style = the batch's fixed style vector in place of smsd(style_prompts)):
+    text_encoder -> duration predictor + heuristic-duration loss -> decoder on
+    the flattened codec tokens with the voice prompt embedded as reference ->
+    codec CE.  The style pipeline's output is dead in train.py (:206-210) and
+    enters no loss.  Returns (loss_total, loss_codec, loss_dur, logits,
+    text_hidden, log_dur_pred)."""
+    codec = batch["codec_tokens"]
+    B, T_codec, C = codec.shape
+    audio_tokens = codec.permute(0, 2, 1).reshape(B, -1)                          # :181-182
+    ids, tmask = batch["phoneme_ids"], batch["text_mask"]
+    text_hidden = text_encoder_ref(p_te, ids, tmask, te_cfg["n_layers"], te_cfg["n_head"], te_cfg["d_k"],
+                                   te_cfg.get("kernel", (9, 1)))                   # :188
+    log_dur = duration_predictor_ref(p_dur, text_hidden, tmask)                    # :198
+    dur_t = heuristic_durations_ref(tmask, audio_tokens.shape[1])                  # :201
+    loss_dur = duration_loss_ref(log_dur, dur_t, tmask)                            # :202
+    v3 = batch["voice_codec"].permute(0, 2, 1)                                     # :216
+    ref_hidden, vmask = embed_codec_tokens_ref(v3, p_dec["token_embed.weight"], p_dec["pos_embed.weight"],
+                                               p_dec["quant_embed.weight"])        # :217
+    logits = decoder_forward_ref(p_dec, dec_cfg["n_layers"], dec_cfg["n_heads"], audio_tokens, text_hidden,
+                                 batch["style_emb"].to(text_hidden.dtype), text_mask=tmask, ref_hidden=ref_hidden,
+                                 ref_mask=vmask)                                    # :220-227
+    loss_codec = codec_ce_loss_ref(logits, audio_tokens)                           # :228
+    loss_smsd = torch.zeros((), dtype=logits.dtype)
+    total = w_codec * loss_codec + w_dur * loss_dur + w_smsd * loss_smsd           # :230
+    return total, loss_codec, loss_dur, logits, text_hidden, log_dur

@@ -237,3 +237,34 @@ def test_bf16_decode_engine_c4_shapes(B):
         outs.append(torch.cat(seq, 1))
     assert (B <= 32) == DecodeEngine(m)._fused_ok(torch.bfloat16, B)
     close(outs[0], outs[1], rtol=3e-2, name=f"engine vs module path, B={B}")
+
+
+def test_decode_engine_out_of_range_token_raises():
+    """A last_token outside token_embed: the reference's nn.Embedding raises
+    (mamba_decoder.py:217).  The fused engine embeds through mtts_embed_sum,
+    which zero-fills the row (no uninitialised memory reaches the logits or
+    the states) and flags it; the engine reads the flag without a host sync
+    and raises IndexError at the next decode_step call at the latest, then
+    clears it (the following steps run normally)."""
+    import mamba_decoder
+    torch.manual_seed(1)
+    m = mamba_decoder.MambaTTSDecoder(10, d_model=1024, n_layers=2, n_heads=8, d_ff=2048, d_style=256).to(DEV).eval()
+    m.compute_dtype = torch.bfloat16
+    B = 4
+    text = torch.randn(B, 16, 1024, device=DEV)
+    z = torch.randn(B, 256, device=DEV)
+    good = torch.randint(0, 10, (B, 1), device=DEV)
+    bad = good.clone()
+    bad[2, 0] = 10
+    with torch.no_grad():
+        lg, st = m.decode_step(good, text, z, [None, None], 0)
+        assert m._engine.fused
+        lg, st = m.decode_step(bad, text, z, st, 1)
+        assert torch.isfinite(lg).all()
+        torch.cuda.synchronize()
+        with pytest.raises(IndexError, match="out of range"):
+            m.decode_step(good, text, z, st, 2)
+        lg, st = m.decode_step(good, text, z, st, 2)
+        torch.cuda.synchronize()
+        lg, st = m.decode_step(good, text, z, st, 3)
+        assert torch.isfinite(lg).all()

@@ -5,4 +5,4 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mamba-tts-project_amd")]
 import bench  # noqa: E402
-print(json.dumps(bench.c5_decoder_bench(steps=2)))
+print(json.dumps(bench.c5_step_bench(0, 1, "cuda", steps=2)))
