@@ -24,7 +24,7 @@ from oracle import mamba_ref as R
 pytestmark = pytest.mark.gpu
 
 SMALL = dict(d_model=64, d_style=16, dec_layers=2, dec_heads=4, d_ff=128, text_layers=2, text_heads=2, text_d_k=32,
-             text_d_inner=128, dur_filter=32, style_heads=4, max_len=256, dropout=0.0)
+             text_d_inner=128, dur_filter=64, style_heads=4, max_len=256, dropout=0.0)
 
 
 def _perturb(mods, seed):
@@ -40,7 +40,9 @@ def _perturb(mods, seed):
 
 
 def _params64(mod):
-    return {k: v.detach().cpu().double().requires_grad_(v.requires_grad) for k, v in mod.state_dict().items()}
+    """float64 CPU copies of the state_dict; the trainable ones require grad."""
+    train = {k for k, v in mod.named_parameters() if v.requires_grad}
+    return {k: v.detach().cpu().double().requires_grad_(k in train) for k, v in mod.state_dict().items()}
 
 
 @pytest.mark.parametrize("B,T_text,T_codec,T_ref", [(2, 12, 24, 16), (3, 9, 40, 8)])
@@ -101,8 +103,8 @@ def test_c5_train_step_vs_oracle(B, T_text, T_codec, T_ref):
     for n, mod in (("te", models.text_encoder), ("dur", models.dur_predictor), ("dec", models.decoder)):
         ref = {"te": p_te, "dur": p_dur, "dec": p_dec}[n]
         for k, v in mod.named_parameters():
-            if ref[k].grad is None:
-                continue
+            if ref[k].grad is None or ref[k].grad.abs().max() < 1e-9:
+                continue   # exact-zero reference gradient: Adam normalises fp32 rounding noise (checked above)
             w = before[n][k].clone().requires_grad_(True)
             w.grad = ref[k].grad.double() * (coef if n == "dec" else 1.0)
             opt = torch.optim.Adam([w], lr=1e-3)

@@ -353,10 +353,10 @@ def test_c4_decode_4096_steps_vs_teacher_forced():
     of its rows, both with quant_embed zeroed: decode_step adds no quantizer
     embedding (quirk 2, mamba_decoder.py:217-221), so with that row zero the
     two paths compute the same function at every position.  Checked at
-    positions 0..3, 100, 1000, 2047, 3000, 4094, 4095: logits within 5e-2
-    (engine vs bf16 forward) and 1e-1 (vs float64) of the logit scale, i.e.
-    no drift of the SSM / conv states over 4096 steps; every state finite at
-    step 4095."""
+    positions 0..3, 100, 1000, 2047, 3000, 4094, 4095: logits within 2e-2
+    (engine vs bf16 forward; measured 7.6e-3) and 3e-2 (vs float64; measured
+    1.0e-2) of the logit scale, i.e. no drift of the SSM / conv states over
+    4096 steps; every state finite at step 4095."""
     m = _decoder(1024, 12, d_ff=2048).eval()
     m.compute_dtype = torch.bfloat16
     with torch.no_grad():
@@ -382,11 +382,11 @@ def test_c4_decode_4096_steps_vs_teacher_forced():
     steps = [0, 1, 2, 3, 100, 1000, 2047, 3000, 4094, 4095]
     e_tf = _rel_err(out[:, steps], tf[:, steps])
     print(f"C4 engine vs teacher-forced bf16: {e_tf:.3e} of the logit scale")
-    assert e_tf <= 5e-2, e_tf
+    assert e_tf <= 2e-2, e_tf
     rows = [0, 5]
     p = _params64(m)
     with torch.no_grad():
         ref = R.decoder_forward_ref(p, 12, 8, tok[rows], text[rows].double(), z[rows].double(), text_mask=mask[rows])
     e_ref = _rel_err(out[rows][:, steps], ref[:, steps])
     print(f"C4 engine vs float64 oracle: {e_ref:.3e} of the logit scale")
-    assert e_ref <= 1e-1, e_ref
+    assert e_ref <= 3e-2, e_ref
