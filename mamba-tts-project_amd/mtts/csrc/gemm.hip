@@ -218,6 +218,161 @@ __device__ __forceinline__ s16x8 frag(const char* region, int rb, int ks, int la
   }
 }
 
+// Epilogue shared by the kernels: the wave's 128x64 accumulator tile
+// (acc[MB][NB], lane rows m = MB*16 + (lane&15), columns 4*(lane>>4) + j of
+// block NB) -> bf16 (+bias / GELU / GELU-backward) or fp32 (split slab, beta).
+template <int EPI, bool OUT_F32>
+__device__ __forceinline__ void store_tile(const GemmParams& p, f32x4 (&acc)[8][4], int m0, int n0, int wr, int wc,
+                                           int lane, int split) {
+  // lane holds rows m = .. + (lane&15), columns n = .. + 4*(lane>>4) + j
+  const int rl = lane & 15, cl = 4 * (lane >> 4);
+  // wave-uniform: the wave's whole 128x64 sub-tile in bounds (no per-lane masks)
+  const bool full = m0 + wr * 128 + 128 <= p.m && n0 + wc * 64 + 64 <= p.n;
+  if constexpr (!OUT_F32) {
+   if (p.wide_out) {
+    // bf16 out: the 16-lane rows g and g^1 of the wave hold adjacent 4-column
+    // groups of the same output rows; one v_permlane16_swap per dword of a
+    // (NB, NB+1) pair gives each lane 8 consecutive columns, so the tile
+    // leaves as 16 dwordx4 stores per lane instead of 32 dwordx2 (the store
+    // tail is issue-bound: cdna_hip_programming.md T21).  After the swap the
+    // even rows hold block 2pr columns 8(g>>1)..+7, the odd rows block 2pr+1.
+    const int g = lane >> 4;
+    const int cw0 = n0 + wc * 64 + (g & 1) * 16 + 8 * (g >> 1);
+#pragma unroll
+    for (int MB = 0; MB < 8; ++MB) {
+      const int row = m0 + wr * 128 + MB * 16 + rl;
+      if (!full && row >= p.m) continue;   // rows g and g^1 share `row`: the swap partners skip together
+      uint32_t o2[4][2], h2[4][2];
+#pragma unroll
+      for (int NB = 0; NB < 4; ++NB) {
+        const int col = n0 + wc * 64 + NB * 16 + cl;
+        const bool cok = full || col < p.n;   // n % 8 == 0: a lane's 4 columns are all in or all out
+        f32x4 v = acc[MB][NB];
+        if (EPI & MTTS_GEMM_EPI_BIAS) {
+          float bb[4] = {0.f, 0.f, 0.f, 0.f};
+          if (cok) {
+            if (p.bias_bf16) {
+              const uint2 raw = *(const uint2*)((const bf16_t*)p.bias + col);
+              bb[0] = __uint_as_float(raw.x << 16); bb[1] = __uint_as_float(raw.x & 0xffff0000u);
+              bb[2] = __uint_as_float(raw.y << 16); bb[3] = __uint_as_float(raw.y & 0xffff0000u);
+            } else {
+              const f32x4 b4 = *(const f32x4*)((const float*)p.bias + col);
+              bb[0] = b4[0]; bb[1] = b4[1]; bb[2] = b4[2]; bb[3] = b4[3];
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += bb[j];
+        }
+        bf16_t o[4];
+        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
+          bf16_t hpre[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hpre[j] = f2bf(v[j]);
+            o[j] = f2bf(gelu_f(bf2f(hpre[j])));
+          }
+          h2[NB][0] = hpre[0] | ((uint32_t)hpre[1] << 16);
+          h2[NB][1] = hpre[2] | ((uint32_t)hpre[3] << 16);
+        } else if constexpr ((EPI & MTTS_GEMM_EPI_DGELU) != 0) {
+          uint2 raw = make_uint2(0, 0);
+          if (cok) raw = *(const uint2*)((const bf16_t*)p.aux + (int64_t)row * p.ld_aux + col);
+          const float h[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
+                              __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(h[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+        }
+        o2[NB][0] = o[0] | ((uint32_t)o[1] << 16);
+        o2[NB][1] = o[2] | ((uint32_t)o[3] << 16);
+      }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto r = __builtin_amdgcn_permlane16_swap(o2[2 * pr][d], o2[2 * pr + 1][d], false, false);
+          w[d] = r[0];
+          w[2 + d] = r[1];
+        }
+        const int cw = cw0 + pr * 32;
+        if (full || cw < p.n) {
+          *(uint4*)((bf16_t*)p.c + (int64_t)row * p.ldc + cw) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto r = __builtin_amdgcn_permlane16_swap(h2[2 * pr][d], h2[2 * pr + 1][d], false, false);
+            w[d] = r[0];
+            w[2 + d] = r[1];
+          }
+          if (full || cw < p.n)
+            *(uint4*)((bf16_t*)p.aux + (int64_t)row * p.ld_aux + cw) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+    }
+    return;
+   }
+  }
+#pragma unroll
+  for (int MB = 0; MB < 8; ++MB) {
+    const int row = m0 + wr * 128 + MB * 16 + rl;
+    if (!full && row >= p.m) continue;
+#pragma unroll
+    for (int NB = 0; NB < 4; ++NB) {
+      const int col = n0 + wc * 64 + NB * 16 + cl;
+      if (!full && col >= p.n) continue;   // n % 8 == 0: a lane's 4 columns are all in or all out
+      f32x4 v = acc[MB][NB];
+      if constexpr (OUT_F32) {
+        float* cp = (float*)p.c + (int64_t)split * p.split_stride + (int64_t)row * p.ldc + col;
+        if (p.beta != 0.f) {
+          const f32x4 o = *(const f32x4*)cp;
+          v = v + p.beta * o;
+        }
+        *(f32x4*)cp = v;
+      } else {
+        if (EPI & MTTS_GEMM_EPI_BIAS) {
+          float bb[4];
+          if (p.bias_bf16) {
+            const uint2 raw = *(const uint2*)((const bf16_t*)p.bias + col);
+            bb[0] = __uint_as_float(raw.x << 16); bb[1] = __uint_as_float(raw.x & 0xffff0000u);
+            bb[2] = __uint_as_float(raw.y << 16); bb[3] = __uint_as_float(raw.y & 0xffff0000u);
+          } else {
+            const f32x4 b4 = *(const f32x4*)((const float*)p.bias + col);
+            bb[0] = b4[0]; bb[1] = b4[1]; bb[2] = b4[2]; bb[3] = b4[3];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += bb[j];
+        }
+        bf16_t o[4];
+        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
+          bf16_t hpre[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hpre[j] = f2bf(v[j]);
+            o[j] = f2bf(gelu_f(bf2f(hpre[j])));
+          }
+          bf16_t* ap = (bf16_t*)p.aux + (int64_t)row * p.ld_aux + col;
+          *(uint2*)ap = make_uint2(hpre[0] | ((uint32_t)hpre[1] << 16), hpre[2] | ((uint32_t)hpre[3] << 16));
+        } else if constexpr ((EPI & MTTS_GEMM_EPI_DGELU) != 0) {
+          const bf16_t* ap = (const bf16_t*)p.aux + (int64_t)row * p.ld_aux + col;
+          const uint2 raw = *(const uint2*)ap;
+          const float h[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
+                              __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(h[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+        }
+        bf16_t* cp = (bf16_t*)p.c + (int64_t)row * p.ldc + col;
+        *(uint2*)cp = make_uint2(o[0] | ((uint32_t)o[1] << 16), o[2] | ((uint32_t)o[3] << 16));
+      }
+    }
+  }
+}
+
 template <bool AK, bool BKM, int EPI, bool OUT_F32>
 __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char lds[kLds];
@@ -395,153 +550,164 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
   for (int t = 0; t < nsteady; ++t) ktile(t, std::true_type{});
   for (int t = nsteady; t < nk; ++t) ktile(t, std::false_type{});
 
-  // ---- epilogue: lane holds rows m = .. + (lane&15), columns n = .. + 4*(lane>>4) + j
-  const int rl = lane & 15, cl = 4 * (lane >> 4);
-  // wave-uniform: the wave's whole 128x64 sub-tile in bounds (no per-lane masks)
-  const bool full = m0 + wr * 128 + 128 <= p.m && n0 + wc * 64 + 64 <= p.n;
-  if constexpr (!OUT_F32) {
-   if (p.wide_out) {
-    // bf16 out: the 16-lane rows g and g^1 of the wave hold adjacent 4-column
-    // groups of the same output rows; one v_permlane16_swap per dword of a
-    // (NB, NB+1) pair gives each lane 8 consecutive columns, so the tile
-    // leaves as 16 dwordx4 stores per lane instead of 32 dwordx2 (the store
-    // tail is issue-bound: cdna_hip_programming.md T21).  After the swap the
-    // even rows hold block 2pr columns 8(g>>1)..+7, the odd rows block 2pr+1.
-    const int g = lane >> 4;
-    const int cw0 = n0 + wc * 64 + (g & 1) * 16 + 8 * (g >> 1);
-#pragma unroll
-    for (int MB = 0; MB < 8; ++MB) {
-      const int row = m0 + wr * 128 + MB * 16 + rl;
-      if (!full && row >= p.m) continue;   // rows g and g^1 share `row`: the swap partners skip together
-      uint32_t o2[4][2], h2[4][2];
-#pragma unroll
-      for (int NB = 0; NB < 4; ++NB) {
-        const int col = n0 + wc * 64 + NB * 16 + cl;
-        const bool cok = full || col < p.n;   // n % 8 == 0: a lane's 4 columns are all in or all out
-        f32x4 v = acc[MB][NB];
-        if (EPI & MTTS_GEMM_EPI_BIAS) {
-          float bb[4] = {0.f, 0.f, 0.f, 0.f};
-          if (cok) {
-            if (p.bias_bf16) {
-              const uint2 raw = *(const uint2*)((const bf16_t*)p.bias + col);
-              bb[0] = __uint_as_float(raw.x << 16); bb[1] = __uint_as_float(raw.x & 0xffff0000u);
-              bb[2] = __uint_as_float(raw.y << 16); bb[3] = __uint_as_float(raw.y & 0xffff0000u);
-            } else {
-              const f32x4 b4 = *(const f32x4*)((const float*)p.bias + col);
-              bb[0] = b4[0]; bb[1] = b4[1]; bb[2] = b4[2]; bb[3] = b4[3];
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += bb[j];
-        }
-        bf16_t o[4];
-        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
-          bf16_t hpre[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            hpre[j] = f2bf(v[j]);
-            o[j] = f2bf(gelu_f(bf2f(hpre[j])));
-          }
-          h2[NB][0] = hpre[0] | ((uint32_t)hpre[1] << 16);
-          h2[NB][1] = hpre[2] | ((uint32_t)hpre[3] << 16);
-        } else if constexpr ((EPI & MTTS_GEMM_EPI_DGELU) != 0) {
-          uint2 raw = make_uint2(0, 0);
-          if (cok) raw = *(const uint2*)((const bf16_t*)p.aux + (int64_t)row * p.ld_aux + col);
-          const float h[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
-                              __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(h[j]));
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
-        }
-        o2[NB][0] = o[0] | ((uint32_t)o[1] << 16);
-        o2[NB][1] = o[2] | ((uint32_t)o[3] << 16);
-      }
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        uint32_t w[4];
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const auto r = __builtin_amdgcn_permlane16_swap(o2[2 * pr][d], o2[2 * pr + 1][d], false, false);
-          w[d] = r[0];
-          w[2 + d] = r[1];
-        }
-        const int cw = cw0 + pr * 32;
-        if (full || cw < p.n) {
-          *(uint4*)((bf16_t*)p.c + (int64_t)row * p.ldc + cw) = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            const auto r = __builtin_amdgcn_permlane16_swap(h2[2 * pr][d], h2[2 * pr + 1][d], false, false);
-            w[d] = r[0];
-            w[2 + d] = r[1];
-          }
-          if (full || cw < p.n)
-            *(uint4*)((bf16_t*)p.aux + (int64_t)row * p.ld_aux + cw) = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-      }
-    }
-    return;
-   }
+  store_tile<EPI, OUT_F32>(p, acc, m0, n0, wr, wc, lane, split);
+}
+
+// ---------------------------------------------------------------------------
+// Ping-pong form (default): the same 256x256 tile, regions, loaders, fragment
+// reads and epilogue, scheduled as two wave GROUPS (wr = 0: waves 0-3, wr = 1:
+// waves 4-7; a workgroup's 8 waves land two per SIMD, one of each group) that
+// run one barrier apart.  A phase of a wave is a READ segment (its fragment
+// ds_reads for this phase + the phase's 2 LDS-DMAs + a counted vmcnt) and an
+// MFMA segment (lgkmcnt(0), 16 MFMAs at s_setprio 1), each closed by a barrier;
+// with the offset, every barrier interval pairs one group's MFMA segment
+// with the other group's read segment on each SIMD, so the matrix pipe is fed
+// while the partner issues its LDS reads and DMAs (MI355X_MICROARCH.md "Two
+// waves per SIMD"; cdna_hip_programming.md §5 "256² 8-phase template").
+//
+// Fragment reads per phase (quadrants as gemm_kernel): q0 A0 + B0, q1 B1,
+// q2 A1, q3 none (A1 and B0 stay in registers).  A region can be restaged two
+// phases after its last read (the partner group retires its reads one barrier
+// later); staging per phase of K-tile t:  q0 A1(t+1), q1 B1(t+1), q2 A0(t+2),
+// q3 B0(t+2), read 6 / 4 / 6 / 5 phases later.  Each read segment ends with the
+// wait for the NEXT phase's regions (counted in DMA regions issued after the
+// needed one: q0 -> B1(t): 3, q1 -> A1(t): 5, q3 -> A0/B0(t+1): 4, fewer in
+// the last K-tiles), and the barrier after it orders every wave's wait before
+// any read.
+template <int N>
+__device__ __forceinline__ void wait_regions() { wait_vm<2 * N>(); }
+__device__ __forceinline__ void wait_regions_rt(int n) {
+  switch (n) {
+    case 0: wait_regions<0>(); break;
+    case 1: wait_regions<1>(); break;
+    case 2: wait_regions<2>(); break;
+    case 3: wait_regions<3>(); break;
+    case 4: wait_regions<4>(); break;
+    default: wait_regions<5>(); break;
   }
-#pragma unroll
-  for (int MB = 0; MB < 8; ++MB) {
-    const int row = m0 + wr * 128 + MB * 16 + rl;
-    if (!full && row >= p.m) continue;
-#pragma unroll
-    for (int NB = 0; NB < 4; ++NB) {
-      const int col = n0 + wc * 64 + NB * 16 + cl;
-      if (!full && col >= p.n) continue;   // n % 8 == 0: a lane's 4 columns are all in or all out
-      f32x4 v = acc[MB][NB];
-      if constexpr (OUT_F32) {
-        float* cp = (float*)p.c + (int64_t)split * p.split_stride + (int64_t)row * p.ldc + col;
-        if (p.beta != 0.f) {
-          const f32x4 o = *(const f32x4*)cp;
-          v = v + p.beta * o;
-        }
-        *(f32x4*)cp = v;
-      } else {
-        if (EPI & MTTS_GEMM_EPI_BIAS) {
-          float bb[4];
-          if (p.bias_bf16) {
-            const uint2 raw = *(const uint2*)((const bf16_t*)p.bias + col);
-            bb[0] = __uint_as_float(raw.x << 16); bb[1] = __uint_as_float(raw.x & 0xffff0000u);
-            bb[2] = __uint_as_float(raw.y << 16); bb[3] = __uint_as_float(raw.y & 0xffff0000u);
-          } else {
-            const f32x4 b4 = *(const f32x4*)((const float*)p.bias + col);
-            bb[0] = b4[0]; bb[1] = b4[1]; bb[2] = b4[2]; bb[3] = b4[3];
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += bb[j];
-        }
-        bf16_t o[4];
-        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
-          bf16_t hpre[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            hpre[j] = f2bf(v[j]);
-            o[j] = f2bf(gelu_f(bf2f(hpre[j])));
-          }
-          bf16_t* ap = (bf16_t*)p.aux + (int64_t)row * p.ld_aux + col;
-          *(uint2*)ap = make_uint2(hpre[0] | ((uint32_t)hpre[1] << 16), hpre[2] | ((uint32_t)hpre[3] << 16));
-        } else if constexpr ((EPI & MTTS_GEMM_EPI_DGELU) != 0) {
-          const bf16_t* ap = (const bf16_t*)p.aux + (int64_t)row * p.ld_aux + col;
-          const uint2 raw = *(const uint2*)ap;
-          const float h[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
-                              __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(h[j]));
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
-        }
-        bf16_t* cp = (bf16_t*)p.c + (int64_t)row * p.ldc + col;
-        *(uint2*)cp = make_uint2(o[0] | ((uint32_t)o[1] << 16), o[2] | ((uint32_t)o[3] << 16));
-      }
+}
+__device__ __forceinline__ void sbar() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#endif
+}
+
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int split = id / tiles;
+  const int tile = id % tiles;
+  const int gsz = p.group * p.tiles_n;
+  const int g0 = (tile / gsz) * p.group;
+  const int gr = min(p.group, p.tiles_m - g0);
+  const int tm = g0 + (tile % gsz) % gr, tn = (tile % gsz) / gr;
+  const int m0 = tm * kTile, n0 = tn * kTile;
+
+  const int64_t k0 = (int64_t)split * p.k;
+  const char* abase;
+  const char* bbase;
+  int64_t astep, bstep;
+  if constexpr (AK) { abase = (const char*)(p.a + k0); astep = kBK * 2; }
+  else { abase = (const char*)(p.a + k0 * p.lda); astep = kBK * p.lda * 2; }
+  if constexpr (BKM) { bbase = (const char*)(p.b + k0); bstep = kBK * 2; }
+  else { bbase = (const char*)(p.b + k0 * p.ldb); bstep = kBK * p.ldb * 2; }
+
+  Loader<AK, true> la;
+  Loader<BKM, false> lb;
+  la.init(tid, m0, p.m, p.lda);
+  lb.init(tid, n0, p.n, p.ldb);
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  auto stage = [&](int kt, int r) {
+    const uint32_t reg = lds0 + (kt & 1) * kBuf + r * kRegion;
+    if (r == R_A0 || r == R_A1) {
+      la.stage1(abase + kt * astep, r - R_A0, reg, wave, 0);
+      la.stage1(abase + kt * astep, r - R_A0, reg, wave, 1);
+    } else {
+      lb.stage1(bbase + kt * bstep, r - R_B0, reg, wave, 0);
+      lb.stage1(bbase + kt * bstep, r - R_B0, reg, wave, 1);
     }
+  };
+
+  const int nk = p.k / kBK;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: all of K-tile 0, A0 / B0 of K-tile 1 (A1 / B1 of K-tile 1 are
+  // staged by K-tile 0's phases 0 / 1)
+  stage(0, R_A0); stage(0, R_B0); stage(0, R_B1); stage(0, R_A1);
+  if (nk > 1) { stage(1, R_A0); stage(1, R_B0); }
+  if (nk > 1) wait_regions<4>(); else wait_regions<2>();   // A0(0), B0(0) landed
+  sbar();
+  if (wr == 1) sbar();   // group 1 runs one barrier behind
+
+  const char* lbase = lds;
+  s16x8 af[2][4], b0f[2][2], b1f[2][2];   // [ks][block]
+#define PP_MFMA(BF, MO, NO)                                                                   \
+  __builtin_amdgcn_sched_barrier(0);                                                        \
+  __builtin_amdgcn_s_waitcnt(0xC07F);                                                        \
+  __builtin_amdgcn_sched_barrier(0);                                                        \
+  __builtin_amdgcn_s_setprio(1);                                                            \
+  _Pragma("unroll") for (int ks_ = 0; ks_ < 2; ++ks_)                                        \
+  _Pragma("unroll") for (int mb_ = 0; mb_ < 4; ++mb_)                                        \
+  _Pragma("unroll") for (int nb_ = 0; nb_ < 2; ++nb_)                                        \
+      acc[(MO) + mb_][(NO) + nb_] = mfma(BF[ks_][nb_], af[ks_][mb_], acc[(MO) + mb_][(NO) + nb_]); \
+  __builtin_amdgcn_s_setprio(0);                                                            \
+  __builtin_amdgcn_sched_barrier(0);                                                        \
+  sbar();
+  for (int t = 0; t < nk; ++t) {
+    const char* bufp = lbase + (t & 1) * kBuf;
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    // ---- q0: A0 x B0 | stage A1(t+1) | wait B1(t)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b0f[ks][nb] = frag<BKM>(bufp + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
+    }
+    if (n1) stage(t + 1, R_A1);
+    if (t == 0) wait_regions_rt(n1 ? 4 : 1); else wait_regions_rt(n1 ? 3 : 0);
+    sbar();
+    PP_MFMA(b0f, 0, 0)
+    // ---- q1: A0 x B1 | stage B1(t+1) | wait A1(t)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b1f[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
+    if (n1) stage(t + 1, R_B1);
+    if (t == 0) wait_regions_rt(n1 ? 4 : 0); else wait_regions_rt(n1 ? 5 : 1);
+    sbar();
+    PP_MFMA(b1f, 0, 2)
+    // ---- q2: A1 x B1 | stage A0(t+2)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A1 * kRegion, wr * 64 + mb * 16, ks, lane);
+    if (n2) stage(t + 2, R_A0);
+    sbar();
+    PP_MFMA(b1f, 4, 2)
+    // ---- q3: A1 x B0 | stage B0(t+2) | wait A0 / B0(t+1)
+    if (n2) stage(t + 2, R_B0);
+    if (n1) wait_regions_rt(n2 ? 4 : 2);
+    sbar();
+    PP_MFMA(b0f, 4, 0)
   }
+#undef PP_MFMA
+  if (wr == 0) sbar();   // the same barrier count for both groups
+  store_tile<EPI, OUT_F32>(p, acc, m0, n0, wr, wc, lane, split);
 }
 
 // out[i] = beta*out[i] + sum_s slab[s][i] (fixed order); rows x cols with row strides
@@ -560,9 +726,14 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restri
   }
 }
 
+static bool use_pp() {   // MTTS_GEMM_PP=0: the round-2 single-group kernel (read per launch: in-process A/B)
+  const char* e = getenv("MTTS_GEMM_PP");
+  return !e || atoi(e) != 0;
+}
 template <bool AK, bool BKM, int EPI, bool F32>
 void launch(const GemmParams& p, int nwg, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
+  if (use_pp()) hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
+  else hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
 }
 
 }  // namespace
