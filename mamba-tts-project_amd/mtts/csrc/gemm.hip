@@ -554,36 +554,55 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// Ping-pong form (default): the same 256x256 tile, regions, loaders, fragment
-// reads and epilogue, scheduled as two wave GROUPS (wr = 0: waves 0-3, wr = 1:
-// waves 4-7; a workgroup's 8 waves land two per SIMD, one of each group) that
-// run one barrier apart.  A phase of a wave is a READ segment (its fragment
-// ds_reads for this phase + the phase's 2 LDS-DMAs + a counted vmcnt) and an
-// MFMA segment (lgkmcnt(0), 16 MFMAs at s_setprio 1), each closed by a barrier;
-// with the offset, every barrier interval pairs one group's MFMA segment
-// with the other group's read segment on each SIMD, so the matrix pipe is fed
-// while the partner issues its LDS reads and DMAs (MI355X_MICROARCH.md "Two
-// waves per SIMD"; cdna_hip_programming.md §5 "256² 8-phase template").
+// Ping-pong persistent form (default): the same 256x256 tile, regions,
+// loaders, fragment reads and epilogue math, scheduled as two wave GROUPS
+// (wr = 0: waves 0-3, wr = 1: waves 4-7; a workgroup's 8 waves land two per
+// SIMD, one of each group) that run one barrier apart.  A phase of a wave is a
+// READ segment (its fragment ds_reads for this phase + the phase's 2 LDS-DMAs
+// + a counted vmcnt) and an MFMA segment (lgkmcnt(0), 16 MFMAs at
+// s_setprio 1), each closed by a barrier; with the offset, every barrier
+// interval pairs one group's MFMA segment with the other group's read segment
+// on each SIMD, so the matrix pipe is fed while the partner issues its LDS
+// reads and DMAs (MI355X_MICROARCH.md "Two waves per SIMD"; cdna_hip_
+// programming.md §5 "256² 8-phase template").
 //
 // Fragment reads per phase (quadrants as gemm_kernel): q0 A0 + B0, q1 B1,
 // q2 A1, q3 none (A1 and B0 stay in registers).  A region can be restaged two
 // phases after its last read (the partner group retires its reads one barrier
-// later); staging per phase of K-tile t:  q0 A1(t+1), q1 B1(t+1), q2 A0(t+2),
-// q3 B0(t+2), read 6 / 4 / 6 / 5 phases later.  Each read segment ends with the
-// wait for the NEXT phase's regions (counted in DMA regions issued after the
-// needed one: q0 -> B1(t): 3, q1 -> A1(t): 5, q3 -> A0/B0(t+1): 4, fewer in
-// the last K-tiles), and the barrier after it orders every wave's wait before
-// any read.
+// later); staging per phase of K-tile g:  q0 A1(g+1), q1 B1(g+1), q2 A0(g+2),
+// q3 B0(g+2), read 6 / 4 / 6 / 5 phases later.  Each read segment ends with the
+// wait for the NEXT phase's regions, counted in VMEM operations issued after
+// the needed one (q0 -> B1(g): 6, q1 -> A1(g): 10, q3 -> A0/B0(g+1): 8, fewer
+// at the end of the stream), and the barrier after it orders every wave's
+// wait before any read.
+//
+// PERSISTENT: a workgroup runs tiles (work items) wid, wid + grid, ... and g
+// counts K-tiles over all of them, so the staging above simply continues into
+// the next tile (its first regions land while the current tile finishes: no
+// per-tile prologue) and the tile's epilogue runs inside the next tile's
+// first read segment, beside the partner group's last MFMA segment, its
+// stores overlapping the next tile's main loop.  Every epilogue memory
+// operation is a single-instruction buffer load / store (out-of-range rows and
+// columns are dropped by the buffer's range check, not by branches), so the
+// number of VMEM operations an epilogue adds to the first K-tile's waits is
+// a compile-time constant (kEpiOps).
 template <int N>
-__device__ __forceinline__ void wait_regions() { wait_vm<2 * N>(); }
-__device__ __forceinline__ void wait_regions_rt(int n) {
+__device__ __forceinline__ void wait_ops() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  wait_vm<N>();
+}
+template <int BASE>
+__device__ __forceinline__ void wait_ops_rt(int n) {   // vmcnt(n), n in [0, 63]; BASE: the common value
+  if (n == BASE) { wait_ops<BASE>(); return; }
   switch (n) {
-    case 0: wait_regions<0>(); break;
-    case 1: wait_regions<1>(); break;
-    case 2: wait_regions<2>(); break;
-    case 3: wait_regions<3>(); break;
-    case 4: wait_regions<4>(); break;
-    default: wait_regions<5>(); break;
+#define W_(k) case k: wait_ops<k>(); break;
+    W_(0) W_(1) W_(2) W_(3) W_(4) W_(5) W_(6) W_(7) W_(8) W_(9) W_(10) W_(11) W_(12) W_(13) W_(14) W_(15)
+    W_(16) W_(17) W_(18) W_(19) W_(20) W_(21) W_(22) W_(23) W_(24) W_(25) W_(26) W_(27) W_(28) W_(29) W_(30)
+    W_(31) W_(32) W_(33) W_(34) W_(35) W_(36) W_(37) W_(38) W_(39) W_(40) W_(41) W_(42) W_(43) W_(44) W_(45)
+    W_(46) W_(47) W_(48) W_(49) W_(50) W_(51) W_(52) W_(53) W_(54) W_(55) W_(56) W_(57) W_(58) W_(59) W_(60)
+    W_(61) W_(62)
+#undef W_
+    default: wait_ops<0>(); break;
   }
 }
 __device__ __forceinline__ void sbar() {
@@ -593,16 +612,141 @@ __device__ __forceinline__ void sbar() {
 #endif
 }
 
-template <bool AK, bool BKM, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char lds[kLds];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kOOB = 0xFFFFFFF0u;   // a buffer offset past every range: the access is dropped / reads 0
 
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// VMEM operations of one tile's epilogue (stores + loads), and the bias loads
+// made at a tile's start: exact instruction counts of store_tile_buf / load_bias
+template <int EPI, bool OUT_F32>
+struct EpiOps {
+  static constexpr int bias = (EPI & MTTS_GEMM_EPI_BIAS) ? 4 : 0;
+  static constexpr int epi = OUT_F32 ? 32 : 16 + ((EPI & MTTS_GEMM_EPI_GELU) ? 16 : 0) +
+                                             ((EPI & MTTS_GEMM_EPI_DGELU) ? 32 : 0);
+};
+
+template <int EPI>
+__device__ __forceinline__ void load_bias(const GemmParams& p, int n0, int wc, int lane, f32x4 (&bias)[4]) {
+  if constexpr ((EPI & MTTS_GEMM_EPI_BIAS) != 0) {
+    const int cl = 4 * (lane >> 4);
+    const int es = p.bias_bf16 ? 2 : 4;
+    const __amdgpu_buffer_rsrc_t r = brsrc(p.bias, (uint32_t)p.n * es);
+#pragma unroll
+    for (int NB = 0; NB < 4; ++NB) {
+      const int col = n0 + wc * 64 + NB * 16 + cl;
+      const uint32_t off = col < p.n ? (uint32_t)col * es : kOOB;
+      if (p.bias_bf16) {
+        const i32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        bias[NB] = f32x4{__uint_as_float((uint32_t)raw.x << 16), __uint_as_float((uint32_t)raw.x & 0xffff0000u),
+                         __uint_as_float((uint32_t)raw.y << 16), __uint_as_float((uint32_t)raw.y & 0xffff0000u)};
+      } else {
+        bias[NB] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+      }
+    }
+  }
+}
+
+// store_tile with buffer stores (beta == 0 for fp32 out): exactly EpiOps::epi
+// VMEM instructions whatever the bounds
+template <int EPI, bool OUT_F32>
+__device__ __forceinline__ void store_tile_buf(const GemmParams& p, f32x4 (&acc)[8][4], const f32x4 (&bias)[4],
+                                               int m0, int n0, int wr, int wc, int lane, int split) {
+  const int rl = lane & 15, cl = 4 * (lane >> 4);
+  if constexpr (OUT_F32) {
+    const __amdgpu_buffer_rsrc_t r = brsrc((const float*)p.c + (int64_t)split * p.split_stride,
+                                           (uint32_t)((int64_t)p.m * p.ldc * 4));
+#pragma unroll
+    for (int MB = 0; MB < 8; ++MB) {
+      const int row = m0 + wr * 128 + MB * 16 + rl;
+#pragma unroll
+      for (int NB = 0; NB < 4; ++NB) {
+        const int col = n0 + wc * 64 + NB * 16 + cl;
+        const uint32_t off = (row < p.m && col < p.n) ? (uint32_t)((row * p.ldc + col) * 4) : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[MB][NB]), r, off, 0, 0);
+      }
+    }
+  } else {
+    const int g = lane >> 4;
+    const int cw0 = n0 + wc * 64 + (g & 1) * 16 + 8 * (g >> 1);
+    const __amdgpu_buffer_rsrc_t rc = brsrc(p.c, (uint32_t)((int64_t)p.m * p.ldc * 2));
+    const __amdgpu_buffer_rsrc_t ra = brsrc(p.aux, (uint32_t)((int64_t)p.m * p.ld_aux * 2));
+#pragma unroll
+    for (int MB = 0; MB < 8; ++MB) {
+      const int row = m0 + wr * 128 + MB * 16 + rl;
+      const bool rok = row < p.m;
+      uint32_t o2[4][2], h2[4][2];
+      i32x2 auxv[4];
+      if constexpr ((EPI & MTTS_GEMM_EPI_DGELU) != 0) {
+#pragma unroll
+        for (int NB = 0; NB < 4; ++NB) {
+          const int col = n0 + wc * 64 + NB * 16 + cl;
+          const uint32_t off = (rok && col < p.n) ? (uint32_t)((row * p.ld_aux + col) * 2) : kOOB;
+          auxv[NB] = __builtin_amdgcn_raw_buffer_load_b64(ra, off, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int NB = 0; NB < 4; ++NB) {
+        f32x4 v = acc[MB][NB];
+        if constexpr ((EPI & MTTS_GEMM_EPI_BIAS) != 0) v += bias[NB];
+        bf16_t o[4];
+        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
+          bf16_t hpre[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hpre[j] = f2bf(v[j]);
+            o[j] = f2bf(gelu_f(bf2f(hpre[j])));
+          }
+          h2[NB][0] = hpre[0] | ((uint32_t)hpre[1] << 16);
+          h2[NB][1] = hpre[2] | ((uint32_t)hpre[3] << 16);
+        } else if constexpr ((EPI & MTTS_GEMM_EPI_DGELU) != 0) {
+          const uint32_t x = (uint32_t)auxv[NB].x, y = (uint32_t)auxv[NB].y;
+          const float h[4] = {__uint_as_float(x << 16), __uint_as_float(x & 0xffff0000u), __uint_as_float(y << 16),
+                              __uint_as_float(y & 0xffff0000u)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(h[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+        }
+        o2[NB][0] = o[0] | ((uint32_t)o[1] << 16);
+        o2[NB][1] = o[2] | ((uint32_t)o[3] << 16);
+      }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto r = __builtin_amdgcn_permlane16_swap(o2[2 * pr][d], o2[2 * pr + 1][d], false, false);
+          w[d] = r[0];
+          w[2 + d] = r[1];
+        }
+        const int cw = cw0 + pr * 32;
+        const bool ok = rok && cw < p.n;   // n % 8 == 0: a lane's 8 columns are all in or all out
+        __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)w[0], (int)w[1], (int)w[2], (int)w[3]}, rc,
+                                               ok ? (uint32_t)((row * p.ldc + cw) * 2) : kOOB, 0, 0);
+        if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto r = __builtin_amdgcn_permlane16_swap(h2[2 * pr][d], h2[2 * pr + 1][d], false, false);
+            w[d] = r[0];
+            w[2 + d] = r[1];
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)w[0], (int)w[1], (int)w[2], (int)w[3]}, ra,
+                                                 ok ? (uint32_t)((row * p.ld_aux + cw) * 2) : kOOB, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+struct WorkItem {
+  int m0, n0, split;
+};
+__device__ __forceinline__ WorkItem work_item(const GemmParams& p, int id) {
   const int tiles = p.tiles_m * p.tiles_n;
   const int split = id / tiles;
   const int tile = id % tiles;
@@ -610,46 +754,108 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   const int g0 = (tile / gsz) * p.group;
   const int gr = min(p.group, p.tiles_m - g0);
   const int tm = g0 + (tile % gsz) % gr, tn = (tile % gsz) / gr;
-  const int m0 = tm * kTile, n0 = tn * kTile;
+  return WorkItem{tm * kTile, tn * kTile, split};
+}
 
-  const int64_t k0 = (int64_t)split * p.k;
-  const char* abase;
-  const char* bbase;
-  int64_t astep, bstep;
-  if constexpr (AK) { abase = (const char*)(p.a + k0); astep = kBK * 2; }
-  else { abase = (const char*)(p.a + k0 * p.lda); astep = kBK * p.lda * 2; }
-  if constexpr (BKM) { bbase = (const char*)(p.b + k0); bstep = kBK * 2; }
-  else { bbase = (const char*)(p.b + k0 * p.ldb); bstep = kBK * p.ldb * 2; }
-
-  Loader<AK, true> la;
-  Loader<BKM, false> lb;
-  la.init(tid, m0, p.m, p.lda);
-  lb.init(tid, n0, p.n, p.ldb);
-
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
-  auto stage = [&](int kt, int r) {
-    const uint32_t reg = lds0 + (kt & 1) * kBuf + r * kRegion;
-    if (r == R_A0 || r == R_A1) {
-      la.stage1(abase + kt * astep, r - R_A0, reg, wave, 0);
-      la.stage1(abase + kt * astep, r - R_A0, reg, wave, 1);
+// per-thread LDS-DMA source offsets of one operand, recomputed per tile from
+// the tile origin (row0) and kept relative to the K-tile origin pointer
+template <bool KMAJ, bool IS_A>
+struct PLoader {
+  uint32_t fixed[2];   // [dma i]: k-major: chunk byte offset; m/n-major: k-row byte offset
+  int rm[2][2];        // [sub s][dma i]: region-local row / column -> tile row / column
+  __device__ void init(int tid, int64_t ld) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (KMAJ) {
+        const int rr = i * 64 + (tid >> 3), pp = tid & 7;
+        fixed[i] = (uint32_t)(((pp ^ ((rr >> 1) & 7)) * 8) * 2);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) rm[s][i] = rmap<IS_A>(rr, s);
+      } else {
+        const int kr = i * 32 + (tid >> 4), pp = tid & 15;
+        const int f = (kr & 3) | (((kr >> 3) & 1) << 2);
+        const int c = pp ^ (f << 1);
+        fixed[i] = (uint32_t)(kr * ld * 2);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) rm[s][i] = rmap<IS_A>(c * 8, s);
+      }
+    }
+  }
+  __device__ __forceinline__ uint32_t off(int row0, int nrows, int64_t ld, int s, int i) const {
+    if constexpr (KMAJ) {
+      int row = row0 + rm[s][i];
+      row = row < nrows ? row : nrows - 1;
+      return (uint32_t)(row * ld * 2) + fixed[i];
     } else {
-      lb.stage1(bbase + kt * bstep, r - R_B0, reg, wave, 0);
-      lb.stage1(bbase + kt * bstep, r - R_B0, reg, wave, 1);
+      int col = row0 + rm[s][i];
+      col = col + 8 <= nrows ? col : ((nrows - 8) & ~7);
+      return fixed[i] + (uint32_t)col * 2;
+    }
+  }
+};
+
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // XCD-aware work order: the ids one XCD holds at a time are consecutive
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int total = p.tiles_m * p.tiles_n * p.splits;
+  const int nitems = (total - wid + nwg - 1) / nwg;   // items wid, wid + nwg, ...
+  const int nk = p.k / kBK;
+  const int G = nitems * nk;                           // K-tiles of the whole stream
+
+  PLoader<AK, true> la;
+  PLoader<BKM, false> lb;
+  la.init(tid, p.lda);
+  lb.init(tid, p.ldb);
+  const int64_t astep = AK ? kBK * 2 : kBK * p.lda * 2;   // bytes per K-tile
+  const int64_t bstep = BKM ? kBK * 2 : kBK * p.ldb * 2;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+
+  // items of the current and the next tile (the stream stages up to two
+  // K-tiles ahead, which may belong to the next tile)
+  WorkItem cur = work_item(p, wid), nxt = cur;
+  if (nitems > 1) nxt = work_item(p, wid + nwg);
+  auto stage = [&](int g, int r, int icur) {
+    const bool next = g >= (icur + 1) * nk;
+    const WorkItem& it = next ? nxt : cur;
+    const int kt = g - (next ? icur + 1 : icur) * nk;
+    const uint32_t reg = lds0 + (g & 1) * kBuf + r * kRegion;
+    const int64_t k0 = (int64_t)it.split * p.k;
+    if (r == R_A0 || r == R_A1) {
+      const char* base = (const char*)(AK ? p.a + k0 : p.a + k0 * p.lda) + kt * astep;
+      const int s = r - R_A0;
+      glds16(base, la.off(it.m0, p.m, p.lda, s, 0), reg + wave * 1024);
+      glds16(base, la.off(it.m0, p.m, p.lda, s, 1), reg + 8192 + wave * 1024);
+    } else {
+      const char* base = (const char*)(BKM ? p.b + k0 : p.b + k0 * p.ldb) + kt * bstep;
+      const int s = r - R_B0;
+      glds16(base, lb.off(it.n0, p.n, p.ldb, s, 0), reg + wave * 1024);
+      glds16(base, lb.off(it.n0, p.n, p.ldb, s, 1), reg + 8192 + wave * 1024);
     }
   };
 
-  const int nk = p.k / kBK;
+  constexpr int kBiasOps = EpiOps<EPI, OUT_F32>::bias;
+  constexpr int kEpiOps = EpiOps<EPI, OUT_F32>::epi + kBiasOps;   // a tile boundary's extra VMEM ops
+  f32x4 bias[4] = {};
+  load_bias<EPI>(p, cur.n0, wc, lane, bias);   // older than every DMA: outside the counts
+
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: all of K-tile 0, A0 / B0 of K-tile 1 (A1 / B1 of K-tile 1 are
-  // staged by K-tile 0's phases 0 / 1)
-  stage(0, R_A0); stage(0, R_B0); stage(0, R_B1); stage(0, R_A1);
-  if (nk > 1) { stage(1, R_A0); stage(1, R_B0); }
-  if (nk > 1) wait_regions<4>(); else wait_regions<2>();   // A0(0), B0(0) landed
+  // prologue: all of K-tile 0, A0 / B0 of K-tile 1
+  stage(0, R_A0, 0); stage(0, R_B0, 0); stage(0, R_B1, 0); stage(0, R_A1, 0);
+  if (G > 1) { stage(1, R_A0, 0); stage(1, R_B0, 0); }
+  if (G > 1) wait_ops<8>(); else wait_ops<4>();   // A0(0), B0(0) landed
   sbar();
   if (wr == 1) sbar();   // group 1 runs one barrier behind
 
@@ -667,47 +873,64 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   __builtin_amdgcn_s_setprio(0);                                                            \
   __builtin_amdgcn_sched_barrier(0);                                                        \
   sbar();
-  for (int t = 0; t < nk; ++t) {
-    const char* bufp = lbase + (t & 1) * kBuf;
-    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
-    // ---- q0: A0 x B0 | stage A1(t+1) | wait B1(t)
+  for (int i = 0; i < nitems; ++i) {
+    for (int t = 0; t < nk; ++t) {
+      const int g = i * nk + t;
+      const char* bufp = lbase + (g & 1) * kBuf;
+      const bool n1 = g + 1 < G, n2 = g + 2 < G;
+      // a tile boundary's epilogue ops sit between the regions the first
+      // K-tile's waits need and that wait
+      const int ex = (t == 0 && i > 0) ? kEpiOps : 0;
+      if (t == 0 && i > 0) {
+        // ---- the previous tile's epilogue, then this tile's bias (read segment of q0)
+        store_tile_buf<EPI, OUT_F32>(p, acc, bias, cur.m0, cur.n0, wr, wc, lane, cur.split);
+        cur = nxt;
+        if (i + 1 < nitems) nxt = work_item(p, wid + (i + 1) * nwg);
+        load_bias<EPI>(p, cur.n0, wc, lane, bias);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+        for (int a = 0; a < 8; ++a)
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) b0f[ks][nb] = frag<BKM>(bufp + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
+          for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      // ---- q0: A0 x B0 | stage A1(g+1) | wait B1(g)
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) b0f[ks][nb] = frag<BKM>(bufp + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
+      }
+      if (n1) stage(g + 1, R_A1, i);
+      if (g == 0) wait_ops_rt<8>(n1 ? 8 : 2); else wait_ops_rt<6>((n1 ? 6 : 0) + ex);
+      sbar();
+      PP_MFMA(b0f, 0, 0)
+      // ---- q1: A0 x B1 | stage B1(g+1) | wait A1(g)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) b1f[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
+      if (n1) stage(g + 1, R_B1, i);
+      if (g == 0) wait_ops_rt<8>(n1 ? 8 : 0); else wait_ops_rt<10>((n1 ? 10 : 2) + ex);
+      sbar();
+      PP_MFMA(b1f, 0, 2)
+      // ---- q2: A1 x B1 | stage A0(g+2)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A1 * kRegion, wr * 64 + mb * 16, ks, lane);
+      if (n2) stage(g + 2, R_A0, i);
+      sbar();
+      PP_MFMA(b1f, 4, 2)
+      // ---- q3: A1 x B0 | stage B0(g+2) | wait A0 / B0(g+1)
+      if (n2) stage(g + 2, R_B0, i);
+      if (n1) wait_ops_rt<8>((n2 ? 8 : 4) + ex);
+      sbar();
+      PP_MFMA(b0f, 4, 0)
     }
-    if (n1) stage(t + 1, R_A1);
-    if (t == 0) wait_regions_rt(n1 ? 4 : 1); else wait_regions_rt(n1 ? 3 : 0);
-    sbar();
-    PP_MFMA(b0f, 0, 0)
-    // ---- q1: A0 x B1 | stage B1(t+1) | wait A1(t)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) b1f[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
-    if (n1) stage(t + 1, R_B1);
-    if (t == 0) wait_regions_rt(n1 ? 4 : 0); else wait_regions_rt(n1 ? 5 : 1);
-    sbar();
-    PP_MFMA(b1f, 0, 2)
-    // ---- q2: A1 x B1 | stage A0(t+2)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A1 * kRegion, wr * 64 + mb * 16, ks, lane);
-    if (n2) stage(t + 2, R_A0);
-    sbar();
-    PP_MFMA(b1f, 4, 2)
-    // ---- q3: A1 x B0 | stage B0(t+2) | wait A0 / B0(t+1)
-    if (n2) stage(t + 2, R_B0);
-    if (n1) wait_regions_rt(n2 ? 4 : 2);
-    sbar();
-    PP_MFMA(b0f, 4, 0)
   }
 #undef PP_MFMA
   if (wr == 0) sbar();   // the same barrier count for both groups
-  store_tile<EPI, OUT_F32>(p, acc, m0, n0, wr, wc, lane, split);
+  store_tile_buf<EPI, OUT_F32>(p, acc, bias, cur.m0, cur.n0, wr, wc, lane, cur.split);
 }
 
 // out[i] = beta*out[i] + sum_s slab[s][i] (fixed order); rows x cols with row strides
@@ -726,14 +949,40 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restri
   }
 }
 
-static bool use_pp() {   // MTTS_GEMM_PP=0: the round-2 single-group kernel (read per launch: in-process A/B)
+// MTTS_GEMM_PP: 0 = the round-2 single-group kernel, 1 = ping-pong with one
+// tile per workgroup, 2 (default) = ping-pong persistent (read per launch:
+// in-process A/B)
+static int pp_mode() {
   const char* e = getenv("MTTS_GEMM_PP");
-  return !e || atoi(e) != 0;
+  return e ? atoi(e) : 2;
+}
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
 }
 template <bool AK, bool BKM, int EPI, bool F32>
 void launch(const GemmParams& p, int nwg, hipStream_t st) {
-  if (use_pp()) hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
-  else hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
+  const int mode = pp_mode();
+  // the ping-pong epilogue stores 16-byte bf16 pieces (wide_out) and
+  // addresses C / aux / each slab with 31-bit buffer offsets
+  const int64_t cbytes = F32 ? (int64_t)p.m * p.ldc * 4 : (int64_t)p.m * p.ldc * 2;
+  const int64_t abytes = (EPI & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) ? (int64_t)p.m * p.ld_aux * 2 : 0;
+  const bool pp_ok = (F32 || p.wide_out) && cbytes < (1ll << 31) && abytes < (1ll << 31) &&
+                     (!F32 || p.beta == 0.f || p.splits == 1);
+  if (mode == 0 || !pp_ok) {
+    hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
+    return;
+  }
+  // persistent: one workgroup per CU looping over the work items, when the
+  // stream has >= 2 K-tiles per item and the epilogue needs no C reads
+  int grid = nwg;
+  if (mode >= 2 && p.k / kBK >= 2 && !(F32 && p.beta != 0.f)) grid = std::min(nwg, num_cus());
+  hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32>), dim3(grid), dim3(kThreads), 0, st, p);
 }
 
 }  // namespace

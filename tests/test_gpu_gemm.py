@@ -133,3 +133,56 @@ def test_ffn_fused_matches_per_op_path():
     names = ["y", "dh", "dW1", "db1", "dW2", "db2"]
     for nm, a, b in zip(names, outs[0], outs[1]):
         assert rel(a, b) < 2e-2, nm
+
+
+@pytest.fixture(params=["2", "1", "0"])
+def gemm_mode(request):
+    """MTTS_GEMM_PP: 2 = ping-pong persistent (default), 1 = ping-pong with one
+    tile per workgroup, 0 = the round-2 single-group kernel."""
+    import os
+    old = os.environ.get("MTTS_GEMM_PP")
+    os.environ["MTTS_GEMM_PP"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("MTTS_GEMM_PP", None)
+    else:
+        os.environ["MTTS_GEMM_PP"] = old
+
+
+@pytest.mark.parametrize("m,n,k", [(16384, 4096, 1024), (16484, 4104, 1024), (4096, 2048, 128), (8192, 1024, 2048)])
+def test_nt_every_kernel_many_tiles(gemm_mode, m, n, k):
+    """More work items than CUs (the persistent kernel runs several tiles per
+    workgroup, its K-tile stream crossing tile boundaries), ragged edges in
+    both dimensions, K of 2 K-tiles; plain, bias + GELU and GELU-backward."""
+    torch.manual_seed(m + n + k)
+    a, b = rnd(m, k), rnd(n, k)
+    ref = a.float() @ b.float().t()
+    assert rel(G.mm_nt(a, b), ref) < 1e-2
+    bias = rnd(n, dtype=torch.float32)
+    pre = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    act = G.mm_nt(a, b, bias=bias, gelu_aux=pre)
+    assert rel(pre, ref + bias) < 1e-2
+    assert torch.equal(act, F.gelu(pre))
+    bias16 = rnd(n)
+    assert rel(G.mm_nt(a, b, bias=bias16), ref + bias16.float()) < 1e-2
+    aux = rnd(m, n, scale=3.0)
+    g = G.mm_nt(a, b, dgelu_aux=aux)
+    assert rel(g, torch.ops.aten.gelu_backward(ref.to(torch.bfloat16), aux)) < 1e-2
+
+
+def test_nt_every_kernel_strided_output(gemm_mode):
+    torch.manual_seed(11)
+    a, b = rnd(9000, 512), rnd(1032, 512)
+    out_full = torch.zeros(9000, 1048, device=dev, dtype=torch.bfloat16)
+    out = out_full[:, 8:8 + 1032]
+    G.mm_nt(a, b, out=out)
+    assert rel(out, a.float() @ b.float().t()) < 1e-2
+    assert out_full[:, :8].abs().max() == 0 and out_full[:, 1040:].abs().max() == 0
+
+
+@pytest.mark.parametrize("m,n,k,splits", [(1024, 1024, 16384, 32), (2056, 1032, 8192, 4), (4096, 1024, 16384, 4)])
+def test_tn_every_kernel_many_items(gemm_mode, m, n, k, splits):
+    torch.manual_seed(m + n + k + splits)
+    dy, x = rnd(k, m), rnd(k, n)
+    out = G.mm_tn(dy, x, splits=splits)
+    assert rel(out, dy.float().t() @ x.float()) < 1e-5
