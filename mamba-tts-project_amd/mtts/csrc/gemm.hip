@@ -794,7 +794,7 @@ struct PLoader {
   }
 };
 
-template <bool AK, bool BKM, int EPI, bool OUT_F32>
+template <bool AK, bool BKM, int EPI, bool OUT_F32, bool PERSIST>
 __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char lds[kLds];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -806,9 +806,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
   const int total = p.tiles_m * p.tiles_n * p.splits;
-  const int nitems = (total - wid + nwg - 1) / nwg;   // items wid, wid + nwg, ...
+  const int nitems = PERSIST ? (total - wid + nwg - 1) / nwg : 1;   // items wid, wid + nwg, ...
   const int nk = p.k / kBK;
-  const int G = nitems * nk;                           // K-tiles of the whole stream
+  const int G = nitems * nk;                                         // K-tiles of the whole stream
 
   PLoader<AK, true> la;
   PLoader<BKM, false> lb;
@@ -818,27 +818,46 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   const int64_t bstep = BKM ? kBK * 2 : kBK * p.ldb * 2;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
 
-  // items of the current and the next tile (the stream stages up to two
-  // K-tiles ahead, which may belong to the next tile)
-  WorkItem cur = work_item(p, wid), nxt = cur;
-  if (nitems > 1) nxt = work_item(p, wid + nwg);
-  auto stage = [&](int g, int r, int icur) {
-    const bool next = g >= (icur + 1) * nk;
-    const WorkItem& it = next ? nxt : cur;
-    const int kt = g - (next ? icur + 1 : icur) * nk;
-    const uint32_t reg = lds0 + (g & 1) * kBuf + r * kRegion;
+  // an item's K-tile-0 operand origins (wave-uniform) and 8 per-thread DMA
+  // offsets (A0/A1 x 2, B0/B1 x 2), made once per item: a DMA's address
+  // register is never recomputed right behind the DMA that reads it.  With
+  // PERSIST the stream stages up to two K-tiles ahead, into the next item.
+  struct Src {
+    const char* a;
+    const char* b;
+    uint32_t o[8];
+  };
+  auto source = [&](const WorkItem& it, Src& sr) {
     const int64_t k0 = (int64_t)it.split * p.k;
-    if (r == R_A0 || r == R_A1) {
-      const char* base = (const char*)(AK ? p.a + k0 : p.a + k0 * p.lda) + kt * astep;
-      const int s = r - R_A0;
-      glds16(base, la.off(it.m0, p.m, p.lda, s, 0), reg + wave * 1024);
-      glds16(base, la.off(it.m0, p.m, p.lda, s, 1), reg + 8192 + wave * 1024);
-    } else {
-      const char* base = (const char*)(BKM ? p.b + k0 : p.b + k0 * p.ldb) + kt * bstep;
-      const int s = r - R_B0;
-      glds16(base, lb.off(it.n0, p.n, p.ldb, s, 0), reg + wave * 1024);
-      glds16(base, lb.off(it.n0, p.n, p.ldb, s, 1), reg + 8192 + wave * 1024);
-    }
+    sr.a = (const char*)(AK ? p.a + k0 : p.a + k0 * p.lda);
+    sr.b = (const char*)(BKM ? p.b + k0 : p.b + k0 * p.ldb);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        sr.o[s * 2 + i] = la.off(it.m0, p.m, p.lda, s, i);
+        sr.o[4 + s * 2 + i] = lb.off(it.n0, p.n, p.ldb, s, i);
+      }
+  };
+  WorkItem cur = work_item(p, wid), nxt = cur;
+  Src scur, snxt;
+  source(cur, scur);
+  if constexpr (PERSIST) {
+    if (nitems > 1) nxt = work_item(p, wid + nwg);
+    source(nxt, snxt);
+  }
+  int kbase = 0;   // stream index of the current item's K-tile 0
+  auto stage = [&](int g, int r) {
+    bool next = false;
+    if constexpr (PERSIST) next = g >= kbase + nk;
+    const int kt = g - (next ? kbase + nk : kbase);
+    const uint32_t reg = lds0 + (g & 1) * kBuf + r * kRegion;
+    const int oi = (r == R_A0 ? 0 : r == R_A1 ? 2 : r == R_B0 ? 4 : 6);
+    const bool isa = r == R_A0 || r == R_A1;
+    const char* base = isa ? (next ? snxt.a : scur.a) + kt * astep : (next ? snxt.b : scur.b) + kt * bstep;
+    const uint32_t o0 = next ? snxt.o[oi] : scur.o[oi], o1 = next ? snxt.o[oi + 1] : scur.o[oi + 1];
+    glds16(base, o0, reg + wave * 1024);
+    glds16(base, o1, reg + 8192 + wave * 1024);
   };
 
   constexpr int kBiasOps = EpiOps<EPI, OUT_F32>::bias;
@@ -853,8 +872,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: all of K-tile 0, A0 / B0 of K-tile 1
-  stage(0, R_A0, 0); stage(0, R_B0, 0); stage(0, R_B1, 0); stage(0, R_A1, 0);
-  if (G > 1) { stage(1, R_A0, 0); stage(1, R_B0, 0); }
+  stage(0, R_A0); stage(0, R_B0); stage(0, R_B1); stage(0, R_A1);
+  if (G > 1) { stage(1, R_A0); stage(1, R_B0); }
   if (G > 1) wait_ops<8>(); else wait_ops<4>();   // A0(0), B0(0) landed
   sbar();
   if (wr == 1) sbar();   // group 1 runs one barrier behind
@@ -873,64 +892,208 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   __builtin_amdgcn_s_setprio(0);                                                            \
   __builtin_amdgcn_sched_barrier(0);                                                        \
   sbar();
-  for (int i = 0; i < nitems; ++i) {
-    for (int t = 0; t < nk; ++t) {
-      const int g = i * nk + t;
-      const char* bufp = lbase + (g & 1) * kBuf;
-      const bool n1 = g + 1 < G, n2 = g + 2 < G;
-      // a tile boundary's epilogue ops sit between the regions the first
-      // K-tile's waits need and that wait
-      const int ex = (t == 0 && i > 0) ? kEpiOps : 0;
-      if (t == 0 && i > 0) {
-        // ---- the previous tile's epilogue, then this tile's bias (read segment of q0)
+  // Wait counts (VMEM ops younger than the needed region): steady 6 / 10 / 8;
+  // the stream's first K-tile 8 / 8 / 8; its last two fewer; + kEpiOps in a
+  // tile's first K-tile after an epilogue.  One uniform branch per wait.
+  for (int g = 0; g < G; ++g) {
+    const int t = g - kbase;
+    if constexpr (PERSIST) {
+      if (t == nk) {
+        // ---- the finished tile's epilogue, then the next tile's bias: in the
+        // read segment of the next K-tile's first phase, beside the partner
+        // group's last MFMA segment
         store_tile_buf<EPI, OUT_F32>(p, acc, bias, cur.m0, cur.n0, wr, wc, lane, cur.split);
+        kbase += nk;
         cur = nxt;
-        if (i + 1 < nitems) nxt = work_item(p, wid + (i + 1) * nwg);
+        scur = snxt;
+        if (kbase + nk < G) {
+          nxt = work_item(p, wid + (kbase / nk + 1) * nwg);
+          source(nxt, snxt);
+        }
         load_bias<EPI>(p, cur.n0, wc, lane, bias);
 #pragma unroll
         for (int a = 0; a < 8; ++a)
 #pragma unroll
           for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      // ---- q0: A0 x B0 | stage A1(g+1) | wait B1(g)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) b0f[ks][nb] = frag<BKM>(bufp + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
-      }
-      if (n1) stage(g + 1, R_A1, i);
-      if (g == 0) wait_ops_rt<8>(n1 ? 8 : 2); else wait_ops_rt<6>((n1 ? 6 : 0) + ex);
-      sbar();
-      PP_MFMA(b0f, 0, 0)
-      // ---- q1: A0 x B1 | stage B1(g+1) | wait A1(g)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) b1f[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
-      if (n1) stage(g + 1, R_B1, i);
-      if (g == 0) wait_ops_rt<8>(n1 ? 8 : 0); else wait_ops_rt<10>((n1 ? 10 : 2) + ex);
-      sbar();
-      PP_MFMA(b1f, 0, 2)
-      // ---- q2: A1 x B1 | stage A0(g+2)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A1 * kRegion, wr * 64 + mb * 16, ks, lane);
-      if (n2) stage(g + 2, R_A0, i);
-      sbar();
-      PP_MFMA(b1f, 4, 2)
-      // ---- q3: A1 x B0 | stage B0(g+2) | wait A0 / B0(g+1)
-      if (n2) stage(g + 2, R_B0, i);
-      if (n1) wait_ops_rt<8>((n2 ? 8 : 4) + ex);
-      sbar();
-      PP_MFMA(b0f, 4, 0)
     }
+    const int ex = (PERSIST && g == kbase && g > 0) ? kEpiOps : 0;
+    const bool steady = g > 0 && g + 2 < G && ex == 0;
+    const bool n1 = g + 1 < G, n2 = g + 2 < G;
+    const char* bufp = lbase + (g & 1) * kBuf;
+    // ---- q0: A0 x B0 | stage A1(g+1) | wait B1(g)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b0f[ks][nb] = frag<BKM>(bufp + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
+    }
+    if (n1) stage(g + 1, R_A1);
+    if (steady) wait_ops<6>();
+    else wait_ops_rt<6>(g == 0 ? (n1 ? 8 : 2) : (n1 ? 6 : 0) + ex);
+    sbar();
+    PP_MFMA(b0f, 0, 0)
+    // ---- q1: A0 x B1 | stage B1(g+1) | wait A1(g)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b1f[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
+    if (n1) stage(g + 1, R_B1);
+    if (steady) wait_ops<10>();
+    else wait_ops_rt<10>(g == 0 ? (n1 ? 8 : 0) : (n1 ? 10 : 2) + ex);
+    sbar();
+    PP_MFMA(b1f, 0, 2)
+    // ---- q2: A1 x B1 | stage A0(g+2)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A1 * kRegion, wr * 64 + mb * 16, ks, lane);
+    if (n2) stage(g + 2, R_A0);
+    sbar();
+    PP_MFMA(b1f, 4, 2)
+    // ---- q3: A1 x B0 | stage B0(g+2) | wait A0 / B0(g+1)
+    if (n2) stage(g + 2, R_B0);
+    if (steady) wait_ops<8>();
+    else if (n1) wait_ops_rt<8>((n2 ? 8 : 4) + ex);
+    sbar();
+    PP_MFMA(b0f, 4, 0)
   }
 #undef PP_MFMA
   if (wr == 0) sbar();   // the same barrier count for both groups
   store_tile_buf<EPI, OUT_F32>(p, acc, bias, cur.m0, cur.n0, wr, wc, lane, cur.split);
+}
+
+// round-3 first ping-pong form (one tile per workgroup, compiler-visible
+// global-store epilogue): kept as MTTS_GEMM_PP=3 for in-process A/B
+template <int N>
+__device__ __forceinline__ void wait_regions() { wait_vm<2 * N>(); }
+__device__ __forceinline__ void wait_regions_rt(int n) {
+  switch (n) {
+    case 0: wait_regions<0>(); break;
+    case 1: wait_regions<1>(); break;
+    case 2: wait_regions<2>(); break;
+    case 3: wait_regions<3>(); break;
+    case 4: wait_regions<4>(); break;
+    default: wait_regions<5>(); break;
+  }
+}
+
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 1) void gemm_pp1_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int split = id / tiles;
+  const int tile = id % tiles;
+  const int gsz = p.group * p.tiles_n;
+  const int g0 = (tile / gsz) * p.group;
+  const int gr = min(p.group, p.tiles_m - g0);
+  const int tm = g0 + (tile % gsz) % gr, tn = (tile % gsz) / gr;
+  const int m0 = tm * kTile, n0 = tn * kTile;
+
+  const int64_t k0 = (int64_t)split * p.k;
+  const char* abase;
+  const char* bbase;
+  int64_t astep, bstep;
+  if constexpr (AK) { abase = (const char*)(p.a + k0); astep = kBK * 2; }
+  else { abase = (const char*)(p.a + k0 * p.lda); astep = kBK * p.lda * 2; }
+  if constexpr (BKM) { bbase = (const char*)(p.b + k0); bstep = kBK * 2; }
+  else { bbase = (const char*)(p.b + k0 * p.ldb); bstep = kBK * p.ldb * 2; }
+
+  Loader<AK, true> la;
+  Loader<BKM, false> lb;
+  la.init(tid, m0, p.m, p.lda);
+  lb.init(tid, n0, p.n, p.ldb);
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  auto stage = [&](int kt, int r) {
+    const uint32_t reg = lds0 + (kt & 1) * kBuf + r * kRegion;
+    if (r == R_A0 || r == R_A1) {
+      la.stage1(abase + kt * astep, r - R_A0, reg, wave, 0);
+      la.stage1(abase + kt * astep, r - R_A0, reg, wave, 1);
+    } else {
+      lb.stage1(bbase + kt * bstep, r - R_B0, reg, wave, 0);
+      lb.stage1(bbase + kt * bstep, r - R_B0, reg, wave, 1);
+    }
+  };
+
+  const int nk = p.k / kBK;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: all of K-tile 0, A0 / B0 of K-tile 1 (A1 / B1 of K-tile 1 are
+  // staged by K-tile 0's phases 0 / 1)
+  stage(0, R_A0); stage(0, R_B0); stage(0, R_B1); stage(0, R_A1);
+  if (nk > 1) { stage(1, R_A0); stage(1, R_B0); }
+  if (nk > 1) wait_regions<4>(); else wait_regions<2>();   // A0(0), B0(0) landed
+  sbar();
+  if (wr == 1) sbar();   // group 1 runs one barrier behind
+
+  const char* lbase = lds;
+  s16x8 af[2][4], b0f[2][2], b1f[2][2];   // [ks][block]
+#define PP_MFMA(BF, MO, NO)                                                                   \
+  __builtin_amdgcn_sched_barrier(0);                                                        \
+  __builtin_amdgcn_s_waitcnt(0xC07F);                                                        \
+  __builtin_amdgcn_sched_barrier(0);                                                        \
+  __builtin_amdgcn_s_setprio(1);                                                            \
+  _Pragma("unroll") for (int ks_ = 0; ks_ < 2; ++ks_)                                        \
+  _Pragma("unroll") for (int mb_ = 0; mb_ < 4; ++mb_)                                        \
+  _Pragma("unroll") for (int nb_ = 0; nb_ < 2; ++nb_)                                        \
+      acc[(MO) + mb_][(NO) + nb_] = mfma(BF[ks_][nb_], af[ks_][mb_], acc[(MO) + mb_][(NO) + nb_]); \
+  __builtin_amdgcn_s_setprio(0);                                                            \
+  __builtin_amdgcn_sched_barrier(0);                                                        \
+  sbar();
+  for (int t = 0; t < nk; ++t) {
+    const char* bufp = lbase + (t & 1) * kBuf;
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    // ---- q0: A0 x B0 | stage A1(t+1) | wait B1(t)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b0f[ks][nb] = frag<BKM>(bufp + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
+    }
+    if (n1) stage(t + 1, R_A1);
+    if (t == 0) wait_regions_rt(n1 ? 4 : 1); else wait_regions_rt(n1 ? 3 : 0);
+    sbar();
+    PP_MFMA(b0f, 0, 0)
+    // ---- q1: A0 x B1 | stage B1(t+1) | wait A1(t)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b1f[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
+    if (n1) stage(t + 1, R_B1);
+    if (t == 0) wait_regions_rt(n1 ? 4 : 0); else wait_regions_rt(n1 ? 5 : 1);
+    sbar();
+    PP_MFMA(b1f, 0, 2)
+    // ---- q2: A1 x B1 | stage A0(t+2)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A1 * kRegion, wr * 64 + mb * 16, ks, lane);
+    if (n2) stage(t + 2, R_A0);
+    sbar();
+    PP_MFMA(b1f, 4, 2)
+    // ---- q3: A1 x B0 | stage B0(t+2) | wait A0 / B0(t+1)
+    if (n2) stage(t + 2, R_B0);
+    if (n1) wait_regions_rt(n2 ? 4 : 2);
+    sbar();
+    PP_MFMA(b0f, 4, 0)
+  }
+#undef PP_MFMA
+  if (wr == 0) sbar();   // the same barrier count for both groups
+  store_tile<EPI, OUT_F32>(p, acc, m0, n0, wr, wc, lane, split);
 }
 
 // out[i] = beta*out[i] + sum_s slab[s][i] (fixed order); rows x cols with row strides
@@ -949,12 +1112,17 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restri
   }
 }
 
-// MTTS_GEMM_PP: 0 = the round-2 single-group kernel, 1 = ping-pong with one
-// tile per workgroup, 2 (default) = ping-pong persistent (read per launch:
-// in-process A/B)
+// MTTS_GEMM_PP: 0 = the round-2 single-group kernel, 1 (default) = ping-pong
+// with one tile per workgroup, 2 = ping-pong persistent, 3 = the first
+// ping-pong form (read per launch: in-process A/B).  Measured on the C2
+// shapes (tools/gemm_pp_ab.py, same box, interleaved): ping-pong 1078-1339
+// TF/s NT, 696-1110 TN, vs 997-1321 / 684-1128 for the round-2 kernel; the
+// persistent form (epilogue inside the next tile's first read segment) 0-7 %
+// slower than one tile per workgroup: the two groups' epilogues serialise
+// on the barrier and cost what a fresh workgroup's prologue does.
 static int pp_mode() {
   const char* e = getenv("MTTS_GEMM_PP");
-  return e ? atoi(e) : 2;
+  return e ? atoi(e) : 1;
 }
 static int num_cus() {
   static int n = [] {
@@ -974,6 +1142,10 @@ void launch(const GemmParams& p, int nwg, hipStream_t st) {
   const int64_t abytes = (EPI & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) ? (int64_t)p.m * p.ld_aux * 2 : 0;
   const bool pp_ok = (F32 || p.wide_out) && cbytes < (1ll << 31) && abytes < (1ll << 31) &&
                      (!F32 || p.beta == 0.f || p.splits == 1);
+  if (mode == 3) {
+    hipLaunchKernelGGL((gemm_pp1_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
+    return;
+  }
   if (mode == 0 || !pp_ok) {
     hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
     return;
@@ -982,7 +1154,8 @@ void launch(const GemmParams& p, int nwg, hipStream_t st) {
   // stream has >= 2 K-tiles per item and the epilogue needs no C reads
   int grid = nwg;
   if (mode >= 2 && p.k / kBK >= 2 && !(F32 && p.beta != 0.f)) grid = std::min(nwg, num_cus());
-  hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32>), dim3(grid), dim3(kThreads), 0, st, p);
+  if (grid < nwg) hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32, true>), dim3(grid), dim3(kThreads), 0, st, p);
+  else hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32, false>), dim3(grid), dim3(kThreads), 0, st, p);
 }
 
 }  // namespace

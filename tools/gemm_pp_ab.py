@@ -54,20 +54,21 @@ for name, (m, n, k) in shapes.items():
     for cname, (ours, blas, ref) in cases.items():
         r = ref()
         errs = {}
-        for v in ("2", "1", "0"):
+        for v in ("2", "1", "0", "3"):
             mode(v)
             errs[v] = rel(ours(), r)
-        res = {"ps": [], "pp": [], "old": [], "blas": []}
-        for _ in range(3):
+        res = {"ps": [], "pp": [], "pp1": [], "old": [], "blas": []}
+        for _ in range(5):
             mode("2"); res["ps"].append(t(ours))
             mode("1"); res["pp"].append(t(ours))
+            mode("3"); res["pp1"].append(t(ours))
             mode("0"); res["old"].append(t(ours))
             if blas is not None:
                 res["blas"].append(t(blas))
         mode("2")
-        med = {kk: sorted(vv)[1] for kk, vv in res.items() if vv}
+        med = {kk: sorted(vv)[len(vv) // 2] for kk, vv in res.items() if vv}
         for kk, vv in med.items():
             tot[(cname, kk)] = tot.get((cname, kk), 0.0) + vv
         print(f"{name:8s} {cname:5s} m={m} n={n} k={k}  " + "  ".join(f"{kk} {fl / vv / 1e9:6.0f} TF/s" for kk, vv in med.items())
-              + f"  err ps {errs['2']:.1e} pp {errs['1']:.1e} old {errs['0']:.1e}", flush=True)
+              + f"  err {max(errs.values()):.1e}", flush=True)
 print({f"{a}/{b}": round(v, 3) for (a, b), v in tot.items()})
