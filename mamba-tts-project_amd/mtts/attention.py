@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import attn_kernels
-from .linear import _want_t, cast_scope, cast_weight, cast_weight_t, colsum, linear, wgrad
+from .linear import _want_t, cast_scope, cast_weight, cast_weight_t, colsum, linear, proj, wgrad
 
 
 class InProjFn(torch.autograd.Function):
@@ -33,8 +33,8 @@ class InProjFn(torch.autograd.Function):
         d = query.shape[-1]
         Wc, bc = cast_weight(weight, cd), cast_weight(bias, cd)
         x2, k2 = query.reshape(-1, d), key.reshape(-1, d)
-        q = torch.addmm(bc[:d], x2, Wc[:d].t())
-        kv = torch.addmm(bc[d:], k2, Wc[d:].t())
+        q = proj(x2, Wc[:d], bc[:d])
+        kv = proj(k2, Wc[d:], bc[d:])
         ctx.save_for_backward(x2, k2, Wc)
         ctx.weight = weight
         ctx.meta = (query.shape, key.shape, weight.dtype, bias.dtype)
@@ -49,8 +49,8 @@ class InProjFn(torch.autograd.Function):
         dkv2 = dkv.reshape(-1, 2 * d).to(Wc.dtype)
         if Wc.dtype == torch.bfloat16 and _want_t(ctx.weight):
             Wt = cast_weight_t(ctx.weight, Wc.dtype)       # (d, 3d): dgrads as dy @ (W^T)^T
-            dquery = (dq2 @ Wt[:, :d].t()).view(qshape) if ctx.needs_input_grad[0] else None
-            dkey = (dkv2 @ Wt[:, d:].t()).view(kshape) if ctx.needs_input_grad[1] else None
+            dquery = proj(dq2, Wt[:, :d]).view(qshape) if ctx.needs_input_grad[0] else None
+            dkey = proj(dkv2, Wt[:, d:]).view(kshape) if ctx.needs_input_grad[1] else None
         else:
             dquery = (dq2 @ Wc[:d]).view(qshape) if ctx.needs_input_grad[0] else None
             dkey = (dkv2 @ Wc[d:]).view(kshape) if ctx.needs_input_grad[1] else None

@@ -18,9 +18,8 @@ EPI_BIAS, EPI_GELU, EPI_DGELU = 1, 2, 4
 NT, TN = 0, 1
 TILE = 256
 ENABLED = True   # routing switch for in-process A/B timing (tools/gemm_step_ab.py)
-FFN_FUSED = False  # FFN with GELU fused into the GEMM epilogues (linear.ffn): off by default,
-#                    the NT kernel is still slower than hipBLASLt by more than the
-#                    GELU launches it saves (tools/gemm_step_ab.py: 36.3 vs 35.8 ms)
+FFN_FUSED = True   # FFN with bias + GELU fused into the first GEMM's epilogue and the GELU
+#                    backward into the second's data gradient (linear.ffn)
 
 
 def _rowmajor(t):

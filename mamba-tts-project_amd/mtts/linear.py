@@ -1,8 +1,8 @@
 """Linear layers of the decoder hot path (projections, FFN, head).
 
-Forward/dgrad GEMMs go to hipBLASLt through torch (plain library GEMMs: they
-already run at 1.0-1.3 PF/s bf16 on MI355X for these shapes, see
-tools/bench_gemm.py).  Two things are done differently from nn.Linear:
+Forward / data-gradient GEMMs of the large projections run on the
+hand-written ping-pong NT MFMA kernel (csrc/gemm.hip, `proj`); skinny and
+short-M ones on hipBLASLt through torch.  Further differences from nn.Linear:
 
 * weight gradients (small output, K = B*T tokens) are computed split-K with
   fp32 partial products (4 K-chunks, summed in fp32): the stock `dy^T @ x`
@@ -154,6 +154,32 @@ def colsum(x2d: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
 HIP_WGRAD_MIN = 256
 
 
+# forward / data-gradient projections y = x W^T (+ b) run on the hand-written
+# NT kernel (mtts_gemm, ping-pong) when both weight dims are >= NT_MIN and the
+# output has >= NT_MIN_TILES 256x256 tiles (half the chip): the C2 / C5
+# projections (in/out_proj, attention q/out, FFN).  Skinny (x_proj, dt_proj,
+# head) and short-M (text K/V, M = B * T_text) GEMMs stay on hipBLASLt, whose
+# small macro-tiles fill the chip there.
+NT_MIN = 256
+NT_MIN_TILES = 128
+
+
+def _nt_route(x2, w, bias=None):
+    m, k = x2.shape
+    n = w.shape[0]
+    return (n >= NT_MIN and k >= NT_MIN and -(-m // G.TILE) * -(-n // G.TILE) >= NT_MIN_TILES and G.nt_ok(x2, w)
+            and (bias is None or (bias.dtype in (torch.float32, torch.bfloat16) and bias.stride(-1) == 1
+                                  and G.epi_ok(bias))))
+
+
+def proj(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor = None) -> torch.Tensor:
+    """x2 (M, K) @ w (N, K)^T (+ bias) in x2's dtype: the NT MFMA kernel when
+    the shape routes there, else torch (hipBLASLt)."""
+    if _nt_route(x2, w, bias):
+        return G.mm_nt(x2, w, bias=bias)
+    return torch.addmm(bias, x2, w.t()) if bias is not None else x2 @ w.t()
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4, out: torch.Tensor = None) -> torch.Tensor:
     """dW = dy^T @ x in fp32; dy (M, n), x (M, k) with the same dtype.
     `out` (n, k) fp32, possibly a row slice of a larger gradient, receives it."""
@@ -186,13 +212,12 @@ class LinearFn(torch.autograd.Function):
         if r0 is not None:
             w = w[r0:r1]
         x2 = x.reshape(-1, x.shape[-1])
+        b = None
         if bias is not None:
             b = cast_weight(bias, cd)
             if r0 is not None:
                 b = b[r0:r1]
-            y = torch.addmm(b, x2, w.t())
-        else:
-            y = x2 @ w.t()
+        y = proj(x2, w, b)
         ctx.save_for_backward(x2, w)
         ctx.weight = weight
         ctx.meta = (x.shape, weight.shape, weight.dtype, None if bias is None else bias.dtype, r0, r1)
@@ -211,7 +236,7 @@ class LinearFn(torch.autograd.Function):
                 wt = cast_weight_t(ctx.weight, w.dtype)        # (k, n): dy @ (W^T)^T, the fast operand layout
                 if r0 is not None:
                     wt = wt[:, r0:r1]
-                dx = (dy2 @ wt.t()).view(xshape)
+                dx = proj(dy2, wt).view(xshape)
             else:
                 dx = (dy2 @ w).view(xshape)
         dW = db = None
@@ -253,7 +278,7 @@ class FFNFn(torch.autograd.Function):
         h2 = h.reshape(-1, h.shape[-1])
         pre = torch.empty(h2.shape[0], W1.shape[0], device=h.device, dtype=cd)
         a = G.mm_nt(h2, W1, bias=B1, gelu_aux=pre)
-        y = torch.addmm(B2, a, W2.t())
+        y = proj(a, W2, B2)
         ctx.save_for_backward(h2, pre, a, W1, W2)
         ctx.ws = (w1, w2)
         ctx.meta = (h.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
@@ -271,7 +296,7 @@ class FFNFn(torch.autograd.Function):
         dh = None
         if ctx.needs_input_grad[0]:
             if _want_t(w1):
-                dh = dpre @ cast_weight_t(w1, W1.dtype).t()
+                dh = proj(dpre, cast_weight_t(w1, W1.dtype))
             else:
                 dh = dpre @ W1
             dh = dh.view(hshape)
