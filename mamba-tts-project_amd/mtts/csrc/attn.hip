@@ -345,23 +345,42 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt) dK[dt] = dV[dt] = f32x16{};
 
+    // Q / dO / O of a 32-query slice are loaded into registers ONE SLICE
+    // AHEAD (issued right after the current slice is staged), so their
+    // global-memory latency hides under the current slice's MFMAs instead of
+    // sitting between two barriers of every slice.
+    constexpr int NPT = (32 * HD / CH + nthr - 1) / nthr;   // 16-byte chunks per thread per array
+    const T* qb = (const T*)f.q + b * f.q_bs + hh * HD;
+    const T* ob = (const T*)f.out + b * f.o_bs + hh * HD;
+    const T* gb = (const T*)a.dout + b * a.do_bs + hh * HD;
+    f32x4 pq[NPT], pg[NPT], po[NPT];
+    auto load_slice = [&](int q0) {
+#pragma unroll
+      for (int j = 0; j < NPT; ++j) {
+        const int i = tid + j * nthr;
+        const int row = i / (HD / CH), cc = (i % (HD / CH)) * CH;
+        const int qi = q0 + row;
+        pq[j] = pg[j] = po[j] = f32x4{};
+        if (i < 32 * HD / CH && qi < qend) {
+          pq[j] = *(const f32x4*)(qb + qi * f.q_ls + cc);
+          pg[j] = *(const f32x4*)(gb + qi * a.do_ls + cc);
+          if constexpr (MODE != kBwdKV) po[j] = *(const f32x4*)(ob + qi * f.o_ls + cc);
+        }
+      }
+    };
+    if (MODE != kBwdQ || kg == 0) load_slice(qbeg);
     for (int q0 = qbeg; q0 < qend; q0 += 32) {
       __syncthreads();
       // ---- stage Q, dO images; delta = rowsum(dO * O); -lse/scale
       // (mode 2: its single slice once, kept across key groups)
       if (MODE != kBwdQ || kg == 0) {
-        const T* qb = (const T*)f.q + b * f.q_bs + hh * HD;
-        const T* ob = (const T*)f.out + b * f.o_bs + hh * HD;
-        const T* gb = (const T*)a.dout + b * a.do_bs + hh * HD;
-        for (int i = tid; i < 32 * HD / CH; i += nthr) {
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+          const int i = tid + j * nthr;
+          if (NPT * nthr != 32 * HD / CH && i >= 32 * HD / CH) break;
           const int row = i / (HD / CH), cc = (i % (HD / CH)) * CH;
           const int qi = q0 + row;
-          f32x4 qv = {}, gv = {}, ov = {};
-          if (qi < qend) {
-            qv = *(const f32x4*)(qb + qi * f.q_ls + cc);
-            gv = *(const f32x4*)(gb + qi * a.do_ls + cc);
-            if constexpr (MODE != kBwdKV) ov = *(const f32x4*)(ob + qi * f.o_ls + cc);
-          }
+          const f32x4 qv = pq[j], gv = pg[j], ov = po[j];
           *(f32x4*)(sQ + row * P + cc) = qv;
           *(f32x4*)(sO + row * P + cc) = gv;
           float dl = 0.f;
@@ -390,6 +409,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
           if (qi < qend) L = -f.lse[((int64_t)b * f.heads + hh) * f.q_len + qi] * inv_scale;  // P = exp2(c (S + L))
           sL[tid] = L;
         }
+        if (MODE != kBwdQ && q0 + 32 < qend) load_slice(q0 + 32);   // next slice, in flight under this one
       }
       __syncthreads();
       // ---- S = Q K^T - lse/scale and dP = dO V^T - delta (key on the lane)

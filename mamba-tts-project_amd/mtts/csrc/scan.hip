@@ -1894,15 +1894,20 @@ static bool wide_io_ok(const MttsScanFwdArgs* a) {
 // checkpoint stores only make the wait stricter).  With DIRECT_STORE 0 the
 // outputs replace u in the tile image and leave as 16-byte row chunks
 // ([stores of it-1] first, wait for NDMA).
-template <typename Tio, typename Tbc, bool SP, bool HZ>
-__global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdArgs a) {
+//
+// SMALL (MTTS_C1_SMALL=1): 8-step tiles and a lighter register budget, so TWO
+// workgroups share a CU (<= 80 KiB of LDS and <= 256 registers per lane each):
+// two waves per SIMD, one hiding the other's dependency and memory stalls.
+template <typename Tio, typename Tbc, bool SP, bool HZ, bool SMALL>
+__global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const MttsScanFwdArgs a) {
   constexpr int ES = (int)sizeof(Tio);
   constexpr int EPC = 16 / ES;            // elements per 16-byte chunk
   constexpr int CPR = 64 / EPC;           // chunks per 64-channel row
   constexpr int RPD = 64 / CPR;           // rows per DMA instruction (1 KiB): 4 fp32, 8 bf16
-  constexpr int DPT = ES == 4 ? 4 : 2;    // DMA instructions per array per tile
-  constexpr int TT = DPT * RPD;           // steps per tile: 16
-  constexpr int NB = ES == 4 ? 3 : 4;     // tile ring: DMA NB-1 tiles ahead (LDS: 155 / 112 KiB)
+  constexpr int DPT = ES == 4 ? (SMALL ? 2 : 4) : (SMALL ? 1 : 2);   // DMA instructions per array per tile
+  constexpr int TT = DPT * RPD;           // steps per tile: 16 (SMALL: 8)
+  // tile ring: DMA NB-1 tiles ahead (LDS per block: 155 / 112 KiB; SMALL 76 / 64 KiB)
+  constexpr int NB = ES == 4 ? 3 : (SMALL ? 5 : 4);
   constexpr int NAR = HZ ? 3 : 2;
   constexpr int IMG = TT * 64;
   constexpr int BCV = TT * 2 * kN / 64;   // B/C values staged per lane per tile
@@ -2140,6 +2145,15 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
 
 // the one-lane-per-channel forward applies: whole 64-channel waves, 16-byte
 // B/C staging loads, and (unless forced for tests) B*D filling every SIMD
+// MTTS_C1_SMALL=1: the 8-step-tile, two-waves-per-SIMD form (read per launch).
+// Measured slower at the north-star shape (tools/scan_ab.py, same box,
+// interleaved: fp32 2.171 vs 2.132 ms, bf16 2.062 vs 1.961 ms): the halved
+// tiles double the per-tile overhead and the partner wave contends for the
+// same VALU, so the default stays the 16-step, one-wave-per-SIMD kernel.
+static bool c1_small() {
+  const char* e = getenv("MTTS_C1_SMALL");
+  return e && atoi(e) != 0;
+}
 static bool c1_ok(const MttsScanFwdArgs* a) {
   if (getenv("MTTS_SCAN_NO_C1") || !wide_io_ok(a) || a->dim % 64) return false;
   const int es = a->dtype_io == MTTS_BF16 ? 2 : 4, eb = a->dtype_bc == MTTS_BF16 ? 2 : 4;
@@ -2159,8 +2173,14 @@ static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream
   float* seg = (float*)a->workspace;
   if (c1_ok(a)) {
     const dim3 grid((a->dim / 64 + 3) / 4, a->batch);
-    if (a->z) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true>), grid, dim3(256), 0, st, *a);
-    else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false>), grid, dim3(256), 0, st, *a);
+    const bool sm = c1_small();
+    if (a->z) {
+      if (sm) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true, true>), grid, dim3(256), 0, st, *a);
+      else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true, false>), grid, dim3(256), 0, st, *a);
+    } else {
+      if (sm) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false, true>), grid, dim3(256), 0, st, *a);
+      else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false, false>), grid, dim3(256), 0, st, *a);
+    }
     return;
   }
   if (wide_io_ok(a) && !getenv("MTTS_SCAN_FWD_V1")) {

@@ -17,8 +17,9 @@ from mtts import ops  # noqa: E402
 
 VARIANTS = [("xl", {}), ("dpp", {"MTTS_SCAN_XDPP": "1"}), ("v1", {"MTTS_SCAN_FWD_V1": "1"}),
             ("p2", {"MTTS_SCAN_P": "2"}), ("p2k2", {"MTTS_SCAN_P": "2", "MTTS_SCAN_SEGS": "2"}),
-            ("k2", {"MTTS_SCAN_SEGS": "2"}), ("p4", {"MTTS_SCAN_P": "4"}), ("w2", {"MTTS_SCAN_NO_C1": "1"})]
-KEYS = ("MTTS_SCAN_FWD_V1", "MTTS_SCAN_XDPP", "MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_NO_C1")
+            ("k2", {"MTTS_SCAN_SEGS": "2"}), ("p4", {"MTTS_SCAN_P": "4"}), ("w2", {"MTTS_SCAN_NO_C1": "1"}),
+            ("c1small", {"MTTS_C1_SMALL": "1"})]
+KEYS = ("MTTS_SCAN_FWD_V1", "MTTS_SCAN_XDPP", "MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_NO_C1", "MTTS_C1_SMALL")
 sel = [a for a in sys.argv[1:] if not a.startswith("-")]
 variants = [v for v in VARIANTS if not sel or v[0] in sel]
 dtypes = (torch.bfloat16, torch.float32)
