@@ -31,6 +31,8 @@
 //     fixed order (deterministic, no atomics).
 // fp32 I/O uses the exact-f32 MFMA (v_mfma_f32_32x32x2_f32) with the same
 // structure.
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -85,6 +87,20 @@ constexpr int tr_pitch(int hd) {
   int dw = hd / 2 < 16 ? 16 : hd / 2;
   while (dw % 64 != 16 && dw % 64 != 48) ++dw;
   return dw * 2;
+}
+
+// sum over NL consecutive lanes (NL | 64, groups lane-aligned) with DPP /
+// permlane stages instead of ds_bpermute shuffles
+template <int NL>
+__device__ __forceinline__ float lane_group_sum(float v) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (NL >= 2) v += mtts::dpp<mtts::kQuadXor1>(v);
+  if constexpr (NL >= 4) v += mtts::dpp<mtts::kQuadXor2>(v);
+  if constexpr (NL >= 8) v += mtts::xor4(v, lane);
+  if constexpr (NL >= 16) v += mtts::xor8(v);
+  if constexpr (NL >= 32) v += mtts::xor16(v, lane);
+  if constexpr (NL >= 64) v += mtts::xor32(v, lane);
+  return v;
 }
 
 template <int NL>
@@ -249,6 +265,137 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(MttsAttnFwdArgs a) {
   }
 }
 
+// Short key side (kv_len <= 128, bf16: C2's 128 text keys): the whole K / V
+// of the (batch, head) staged in LDS ONCE per workgroup (one barrier), then
+// every wave runs NSL 32-query slices back to back with no further barrier,
+// the next slice's Q fragments loaded into registers while the current one
+// computes.  Same math per slice as attn_fwd_kernel (all keys in one tile
+// sweep, online max / sum across the four 32-key tiles).
+constexpr int kShortKV = 128;
+
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_fwd_short_kernel(MttsAttnFwdArgs a, int nsl) {
+  constexpr int KP = HD + 8;         // K image: conflict-free row reads
+  constexpr int VP = tr_pitch(HD);   // V image: conflict-free column reads
+  constexpr int ND = (HD + 31) / 32;
+  constexpr int CH = 8;
+  constexpr int NQ = HD / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t sK[kShortKV * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[kShortKV * VP + 32];
+  __shared__ uint32_t sMask[kShortKV / 32];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, hh = blockIdx.y;
+  const bf16_t* kbase = (const bf16_t*)a.k + b * a.k_bs + hh * HD;
+  const bf16_t* vbase = (const bf16_t*)a.v + b * a.v_bs + hh * HD;
+  const uint8_t* mb = a.key_padding_mask ? a.key_padding_mask + b * a.mask_bs : nullptr;
+  const float c = a.scale * kLog2e;
+  const int nkt = (a.kv_len + 31) / 32;
+
+  // query slice sl of this wave: 32 queries
+  auto qrow = [&](int sl) { return ((blockIdx.x * nsl + sl) * nw + wave) * 32 + r; };
+  s16x8 QF[NQ], QN[NQ];
+  auto load_q = [&](int sl, s16x8 (&o)[NQ]) {
+    const int q = qrow(sl);
+    const bool qv = sl < nsl && q < a.q_len;
+    const bf16_t* qp = (const bf16_t*)a.q + b * a.q_bs + (int64_t)(qv ? q : 0) * a.q_ls + hh * HD;
+#pragma unroll
+    for (int s = 0; s < NQ; ++s) o[s] = qv ? *(const s16x8*)(qp + 16 * s + 8 * h) : s16x8{};
+  };
+  load_q(0, QF);
+
+  for (int i = tid; i < kShortKV * HD / CH; i += blockDim.x) {
+    const int row = i / (HD / CH), cc = (i % (HD / CH)) * CH;
+    f32x4 kv = {}, vv = {};
+    if (row < a.kv_len) {
+      kv = *(const f32x4*)(kbase + row * a.k_ls + cc);
+      vv = *(const f32x4*)(vbase + row * a.v_ls + cc);
+    }
+    *(f32x4*)(sK + row * KP + cc) = kv;
+    *(f32x4*)(sV + row * VP + cc) = vv;
+  }
+  if (wave < kShortKV / 64) {
+    const int key = 64 * wave + lane;
+    const bool ok = key < a.kv_len && !(mb && mb[key]);
+    const uint64_t bal = __ballot(ok);
+    if (lane == 0) {
+      sMask[2 * wave] = (uint32_t)bal;
+      sMask[2 * wave + 1] = (uint32_t)(bal >> 32);
+    }
+  }
+  __syncthreads();
+
+  for (int sl = 0; sl < nsl; ++sl) {
+    if (sl + 1 < nsl) load_q(sl + 1, QN);   // in flight under this slice
+    const int q = qrow(sl);
+    float m = -INFINITY, l = 0.f;
+    f32x16 O[ND];
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) O[dt] = f32x16{};
+#pragma unroll
+    for (int t = 0; t < kShortKV / 32; ++t) {
+      if (t >= nkt) break;
+      f32x16 S = {};
+      const bf16_t* kr = sK + (t * 32 + r) * KP + 8 * h;
+#pragma unroll
+      for (int s = 0; s < NQ; ++s) S = mfma_bf16(*(const s16x8*)(kr + 16 * s), QF[s], S);
+      const uint32_t w = sMask[t] >> (4 * h);
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const bool ok = (w >> ((i & 3) + 8 * (i >> 2))) & 1u;
+        S[i] = ok ? S[i] * c : -INFINITY;
+        tmax = fmaxf(tmax, S[i]);
+      }
+      tmax = fmaxf(tmax, mtts::xor32(tmax, lane));
+      const float mn = fmaxf(m, tmax);
+      const float ms = mn == -INFINITY ? 0.f : mn;
+      const float alpha = exp2_raw(m - ms);
+      float ps = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        S[i] = exp2_raw(S[i] - ms);
+        ps += S[i];
+      }
+      l = l * alpha + ps;
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) O[dt][i] *= alpha;
+      const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 pb = pack8(S, s);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          const bf16_t* p0 = sV + (t * 32 + 16 * s + 4 * h + qq) * VP + dt * 32 + 16 * g + 4 * pp;
+          O[dt] = mfma_bf16(cat(tr_read(p0), tr_read(p0 + 8 * VP)), pb, O[dt]);
+        }
+      }
+    }
+    const float lt = mtts::sum_xor32(l);
+    const float inv = 1.f / lt;  // fully masked: 0 * inf = NaN (torch MHA)
+    if (q < a.q_len) {
+      bf16_t* op = (bf16_t*)a.out + b * a.o_bs + (int64_t)q * a.o_ls + hh * HD;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = dt * 32 + 8 * g4 + 4 * h;
+          s16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = bfbits(O[dt][4 * g4 + e] * inv);
+          *(s16x4*)(op + d0) = v;
+        }
+      if (a.lse && h == 0) a.lse[((int64_t)b * a.heads + hh) * a.q_len + q] = (m + __builtin_amdgcn_logf(lt)) * kLn2;
+    }
+#pragma unroll
+    for (int s = 0; s < NQ; ++s) QF[s] = QN[s];
+  }
+}
+
 // ============================================================== backward
 struct BwdParams {
   MttsAttnBwdArgs a;
@@ -256,6 +403,7 @@ struct BwdParams {
   float* part;         // nchunk > 1: fp32 dK|dV partials [nchunk][B][Tk][2*H*hd]
   float* dq_acc;       // > 1 key group (mode 0): fp32 dq accumulator [B][Tq][H*hd]
   float* delta;        // modes 1/2: -rowsum(dO * O) per (b, h, query) [B][H][Tq]
+  int dq_vec;          // dq base / row stride 16-byte aligned: 16-byte dQ row stores
 };
 
 // Backward modes.  0: short key side (C2, <= one key group): workgroup =
@@ -291,6 +439,9 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
   __shared__ __attribute__((aligned(16))) T sS[KG * PS + 32];  // dS^T [key][query]
   __shared__ float sL[32], sD[32];
   __shared__ uint32_t sMask[KG / 32];
+  // per wave: its 32x32 dQ tile on the way to 16-byte row stores
+  constexpr int DQP = 32 + 16 / sizeof(T);
+  __shared__ __attribute__((aligned(16))) T sDq[NW][32 * DQP];
 
   const MttsAttnBwdArgs& a = p.a;
   const MttsAttnFwdArgs& f = a.f;
@@ -354,7 +505,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
     const T* ob = (const T*)f.out + b * f.o_bs + hh * HD;
     const T* gb = (const T*)a.dout + b * a.do_bs + hh * HD;
     f32x4 pq[NPT], pg[NPT], po[NPT];
+    float plse = 0.f;
     auto load_slice = [&](int q0) {
+      if (tid < 32) {
+        const int qi = q0 + tid;
+        plse = qi < qend ? f.lse[((int64_t)b * f.heads + hh) * f.q_len + qi] : 0.f;
+      }
 #pragma unroll
       for (int j = 0; j < NPT; ++j) {
         const int i = tid + j * nthr;
@@ -392,7 +548,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) dl += gv[e] * ov[e];
           }
-          dl = group_sum<HD / CH>(dl);
+          dl = lane_group_sum<HD / CH>(dl);
           if constexpr (MODE != kBwdKV) {
             if (i % (HD / CH) == 0) {
               sD[row] = -dl;
@@ -403,12 +559,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
         if constexpr (MODE == kBwdKV) {
           if (tid < 32) sD[tid] = q0 + tid < qend ? dbuf[q0 + tid] : 0.f;
         }
-        if (tid < 32) {
-          const int qi = q0 + tid;
-          float L = 0.f;
-          if (qi < qend) L = -f.lse[((int64_t)b * f.heads + hh) * f.q_len + qi] * inv_scale;  // P = exp2(c (S + L))
-          sL[tid] = L;
-        }
+        if (tid < 32) sL[tid] = q0 + tid < qend ? -plse * inv_scale : 0.f;  // P = exp2(c (S + L))
         if (MODE != kBwdQ && q0 + 32 < qend) load_slice(q0 + 32);   // next slice, in flight under this one
       }
       __syncthreads();
@@ -512,7 +663,27 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
           continue;
         }
         const int dim = dt * 32 + r;
-        if (dim < HD) {
+        if (nkg == 1 && HD % 32 == 0 && p.dq_vec) {
+          // one key group: the tile is final.  Through the wave's LDS tile so
+          // each lane stores whole 16-byte row pieces (a lane's accumulator
+          // holds one column: 16 two-byte stores per lane otherwise, and the
+          // store issue, not the MFMAs, set the slice time)
+          T* t = sDq[wave];
+#pragma unroll
+          for (int i = 0; i < 16; ++i) mtts::stf(t + acc_row(i, h) * DQP + r, Q[i] * f.scale);
+          __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the wave's own LDS writes, read back below
+          __builtin_amdgcn_wave_barrier();
+          constexpr int CPRW = 32 * sizeof(T) / 16;   // 16-byte pieces per tile row
+#pragma unroll
+          for (int j = 0; j < 32 * CPRW / 64; ++j) {
+            const int idx = lane + 64 * j, row = idx / CPRW, cc = (idx % CPRW) * (16 / sizeof(T));
+            const int qi = q0 + row;
+            if (qi < qend)
+              *(f32x4*)((T*)a.dq + b * a.dq_bs + (int64_t)qi * a.dq_ls + hh * HD + dt * 32 + cc) =
+                  *(const f32x4*)(t + row * DQP + cc);
+          }
+          __builtin_amdgcn_wave_barrier();
+        } else if (dim < HD) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int qi = q0 + acc_row(i, h);
@@ -754,6 +925,17 @@ int check_fwd(const MttsAttnFwdArgs* a, const char* who) {
 
 template <typename T, int HD>
 void launch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
+  if constexpr (sizeof(T) == 2 && HD % 32 == 0) {
+    const char* e = getenv("MTTS_ATTN_FWD_SHORT");
+    if (a->kv_len <= kShortKV && a->q_len >= 128 && (!e || atoi(e) != 0)) {
+      // >= 512 workgroups (two per CU), as many query slices per wave as that allows
+      const int64_t blocks128 = (int64_t)((a->q_len + 127) / 128) * a->heads * a->batch;
+      int nsl = (int)std::max<int64_t>(1, std::min<int64_t>(8, blocks128 / 512));
+      dim3 grid((a->q_len + 128 * nsl - 1) / (128 * nsl), a->heads, a->batch);
+      attn_fwd_short_kernel<HD><<<grid, 256, 0, st>>>(*a, nsl);
+      return;
+    }
+  }
   const int nw = a->q_len >= 128 ? 4 : (a->q_len + 31) / 32;
   dim3 grid((a->q_len + 32 * nw - 1) / (32 * nw), a->heads, a->batch);
   attn_fwd_kernel<T, HD><<<grid, 64 * nw, 0, st>>>(*a);
@@ -1120,6 +1302,10 @@ extern "C" int mtts_attention_bwd(const MttsAttnBwdArgs* a, void* stream) {
   p.part = pl.part_bytes ? (float*)a->workspace : nullptr;
   p.dq_acc = pl.dq_bytes ? (float*)((char*)a->workspace + pl.part_bytes) : nullptr;
   p.delta = pl.delta_bytes ? (float*)((char*)a->workspace + pl.part_bytes + pl.dq_bytes) : nullptr;
+  {
+    const int es = f.dtype == MTTS_BF16 ? 2 : 4;
+    p.dq_vec = ((uintptr_t)a->dq % 16 == 0) && (a->dq_bs * es) % 16 == 0 && (a->dq_ls * es) % 16 == 0;
+  }
   if (f.dtype == MTTS_BF16)
     dispatch_bwd<bf16_t>(p, pl.split, st);
   else

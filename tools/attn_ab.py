@@ -35,6 +35,16 @@ for name, (B, T, S) in {"C2": (8, 2048, 128), "C5": (4, 5120, 5248)}.items():
     fl = 4 * B * T * S * d
     tf = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
     print(f"{name} fwd {tf * 1e3:.1f} us {fl / tf / 1e9:.0f} TF/s", flush=True)
+    if name == "C2":
+        os.environ["MTTS_ATTN_FWD_SHORT"] = "0"
+        tf0 = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
+        os.environ.pop("MTTS_ATTN_FWD_SHORT")
+        o0, l0 = A.attention_fwd(q, k, v, H, kpm, want_lse=True)
+        os.environ["MTTS_ATTN_FWD_SHORT"] = "0"
+        o1, l1 = A.attention_fwd(q, k, v, H, kpm, want_lse=True)
+        os.environ.pop("MTTS_ATTN_FWD_SHORT")
+        print(f"{name} fwd generic kernel {tf0 * 1e3:.1f} us; short vs generic max|diff| out "
+              f"{(o0.float() - o1.float()).abs().max().item():.2e} lse {(l0 - l1).abs().max().item():.2e}", flush=True)
     for ch in ([None, "8", "16", "32"] if name == "C2" else [None]):
         if ch:
             os.environ["MTTS_ATTN_CHUNKS"] = ch
