@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 5
+#define MTTS_ABI_VERSION 6
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -569,6 +569,35 @@ typedef struct {
 
 int64_t mtts_gemm_workspace(const MttsGemmArgs* a);
 int mtts_gemm(const MttsGemmArgs* a, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Skinny bf16 GEMMs of the Mamba mixer's inner projections (csrc/skinny.hip).
+ * Replace the x_proj / dt_proj matmuls of [upstream] mamba_inner_fn
+ * (x_dbl = F.linear(u, x_proj.weight); delta = dt_proj.weight @ dt^T, and
+ * their data gradients), reached from the reference at mamba_decoder.py:61
+ * through Mamba(d_model) (:29).
+ *   C[m,n] = A[m,k] . B[n,k]^T + beta * C     (A, B bf16, k-contiguous rows)
+ *   mode SKINNY_N  : n <= 128 (one workgroup per row block, K split over its
+ *                    4 waves, fixed-order sum)
+ *   mode SMALL_K   : k <= 128 (64 x 256 output tiles)
+ * k % 32 == 0, n % 4 == 0; A / B 16-byte aligned, lda / ldb multiples of 8;
+ * C bf16 (8-byte aligned) or fp32 (16-byte aligned), ldc % 4 == 0;
+ * beta 0 or 1 (accumulate into C, e.g. du += d(x_dbl) W_x).
+ * ------------------------------------------------------------------------ */
+#define MTTS_SKINNY_N 0
+#define MTTS_SKINNY_SMALL_K 1
+typedef struct {
+  int mode;                  /* MTTS_SKINNY_N / MTTS_SKINNY_SMALL_K */
+  int m, n, k;
+  int c_dtype;               /* MTTS_F32 / MTTS_BF16 */
+  float beta;
+  int64_t lda, ldb, ldc;
+  const void* a;
+  const void* b;
+  void* c;
+} MttsSkinnyArgs;
+
+int mtts_gemm_skinny(const MttsSkinnyArgs* a, void* stream);
 
 #ifdef __cplusplus
 }

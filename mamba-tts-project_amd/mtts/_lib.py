@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -88,6 +88,11 @@ class GemmArgs(C.Structure):
                 ("a", vp), ("b", vp), ("c", vp), ("bias", vp), ("aux", vp), ("workspace", vp), ("beta", f32)]
 
 
+class SkinnyArgs(C.Structure):
+    _fields_ = [("mode", i32), ("m", i32), ("n", i32), ("k", i32), ("c_dtype", i32), ("beta", f32),
+                ("lda", i64), ("ldb", i64), ("ldc", i64), ("a", vp), ("b", vp), ("c", vp)]
+
+
 class LNArgs(C.Structure):
     _fields_ = [("rows", i32), ("cols", i32), ("dtype", i32), ("rows_per_group", i32), ("eps", f32),
                 ("x_rs", i64), ("res_rs", i64), ("xsum_rs", i64), ("y_rs", i64), ("gb_rs", i64),
@@ -146,6 +151,7 @@ _SIGS = {
     "mtts_pack_rows_weight": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_gemm_workspace": ([C.POINTER(GemmArgs)], i64),
     "mtts_gemm": ([C.POINTER(GemmArgs), vp], i32),
+    "mtts_gemm_skinny": ([C.POINTER(SkinnyArgs), vp], i32),
     "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),
     "mtts_layernorm_bwd": ([C.POINTER(LNBwdArgs), vp], i32),
     "mtts_colsum_workspace": ([i32, i32, i32], i64),

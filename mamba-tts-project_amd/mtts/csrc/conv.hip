@@ -10,6 +10,8 @@
 // store is a coalesced 16-byte access.  HBM-bound.
 #include "common.h"
 
+#include <type_traits>
+
 namespace mtts {
 
 constexpr int kK = 4;
@@ -44,6 +46,9 @@ __device__ __forceinline__ void stv(T* p, const float (&v)[CPT]) {
       w = make_uint4(q[0], q[1], q[2], q[3]);
     }
     *reinterpret_cast<uint4*>(p) = w;
+  } else if constexpr (sizeof(T) == 2 && CPT == 4) {
+    *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                              (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
   } else {
 #pragma unroll
     for (int q = 0; q < CPT; ++q) stf(p + q, v[q]);
@@ -207,6 +212,209 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(const MttsConvBwdArgs a, 
   }
 }
 
+// ---------------------------------------------------------------- tiled forms
+// The kernels above walk a 32-step tile with one load per step: each load is
+// issued behind the previous step's store (which may alias it), so a thread
+// has one load in flight and the kernel runs latency-bound (C2: fwd 43 us,
+// bwd 84 us per call for 67 MB per operand).  The tiled forms issue ALL of a
+// tile's 16-byte row loads before any arithmetic or store (x rows t0-3 ..
+// t0+TT-1 for the forward; x rows t0-3 .. t0+TT+2 and dout rows t0 .. t0+TT+2
+// for the backward), so a wave keeps TT+3 (2TT+9) loads in flight.
+//
+// Backward block = 8 waves = 8 consecutive 8-step tiles of the same 64 x CPT
+// channels: the dw / db partials of the 8 tiles are summed through LDS, so
+// the partial slab has one row per 64 steps (C2: 10 MB instead of 21).
+
+template <typename T, int CPT>
+using rawv_t = typename std::conditional<sizeof(T) * CPT == 16, uint4, uint2>::type;
+
+template <typename T, int CPT>
+__device__ __forceinline__ void unpack16(const uint2& v, float (&o)[CPT]) {   // 4 bf16 channels
+  static_assert(sizeof(T) == 2 && CPT == 4, "8-byte rows: bf16 x 4");
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+template <typename T, int CPT>
+__device__ __forceinline__ void unpack16(const uint4& v, float (&o)[CPT]) {
+  if constexpr (sizeof(T) == 4) {
+    o[0] = __uint_as_float(v.x); o[1] = __uint_as_float(v.y); o[2] = __uint_as_float(v.z); o[3] = __uint_as_float(v.w);
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { o[2 * q] = __uint_as_float(w[q] << 16); o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+  }
+}
+
+// x value at t < 0: the conv_state_in history column (or 0)
+template <int CPT>
+__device__ __forceinline__ void hist_x(const MttsConvFwdArgs& a, int b, int c0, int t, float (&o)[CPT]) {
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) o[q] = a.conv_state_in ? a.conv_state_in[((int64_t)b * a.dim + c0 + q) * kK + (kK + t)] : 0.f;
+}
+
+template <typename T, int CPT, int TT>
+__global__ __launch_bounds__(256) void conv_fwd_tile_kernel(const MttsConvFwdArgs a) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * CPT;
+  if (c0 >= a.dim) return;
+  const int b = blockIdx.z;
+  const int t0 = blockIdx.y * TT;
+  const int L = a.seqlen;
+  const T* xb = (const T*)a.x + (int64_t)b * a.x_bs + c0;
+  uint4 raw[TT + 3];
+#pragma unroll
+  for (int i = 0; i < TT + 3; ++i) {   // rows outside [0, L) load a valid row, replaced below / never stored
+    const int t = min(max(t0 - 3 + i, 0), L - 1);
+    raw[i] = *reinterpret_cast<const uint4*>(xb + (int64_t)t * a.x_ls);
+  }
+  float w[kK][CPT], bias[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const float4 wq = *reinterpret_cast<const float4*>(a.w + (c0 + q) * kK);
+    w[0][q] = wq.x; w[1][q] = wq.y; w[2][q] = wq.z; w[3][q] = wq.w;
+    bias[q] = a.bias ? a.bias[c0 + q] : 0.f;
+  }
+  float x0[CPT], x1[CPT], x2[CPT];
+  if (t0 == 0) {
+    hist_x<CPT>(a, b, c0, -3, x0);
+    hist_x<CPT>(a, b, c0, -2, x1);
+    hist_x<CPT>(a, b, c0, -1, x2);
+  } else {
+    unpack16<T, CPT>(raw[0], x0);
+    unpack16<T, CPT>(raw[1], x1);
+    unpack16<T, CPT>(raw[2], x2);
+  }
+  T* out = (T*)a.out + (int64_t)b * a.out_bs + c0;
+#pragma unroll
+  for (int s = 0; s < TT; ++s) {
+    float x3[CPT], o[CPT];
+    unpack16<T, CPT>(raw[s + 3], x3);
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      const float v = fmaf(w[0][q], x0[q], fmaf(w[1][q], x1[q], fmaf(w[2][q], x2[q], fmaf(w[3][q], x3[q], bias[q]))));
+      o[q] = a.silu ? silu_f(v) : v;
+      x0[q] = x1[q]; x1[q] = x2[q]; x2[q] = x3[q];
+    }
+    if (t0 + s < L) stv<T, CPT>(out + (int64_t)(t0 + s) * a.out_ls, o);
+  }
+}
+
+template <typename T, int CPT, int TT>
+__global__ __launch_bounds__(512) void conv_bwd_tile_kernel(const MttsConvBwdArgs a, float* __restrict__ part) {
+  const MttsConvFwdArgs& f = a.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * CPT;
+  const bool cok = c0 < f.dim;
+  const int cc = cok ? c0 : 0;       // lanes past dim run on channel 0 and store nothing (no early exit: LDS sum below)
+  const int b = blockIdx.z;
+  const int t0 = (blockIdx.y * 8 + wave) * TT;
+  const int L = f.seqlen;
+  const T* xb = (const T*)f.x + (int64_t)b * f.x_bs + cc;
+  const T* gb = (const T*)a.dout + (int64_t)b * a.dout_bs + cc;
+  // x rows t0-3 .. t0+TT+2, dout rows t0 .. t0+TT+2 (g beyond L is 0)
+  using RV = rawv_t<T, CPT>;
+  RV rx[TT + 6], rg[TT + 3];
+#pragma unroll
+  for (int i = 0; i < TT + 6; ++i) {
+    const int t = min(max(t0 - 3 + i, 0), L - 1);
+    rx[i] = *reinterpret_cast<const RV*>(xb + (int64_t)t * f.x_ls);
+  }
+#pragma unroll
+  for (int i = 0; i < TT + 3; ++i) {
+    const int t = min(t0 + i, L - 1);
+    rg[i] = *reinterpret_cast<const RV*>(gb + (int64_t)t * a.dout_ls);
+  }
+  float w[kK][CPT], bias[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const float4 wq = *reinterpret_cast<const float4*>(f.w + (cc + q) * kK);
+    w[0][q] = wq.x; w[1][q] = wq.y; w[2][q] = wq.z; w[3][q] = wq.w;
+    bias[q] = f.bias ? f.bias[cc + q] : 0.f;
+  }
+  float x0[CPT], x1[CPT], x2[CPT];
+  if (t0 == 0) {
+    hist_x<CPT>(f, b, cc, -3, x0);
+    hist_x<CPT>(f, b, cc, -2, x1);
+    hist_x<CPT>(f, b, cc, -1, x2);
+  } else {
+    unpack16<T, CPT>(rx[0], x0);
+    unpack16<T, CPT>(rx[1], x1);
+    unpack16<T, CPT>(rx[2], x2);
+  }
+  float g0[CPT], g1[CPT], g2[CPT], dw[kK][CPT], db[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    g0[q] = g1[q] = g2[q] = 0.f;
+    db[q] = 0.f;
+#pragma unroll
+    for (int k = 0; k < kK; ++k) dw[k][q] = 0.f;
+  }
+  T* dx = (T*)a.dx + (int64_t)b * a.dx_bs + cc;
+  // step s (time t0 + s): g[t] = dout[t] * silu'(pre[t]) for t < L, else 0;
+  // dx[t-3] = w3 g[t-3] + w2 g[t-2] + w1 g[t-1] + w0 g[t] for t-3 in the tile
+#pragma unroll
+  for (int s = 0; s < TT + 3; ++s) {
+    const int t = t0 + s;
+    const bool live = t < L;
+    const bool own = s < TT && live;
+    float x3[CPT], go[CPT], g[CPT];
+    unpack16<T, CPT>(rx[s + 3], x3);
+    unpack16<T, CPT>(rg[s], go);
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      const float v = fmaf(w[0][q], x0[q], fmaf(w[1][q], x1[q], fmaf(w[2][q], x2[q], fmaf(w[3][q], x3[q], bias[q]))));
+      float gg = live ? go[q] : 0.f;
+      if (f.silu) {
+        const float sg = sigmoid_f(v);
+        gg *= sg * (1.f + v * (1.f - sg));
+      }
+      g[q] = gg;
+      if (own) {
+        db[q] += gg;
+        dw[0][q] = fmaf(gg, x0[q], dw[0][q]);
+        dw[1][q] = fmaf(gg, x1[q], dw[1][q]);
+        dw[2][q] = fmaf(gg, x2[q], dw[2][q]);
+        dw[3][q] = fmaf(gg, x3[q], dw[3][q]);
+      }
+    }
+    if (s >= 3 && cok && t - 3 < L) {
+      float o[CPT];
+#pragma unroll
+      for (int q = 0; q < CPT; ++q) o[q] = fmaf(w[3][q], g0[q], fmaf(w[2][q], g1[q], fmaf(w[1][q], g2[q], w[0][q] * g[q])));
+      stv<T, CPT>(dx + (int64_t)(t - 3) * a.dx_ls, o);
+    }
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      x0[q] = x1[q]; x1[q] = x2[q]; x2[q] = x3[q];
+      g0[q] = g1[q]; g1[q] = g2[q]; g2[q] = g[q];
+    }
+  }
+  // sum the 8 waves' (time tiles') partials: (K + 1) * CPT values per lane
+  constexpr int NV = (kK + 1) * CPT;
+  __shared__ float red[7][NV][64];
+  if (wave > 0) {
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+#pragma unroll
+      for (int k = 0; k < kK; ++k) red[wave - 1][q * (kK + 1) + k][lane] = dw[k][q];
+      red[wave - 1][q * (kK + 1) + kK][lane] = db[q];
+    }
+  }
+  __syncthreads();
+  if (wave == 0 && cok) {
+    float* pp = part + ((int64_t)(b * gridDim.y + blockIdx.y) * f.dim + c0) * (kK + 1);
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+#pragma unroll
+      for (int k = 0; k <= kK; ++k) {
+        float v = k < kK ? dw[k][q] : db[q];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) v += red[j][q * (kK + 1) + k][lane];
+        pp[q * (kK + 1) + k] = v;
+      }
+    }
+  }
+}
+
 __global__ void conv_bwd_split(const float* __restrict__ sums, int dim, float* dw, float* db) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= dim * (kK + 1)) return;
@@ -234,8 +442,20 @@ static int check_conv(const MttsConvFwdArgs* a) {
   return MTTS_OK;
 }
 
+constexpr int kFwdTT = 16;   // tiled forward: steps per thread
+constexpr int kBwdTT = 8;    // tiled backward: steps per wave (8 waves = 64 steps per block)
+
+static bool tiled_off() { return getenv("MTTS_CONV_UNTILED") != nullptr; }
+
 template <typename T, int CPT>
 static void launch_fwd(const MttsConvFwdArgs* a, hipStream_t st) {
+  if constexpr (sizeof(T) * CPT == 16) {
+   if (!tiled_off()) {
+    dim3 grid((a->dim / CPT + 255) / 256, (a->seqlen + kFwdTT - 1) / kFwdTT, a->batch);
+    hipLaunchKernelGGL((conv_fwd_tile_kernel<T, CPT, kFwdTT>), grid, dim3(256), 0, st, *a);
+    return;
+   }
+  }
   dim3 grid((a->dim / CPT + 255) / 256, (a->seqlen + kTT - 1) / kTT, a->batch);
   hipLaunchKernelGGL((conv_fwd_kernel<T, CPT>), grid, dim3(256), 0, st, *a);
 }
@@ -250,10 +470,10 @@ extern "C" int mtts_causal_conv1d_fwd(const MttsConvFwdArgs* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (a->seqlen > 0) {
     if (a->dtype == MTTS_F32) {
-      if (vec_ok<float>(a, 4)) launch_fwd<float, 4>(a, st);
+      if (vec_ok<float>(a, 4) && (uintptr_t)a->w % 16 == 0) launch_fwd<float, 4>(a, st);
       else launch_fwd<float, 1>(a, st);
     } else {
-      if (vec_ok<bf16_t>(a, 8)) launch_fwd<bf16_t, 8>(a, st);
+      if (vec_ok<bf16_t>(a, 8) && (uintptr_t)a->w % 16 == 0) launch_fwd<bf16_t, 8>(a, st);
       else launch_fwd<bf16_t, 1>(a, st);
     }
     MTTS_LAUNCH_CHECK("causal_conv1d_fwd");
@@ -273,10 +493,19 @@ extern "C" int64_t mtts_causal_conv1d_bwd_workspace(int batch, int dim, int seql
   return ((int64_t)batch * ntile + 1) * dim * (kK + 1) * 4 + 256;
 }
 
+// returns the number of partial rows written
 template <typename T, int CPT>
-static void launch_bwd(const MttsConvBwdArgs* a, hipStream_t st, float* part) {
+static int launch_bwd(const MttsConvBwdArgs* a, hipStream_t st, float* part, bool tiled) {
+  if constexpr (sizeof(T) * CPT >= 8) {
+   if (tiled) {
+    dim3 grid((a->f.dim / CPT + 63) / 64, (a->f.seqlen + 8 * kBwdTT - 1) / (8 * kBwdTT), a->f.batch);
+    hipLaunchKernelGGL((conv_bwd_tile_kernel<T, CPT, kBwdTT>), grid, dim3(512), 0, st, *a, part);
+    return (int)(grid.y * grid.z);
+   }
+  }
   dim3 grid((a->f.dim / CPT + 255) / 256, (a->f.seqlen + kTT - 1) / kTT, a->f.batch);
   hipLaunchKernelGGL((conv_bwd_kernel<T, CPT>), grid, dim3(256), 0, st, *a, part);
+  return (int)(grid.y * grid.z);
 }
 
 extern "C" int mtts_causal_conv1d_bwd(const MttsConvBwdArgs* a, void* stream) {
@@ -294,15 +523,17 @@ extern "C" int mtts_causal_conv1d_bwd(const MttsConvBwdArgs* a, void* stream) {
                    (uintptr_t)a->dx % 16 == 0 && (f.x_ls * es) % 16 == 0 && (f.x_bs * es) % 16 == 0 &&
                    (a->dout_ls * es) % 16 == 0 && (a->dout_bs * es) % 16 == 0 && (a->dx_ls * es) % 16 == 0 &&
                    (a->dx_bs * es) % 16 == 0;
+  const bool tiled = vec && (uintptr_t)f.w % 16 == 0 && !tiled_off();
+  int nparts;
   if (f.dtype == MTTS_F32) {
-    if (vec) launch_bwd<float, 4>(a, st, part);
-    else launch_bwd<float, 1>(a, st, part);
+    if (vec) nparts = launch_bwd<float, 4>(a, st, part, tiled);
+    else nparts = launch_bwd<float, 1>(a, st, part, false);
   } else {
-    if (vec) launch_bwd<bf16_t, 8>(a, st, part);
-    else launch_bwd<bf16_t, 1>(a, st, part);
+    if (tiled) nparts = launch_bwd<bf16_t, 4>(a, st, part, true);   // 8-byte rows: half the live registers
+    else if (vec) nparts = launch_bwd<bf16_t, 8>(a, st, part, false);
+    else nparts = launch_bwd<bf16_t, 1>(a, st, part, false);
   }
   MTTS_LAUNCH_CHECK("causal_conv1d_bwd");
-  const int nparts = f.batch * ((f.seqlen + kTT - 1) / kTT);
   float* sums = part + (int64_t)nparts * f.dim * (kK + 1);
   colsum(part, nparts, nparts, (int64_t)f.dim * (kK + 1), f.dim * (kK + 1), sums, 0, st);
   hipLaunchKernelGGL(conv_bwd_split, dim3((f.dim * (kK + 1) + 255) / 256), dim3(256), 0, st, sums, f.dim, a->dw,

@@ -111,3 +111,51 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, beta: floa
         args.workspace = ws.data_ptr()
     L.call("mtts_gemm", args)
     return out
+
+
+# ------------------------------------------------------------------ skinny GEMMs (csrc/skinny.hip)
+SKINNY_N, SKINNY_SMALL_K = 0, 1
+SKINNY = True   # routing switch (in-process A/B: tools/skinny_ab.py)
+SKINNY_TN = False  # x_proj / dt_proj weight gradients on the TN kernel (35.5 vs 33.7 us bmm split: off)
+SKINNY_XPROJ = False   # x_proj forward on SKINNY_N (25 vs 21 us hipBLASLt: off)
+
+
+def _skinny_operand(t):
+    return (t.dim() == 2 and t.dtype == torch.bfloat16 and t.is_cuda and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.data_ptr() % 16 == 0)
+
+
+def skinny_ok(a: torch.Tensor, b: torch.Tensor, out_dtype=torch.bfloat16, out: torch.Tensor = None) -> bool:
+    """a (m, k) . b (n, k)^T on csrc/skinny.hip: bf16 k-contiguous operands,
+    k % 32 == 0, n % 4 == 0, and either n <= 128 or k <= 128."""
+    if not (SKINNY and _skinny_operand(a) and _skinny_operand(b) and a.shape[1] == b.shape[1]):
+        return False
+    m, k = a.shape
+    n = b.shape[0]
+    if m == 0 or k % 32 or n % 4 or not (n <= 128 or k <= 128):
+        return False
+    if out is not None:
+        es = 4 if out.dtype == torch.float32 else 2
+        if (out.dtype not in (torch.float32, torch.bfloat16) or out.stride(1) != 1 or out.stride(0) % 4
+                or out.data_ptr() % (4 * es) or tuple(out.shape) != (m, n)):
+            return False
+    return out_dtype in (torch.float32, torch.bfloat16)
+
+
+def mm_skinny(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, beta: float = 0.0,
+              out_dtype=torch.bfloat16) -> torch.Tensor:
+    """C[m, n] = a[m, k] . b[n, k]^T (+ beta C) with fp32 accumulation; the
+    SKINNY_N kernel for n <= 128, else SMALL_K (k <= 128)."""
+    m, k = a.shape
+    n = b.shape[0]
+    if out is None:
+        out = torch.empty(m, n, device=a.device, dtype=out_dtype)
+    args = L.SkinnyArgs()
+    args.mode = SKINNY_N if n <= 128 else SKINNY_SMALL_K
+    args.m, args.n, args.k = m, n, k
+    args.c_dtype = L.dtype_code(out)
+    args.beta = beta
+    args.lda, args.ldb, args.ldc = a.stride(0), b.stride(0), out.stride(0)
+    args.a, args.b, args.c = a.data_ptr(), b.data_ptr(), out.data_ptr()
+    L.call("mtts_gemm_skinny", args)
+    return out

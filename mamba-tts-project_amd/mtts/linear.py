@@ -34,7 +34,7 @@ TRANSPOSE_MIN = 512   # weights with both dims >= this also get a W^T copy
 
 
 def _want_t(p):
-    return p.dim() == 2 and min(p.shape) >= TRANSPOSE_MIN
+    return p.dim() == 2 and (min(p.shape) >= TRANSPOSE_MIN or getattr(p, "_mtts_want_t", False))
 
 
 def _cast_multi_bf16(params):
@@ -186,7 +186,9 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4, out: torch.Tensor 
     M = dy.shape[0]
     if dy.dtype == torch.float32:
         return torch.mm(dy.t(), x, out=out) if out is not None else dy.t() @ x
-    if (dy.shape[1] >= HIP_WGRAD_MIN and x.shape[1] >= HIP_WGRAD_MIN and G.tn_ok(dy, x)
+    big = dy.shape[1] >= HIP_WGRAD_MIN and x.shape[1] >= HIP_WGRAD_MIN
+    skinny = G.SKINNY_TN and min(dy.shape[1], x.shape[1]) >= 64 and max(dy.shape[1], x.shape[1]) >= HIP_WGRAD_MIN
+    if ((big or skinny) and G.tn_ok(dy, x)
             and (out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0))):
         return G.mm_tn(dy, x, out=out)
     if splits > 1 and M % splits == 0 and M >= 2048:

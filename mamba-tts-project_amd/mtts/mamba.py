@@ -29,8 +29,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import gemm as G
 from . import ops
-from .linear import cast_scope, cast_weight, linear, wgrad
+from .linear import cast_scope, cast_weight, cast_weight_t, linear, wgrad
 
 
 class MambaInnerFn(torch.autograd.Function):
@@ -45,9 +46,14 @@ class MambaInnerFn(torch.autograd.Function):
         Wx, Wdt = cast_weight(W_x, cd), cast_weight(W_dt, cd)
         x, z = xz[..., :di], xz[..., di:]
         u, conv_state = ops.conv_fwd(x, conv_w, conv_b, True, state_in=conv_state_in, want_state=True)
-        x_dbl = u @ Wx.t()
+        u2 = u.view(-1, di)
+        # x_proj stays on hipBLASLt (21 us vs 25 for SKINNY_N at C2, tools/skinny_ab.py);
+        # dt_proj on the SMALL_K MFMA kernel (csrc/skinny.hip) when the shapes allow
+        x_dbl = (G.mm_skinny(u2, Wx) if G.SKINNY_XPROJ and G.skinny_ok(u2, Wx) else u2 @ Wx.t()).view(
+            *u.shape[:-1], r + 2 * N)
         dt, Bm, Cm = x_dbl[..., :r], x_dbl[..., r:r + N], x_dbl[..., r + N:]
-        delta = dt @ Wdt.t()
+        dt2 = x_dbl.view(-1, r + 2 * N)[:, :r]
+        delta = (G.mm_skinny(dt2, Wdt) if G.skinny_ok(dt2, Wdt) else dt2 @ Wdt.t()).view(*u.shape[:-1], di)
         A = -torch.exp(A_log.float())
         need = any(ctx.needs_input_grad)
         y, last, ckpt = ops.scan_fwd(u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, want_last=True, want_ckpt=need)
@@ -78,14 +84,24 @@ class MambaInnerFn(torch.autograd.Function):
         du, ddelta, _, _, _, dA, dD, dbias, dh0 = ops.scan_bwd(
             u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, ckpt, dy,
             dz=dxz[..., di:], dB=dx_dbl[..., r:r + N], dC=dx_dbl[..., r + N:], need_dh0=need_dh0)
-        # dt_proj: delta = dt @ W_dt^T
+        # dt_proj: delta = dt @ W_dt^T  ->  d(dt) = d(delta) W_dt (fp32, into d(x_dbl)), dW_dt
         dd2 = ddelta.reshape(-1, di)
-        dx_dbl[..., :r] = (ddelta @ Wdt).float()
-        dW_dt = wgrad(dd2, dt.reshape(-1, r))
-        # x_proj: x_dbl = u @ W_x^T
-        gx = dx_dbl.to(cd)
-        du.view(-1, di).addmm_(gx.view(-1, r + 2 * N), Wx)   # du += d(x_dbl) W_x, accumulated by the GEMM
-        dW_x = wgrad(gx.reshape(-1, r + 2 * N), u.reshape(-1, di))
+        dxd2 = dx_dbl.view(-1, r + 2 * N)
+        WdtT = cast_weight_t(W_dt, cd) if cd == torch.bfloat16 else None   # (r, di): k-contiguous
+        if WdtT is not None and G.skinny_ok(dd2, WdtT, out_dtype=torch.float32, out=dxd2[:, :r]):
+            G.mm_skinny(dd2, WdtT, out=dxd2[:, :r])
+        else:
+            dx_dbl[..., :r] = (ddelta @ Wdt).float()
+        dW_dt = wgrad(dd2, x_dbl.view(-1, r + 2 * N)[:, :r])
+        # x_proj: x_dbl = u @ W_x^T  ->  du += d(x_dbl) W_x (accumulated by the GEMM), dW_x
+        gx = dx_dbl.to(cd).view(-1, r + 2 * N)
+        du2 = du.view(-1, di)
+        WxT = cast_weight_t(W_x, cd) if cd == torch.bfloat16 else None     # (di, r + 2N): k-contiguous
+        if WxT is not None and G.skinny_ok(gx, WxT, out=du2):
+            G.mm_skinny(gx, WxT, out=du2, beta=1.0)
+        else:
+            du2.addmm_(gx, Wx)
+        dW_x = wgrad(gx, u.reshape(-1, di))
         # the conv's left history (a prefilled conv_state) enters the
         # recomputed pre-activations and the weight gradient
         _, dw, db = ops.conv_bwd(x, conv_w, conv_b, du, True, dx=dxz[..., :di], state_in=conv_state_in)
@@ -138,6 +154,10 @@ class Mamba(nn.Module):
         self.conv1d = nn.Conv1d(di, di, kernel_size=d_conv, groups=di, padding=d_conv - 1, bias=conv_bias, **fk)
         self.x_proj = nn.Linear(di, self.dt_rank + d_state * 2, bias=False, **fk)
         self.dt_proj = nn.Linear(self.dt_rank, di, bias=True, **fk)
+        # the per-step weight cast also writes W^T for these two (their data
+        # gradients run as d(.) . (W^T)^T on the skinny kernels)
+        self.x_proj.weight._mtts_want_t = True
+        self.dt_proj.weight._mtts_want_t = True
         dt_init_std = self.dt_rank ** -0.5 * dt_scale
         with torch.no_grad():
             if dt_init == "constant":

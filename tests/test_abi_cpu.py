@@ -35,7 +35,7 @@ STRUCTS = {
     "MttsConvBwdArgs": "ConvBwdArgs", "MttsConvUpdateArgs": "ConvUpdateArgs",
     "MttsStateUpdateArgs": "StateUpdateArgs", "MttsLNArgs": "LNArgs", "MttsLNBwdArgs": "LNBwdArgs",
     "MttsAttnFwdArgs": "AttnFwdArgs", "MttsAttnBwdArgs": "AttnBwdArgs", "MttsCastDesc": "CastDesc",
-    "MttsAdamTensor": "AdamTensor", "MttsRowsArgs": "RowsArgs", "MttsGemmArgs": "GemmArgs",
+    "MttsAdamTensor": "AdamTensor", "MttsRowsArgs": "RowsArgs", "MttsGemmArgs": "GemmArgs", "MttsSkinnyArgs": "SkinnyArgs",
 }
 
 

@@ -186,3 +186,74 @@ def test_tn_every_kernel_many_items(gemm_mode, m, n, k, splits):
     dy, x = rnd(k, m), rnd(k, n)
     out = G.mm_tn(dy, x, splits=splits)
     assert rel(out, dy.float().t() @ x.float()) < 1e-5
+
+
+# ---------------------------------------------------------------- skinny GEMMs (csrc/skinny.hip)
+@pytest.mark.parametrize("m,n,k", [(16384, 96, 2048), (16384, 64, 2048), (1000, 96, 2048), (37, 36, 128),
+                                   (130, 128, 96), (64, 4, 32), (513, 100, 4096)])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_skinny_n(m, n, k, out_dtype):
+    """SKINNY_N (n <= 128: x_proj forward, dt_proj data gradient) vs the fp32
+    product of the same bf16 operands; ragged m and n, K split over 4 waves."""
+    torch.manual_seed(m + n + k)
+    a, b = rnd(m, k), rnd(n, k)
+    assert G.skinny_ok(a, b)
+    out = G.mm_skinny(a, b, out_dtype=out_dtype)
+    ref = a.float() @ b.float().t()
+    assert rel(out, ref) < (1e-2 if out_dtype == torch.bfloat16 else 1e-5)
+
+
+@pytest.mark.parametrize("m,n,k", [(16384, 2048, 64), (16384, 2048, 96), (1000, 520, 64), (77, 256, 128),
+                                   (64, 200, 32)])
+def test_skinny_small_k(m, n, k):
+    """SMALL_K (k <= 128: dt_proj forward) vs fp32 of the same operands."""
+    torch.manual_seed(m + n + k + 1)
+    a, b = rnd(m, k), rnd(n, k)
+    out = G.mm_skinny(a, b)
+    assert rel(out, a.float() @ b.float().t()) < 1e-2
+
+
+def test_skinny_strided_views_and_accumulate():
+    """The decoder's operand layouts: dt = x_dbl[:, :64] (row stride 96) for
+    the dt_proj forward; d(dt) written as fp32 into the d(x_dbl)[:, :64] slice;
+    du += d(x_dbl) W_x accumulated in place (beta = 1, bf16 du) -- the rest of
+    each row untouched."""
+    torch.manual_seed(7)
+    m, di, r = 2048, 2048, 64
+    x_dbl = rnd(m, r + 32)
+    wdt = rnd(di, r)
+    delta = G.mm_skinny(x_dbl[:, :r], wdt)
+    assert rel(delta, x_dbl[:, :r].float() @ wdt.float().t()) < 1e-2
+    dd = rnd(m, di)
+    dx = torch.full((m, r + 32), 7.0, device=dev)
+    wdt_t = wdt.t().contiguous()
+    G.mm_skinny(dd, wdt_t, out=dx[:, :r])
+    assert rel(dx[:, :r], dd.float() @ wdt.float()) < 1e-5
+    assert (dx[:, r:] == 7.0).all()
+    gx = rnd(m, r + 32)
+    wx_t = rnd(di, r + 32)
+    du = rnd(m, di)
+    ref = (du.float() + gx.float() @ wx_t.float().t())
+    G.mm_skinny(gx, wx_t, out=du, beta=1.0)
+    assert rel(du, ref) < 1e-2
+
+
+def test_skinny_rejects_bad_shapes():
+    a, b = rnd(64, 48), rnd(32, 48)
+    assert not G.skinny_ok(a, b)                     # k % 32
+    a, b = rnd(64, 256), rnd(200, 256)
+    assert not G.skinny_ok(a, b)                     # n > 128 and k > 128
+    with pytest.raises(RuntimeError, match="gemm_skinny"):
+        G.mm_skinny(a, b)
+
+
+@pytest.mark.parametrize("shape", [(96, 2048), (2048, 64)])
+def test_tn_skinny_weight_gradients(shape):
+    """x_proj / dt_proj weight gradients (one output dim 64-96) on the TN
+    kernel, split-K: dW = dy^T x in fp32."""
+    torch.manual_seed(11)
+    M = 16384
+    dy, x = rnd(M, shape[0]), rnd(M, shape[1])
+    out = LIN.wgrad(dy, x)
+    ref = dy.float().t() @ x.float()
+    assert rel(out, ref) < 1e-5

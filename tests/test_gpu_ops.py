@@ -300,6 +300,50 @@ def test_conv1d_shapes_strided_and_prefix_state(shape, dtype):
     close(db, br.grad, rtol=tol, name="db")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 2048, 2048), (1, 71, 256), (3, 130, 64)])
+def test_conv1d_tiled_vs_oracle_with_state(shape, dtype):
+    """Tiled conv kernels (all tile loads in flight; 8-wave backward with an
+    LDS sum of the time tiles' dw/db) on the in_proj layout (x = xz[..., :D],
+    row stride 2D), ragged L, a prefilled conv_state entering the forward AND
+    the backward (pre-activations and dw include the history), vs the float64
+    oracle; the untiled kernels (MTTS_CONV_UNTILED) give the same values."""
+    import os
+    from mtts import ops
+    torch.manual_seed(2)
+    B, L, D = shape
+    xz = torch.randn(B, L, 2 * D, device=DEV).to(dtype)
+    x = xz[..., :D]
+    w = torch.randn(D, 4, device=DEV) * 0.5
+    b = torch.randn(D, device=DEV) * 0.1
+    st = torch.randn(B, D, 4, device=DEV)
+    out, st_out = ops.conv_fwd(x, w, b, True, state_in=st, want_state=True)
+    xr = x.transpose(1, 2).double().cpu().requires_grad_(True)
+    wr, br = w.double().cpu().requires_grad_(True), b.double().cpu().requires_grad_(True)
+    ref, _ = R.causal_conv1d_ref(xr, wr, br, "silu", st.double().cpu())
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    close(out.transpose(1, 2).float(), ref.detach(), rtol=tol, name="fwd vs oracle")
+    go = torch.randn(B, L, D, device=DEV).to(dtype)
+    dxz = torch.zeros_like(xz)
+    _, dw, db = ops.conv_bwd(x, w, b, go, True, dx=dxz[..., :D], state_in=st)
+    (ref * go.transpose(1, 2).double().cpu()).sum().backward()
+    close(dxz[..., :D].transpose(1, 2).float(), xr.grad, rtol=tol, name="dx")
+    assert dxz[..., D:].abs().max().item() == 0.0, "dx wrote outside its half of d(xz)"
+    close(dw, wr.grad, rtol=tol, name="dw")
+    close(db, br.grad, rtol=tol, name="db")
+    os.environ["MTTS_CONV_UNTILED"] = "1"
+    try:
+        out2, _ = ops.conv_fwd(x, w, b, True, state_in=st, want_state=True)
+        dxz2 = torch.zeros_like(xz)
+        _, dw2, db2 = ops.conv_bwd(x, w, b, go, True, dx=dxz2[..., :D], state_in=st)
+    finally:
+        del os.environ["MTTS_CONV_UNTILED"]
+    assert torch.equal(out, out2), "tiled and untiled forward differ"
+    assert torch.equal(dxz, dxz2), "tiled and untiled dx differ"
+    close(dw2, dw, rtol=1e-5, name="dw tiled vs untiled")
+    close(db2, db, rtol=1e-5, name="db tiled vs untiled")
+
+
 def test_state_update_vs_golden(golden):
     from mtts import ops
     g = golden("state_update.npz")

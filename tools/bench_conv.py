@@ -30,7 +30,14 @@ def t(fn, it=20):
     return e0.elapsed_time(e1) / it * 1e3
 
 
-tf = t(lambda: ops.conv_fwd(x, w, bias, True))
-tb = t(lambda: ops.conv_bwd(x, w, bias, du, True, dx=dxz[..., :D]))
 n = B * L * D * 2
-print(f"conv fwd {tf:.1f} us ({2 * n / tf / 1e3:.0f} GB/s)   bwd {tb:.1f} us ({3 * n / tb / 1e3:.0f} GB/s)")
+for rnd in range(2):
+    for mode in ("tiled", "untiled"):
+        if mode == "untiled":
+            os.environ["MTTS_CONV_UNTILED"] = "1"
+        else:
+            os.environ.pop("MTTS_CONV_UNTILED", None)
+        tf = t(lambda: ops.conv_fwd(x, w, bias, True))
+        tb = t(lambda: ops.conv_bwd(x, w, bias, du, True, dx=dxz[..., :D]))
+        print(f"{mode:8s} conv fwd {tf:.1f} us ({2 * n / tf / 1e3:.0f} GB/s)   bwd {tb:.1f} us "
+              f"({3 * n / tb / 1e3:.0f} GB/s)", flush=True)
