@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 6
+#define MTTS_ABI_VERSION 7
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -66,6 +66,9 @@ typedef struct {
   int dtype_io, dtype_bc;
   int delta_softplus;
   int ckpt_chunk;                 /* 16 iff ckpt != NULL (the backward chunk) */
+  int a_is_log;                   /* 1: `A` holds A_log and A = -exp(A_log) is formed in-kernel;
+                                     the backward's dA is then d/dA_log (= dA * A) */
+  int reserved_;
   int64_t u_bs, u_ls;             /* element strides (batch, time)       */
   int64_t delta_bs, delta_ls;
   int64_t z_bs, z_ls;

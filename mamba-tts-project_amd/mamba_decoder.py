@@ -59,10 +59,12 @@ class MambaTTSDecoderLayer(nn.Module):
             x, ff_out, new_state = self.forward_fused(x, None, text_hidden, z_style, text_mask, mamba_state)
         return x + ff_out, new_state                                          # :88-89
 
-    def forward_fused(self, x, pending, text_hidden, z_style, text_mask=None, mamba_state=None, kpm=None):
+    def forward_fused(self, x, pending, text_hidden, z_style, text_mask=None, mamba_state=None, kpm=None, gb=None):
         """Same math as forward(); the input residual `x + pending` and the
         output residual `x + ff_out` are left to the neighbouring fused
-        residual+LayerNorm kernels.  Returns (x, ff_out, new_state)."""
+        residual+LayerNorm kernels.  `gb` (B, 2d): this layer's
+        style_mlp(z_style) when the decoder computed all layers' at once.
+        Returns (x, ff_out, new_state)."""
         T = x.shape[1]
         # 1) (x += pending) ; h = norm_mamba(x) ; Mamba   (mamba_decoder.py:59-64)
         h, xs = ops.layer_norm(x if pending is None else pending, self.norm_mamba.weight, self.norm_mamba.bias,
@@ -80,7 +82,8 @@ class MambaTTSDecoderLayer(nn.Module):
                                       key_padding_mask=key_padding_mask)
 
         # 3) x = x + attn ; h = gamma * norm_ff(x) + beta   (fused, :78-86)
-        gb = self.style_mlp(z_style.to(self.style_mlp[0].weight.dtype))
+        if gb is None:
+            gb = self.style_mlp(z_style.to(self.style_mlp[0].weight.dtype))
         gamma, beta = torch.chunk(gb.to(h.dtype), 2, dim=-1)
         h, x = ops.layer_norm(attn_out, self.norm_ff.weight, self.norm_ff.bias, self.norm_ff.eps, res=x,
                               gamma=gamma, beta=beta, rows_per_group=T)
@@ -163,13 +166,32 @@ class MambaTTSDecoder(nn.Module):
                    l.cross_attn.out_proj.bias, l.ff[0].weight, l.ff[0].bias, l.ff[2].weight, l.ff[2].bias]
         return [w for w in ws if w is not None]
 
+    def _style_all(self, z_style, cd):
+        """Every layer's style_mlp(z_style) = tanh(z W_l^T + b_l) (:52-55, applied
+        at :82-84) as ONE batched GEMM over the stacked layer weights (fp32, the
+        parameters' dtype), cast to the compute dtype once: (n_layers, B, 2d).
+        Autograd splits the stacked gradients back to each layer's parameters.
+        None when the layers' style MLPs differ in shape / dtype."""
+        lins = [l.style_mlp[0] for l in self.layers]
+        w0 = lins[0].weight
+        if (len(lins) < 2 or any(m.weight.shape != w0.shape or m.weight.dtype != w0.dtype or m.bias is None
+                                 for m in lins)):
+            return None
+        W = torch.stack([m.weight for m in lins])                         # (L, 2d, d_style)
+        b = torch.stack([m.bias for m in lins])                           # (L, 2d)
+        z = z_style.to(w0.dtype)
+        gb = torch.tanh(torch.baddbmm(b[:, None, :], z[None].expand(len(lins), -1, -1), W.transpose(1, 2)))
+        return gb.to(cd)
+
     def _run_layers(self, x, text_hidden, z_style, text_mask, states):
         pending = None
         new_states = []
         kpm = None if text_mask is None else ~text_mask                     # :68-70 (sic), once for all layers
+        gbs = self._style_all(z_style, x.dtype) if x.shape[1] > 1 else None
         for i, layer in enumerate(self.layers):
             x, pending, st = layer.forward_fused(x, pending, text_hidden, z_style, text_mask,
-                                                 None if states is None else states[i], kpm=kpm)
+                                                 None if states is None else states[i], kpm=kpm,
+                                                 gb=None if gbs is None else gbs[i])
             new_states.append(st)
         return x, pending, new_states
 

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -25,7 +25,7 @@ i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
 class ScanFwdArgs(C.Structure):
     _fields_ = [("batch", i32), ("dim", i32), ("seqlen", i32), ("dstate", i32),
                 ("dtype_io", i32), ("dtype_bc", i32), ("delta_softplus", i32), ("ckpt_chunk", i32),
-                ("u_bs", i64), ("u_ls", i64), ("delta_bs", i64), ("delta_ls", i64),
+                ("a_is_log", i32), ("reserved_", i32), ("u_bs", i64), ("u_ls", i64), ("delta_bs", i64), ("delta_ls", i64),
                 ("z_bs", i64), ("z_ls", i64), ("out_bs", i64), ("out_ls", i64),
                 ("B_bs", i64), ("B_ls", i64), ("C_bs", i64), ("C_ls", i64),
                 ("u", vp), ("delta", vp), ("A", vp), ("Bm", vp), ("Cm", vp), ("D", vp), ("z", vp),

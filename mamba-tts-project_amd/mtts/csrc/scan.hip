@@ -46,6 +46,14 @@ template <int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
+// A[c, n]: the fp32 tensor itself, or -exp(A_log[c, n]) when the caller
+// passes A_log (a_is_log; the Mamba mixer's parameter, so no per-step
+// exp / neg launches): one accurate expf per value, loaded once per thread
+__device__ __forceinline__ float ld_A(const MttsScanFwdArgs& a, int64_t i) {
+  const float v = a.A[i];
+  return a.a_is_log ? -expf(v) : v;
+}
+
 template <int P, int S>
 __device__ __forceinline__ float group_bcast(float v) {
   if constexpr (P == 1) {
@@ -257,7 +265,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
 
   float A2[NS], h[NS];
 #pragma unroll
-  for (int i = 0; i < NS; ++i) A2[i] = a.A[(int64_t)c * kN + j * NS + i] * kLog2e;
+  for (int i = 0; i < NS; ++i) A2[i] = ld_A(a, (int64_t)c * kN + j * NS + i) * kLog2e;
   const float Dc = a.D ? a.D[c] : 0.f;
   const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
   float S = 0.f;
@@ -537,7 +545,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_wide_kernel(const MttsScan
 
   float A2[NS], h[NS];
 #pragma unroll
-  for (int i = 0; i < NS; ++i) A2[i] = a.A[(int64_t)c * kN + j * NS + i] * kLog2e;
+  for (int i = 0; i < NS; ++i) A2[i] = ld_A(a, (int64_t)c * kN + j * NS + i) * kLog2e;
   const float Dc = a.D ? a.D[c] : 0.f;
   const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
   float S = 0.f;
@@ -898,8 +906,8 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
   f2 A2[NP2], h[NP2];
 #pragma unroll
   for (int p = 0; p < NP2; ++p) {
-    const float* ap = a.A + (int64_t)c * kN + j * NS + 2 * p;
-    A2[p] = f2{ap[0] * kLog2e, ap[1] * kLog2e};
+    const int64_t ai = (int64_t)c * kN + j * NS + 2 * p;
+    A2[p] = f2{ld_A(a, ai) * kLog2e, ld_A(a, ai + 1) * kLog2e};
   }
   const float Dc = a.D ? a.D[c] : 0.f;
   const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
@@ -1266,7 +1274,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   const int st_s = e0 / kN, st_n = e0 % kN;
   float A2[kNSB];
 #pragma unroll
-  for (int i = 0; i < kNSB; ++i) A2[i] = f.A[(int64_t)c * kN + j * kNSB + i] * kLog2e;
+  for (int i = 0; i < kNSB; ++i) A2[i] = ld_A(f, (int64_t)c * kN + j * kNSB + i) * kLog2e;
   const f2 A2v[2] = {f2{A2[0], A2[1]}, f2{A2[2], A2[3]}};
   f2 carry2[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
   const float bias = f.delta_bias ? f.delta_bias[c] : 0.f;
@@ -1466,7 +1474,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   float An[kNSB], A2[kNSB];
 #pragma unroll
   for (int i = 0; i < kNSB; ++i) {
-    An[i] = f.A[(int64_t)c * kN + j * kNSB + i];
+    An[i] = ld_A(f, (int64_t)c * kN + j * kNSB + i);
     A2[i] = An[i] * kLog2e;
   }
   const f2 Anv[2] = {f2{An[0], An[1]}, f2{An[2], An[3]}};
@@ -1779,14 +1787,15 @@ __global__ void scan_bwd_reduce_bc(const float* __restrict__ slab, int batch, in
 }
 
 // dA[c,n], dD[c], ddelta_bias[c] = sum over batch of the per-(b,c) partials
+// (A_log given: dA_log = dA * A, A = -exp(A_log))
 __global__ void scan_bwd_reduce_par(const float* __restrict__ par, int batch, int dim, float* dA, float* dD,
-                                    float* dbias) {
+                                    float* dbias, const float* __restrict__ a_log) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= dim * (kN + 2)) return;
   float s = 0.f;
   for (int b = 0; b < batch; ++b) s += par[(int64_t)b * dim * (kN + 2) + idx];
   const int c = idx / (kN + 2), q = idx % (kN + 2);
-  if (q < kN) dA[c * kN + q] = s;
+  if (q < kN) dA[c * kN + q] = a_log ? s * -expf(a_log[c * kN + q]) : s;
   else if (q == kN) { if (dD) dD[c] = s; }
   else if (dbias) dbias[c] = s;
 }
@@ -1958,8 +1967,8 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
   f2 A2[kN / 2], h[kN / 2];
 #pragma unroll
   for (int p = 0; p < kN / 2; ++p) {
-    const float* ap = a.A + (int64_t)c * kN + 2 * p;
-    A2[p] = f2{ap[0] * kLog2e, ap[1] * kLog2e};
+    const int64_t ai = (int64_t)c * kN + 2 * p;
+    A2[p] = f2{ld_A(a, ai) * kLog2e, ld_A(a, ai + 1) * kLog2e};
     const int64_t o = ((int64_t)b * a.dim + c) * kN + 2 * p;
     h[p] = a.h0 ? f2{a.h0[o], a.h0[o + 1]} : f2{0.f, 0.f};
   }
@@ -2345,7 +2354,7 @@ extern "C" int mtts_selective_scan_bwd(const MttsScanBwdArgs* a, void* stream) {
                      a->dB_bs, a->dB_ls, a->dC, a->dC_bs, a->dC_ls);
   MTTS_LAUNCH_CHECK("selective_scan_bwd_reduce_bc");
   hipLaunchKernelGGL(scan_bwd_reduce_par, dim3((a->f.dim * (kN + 2) + 255) / 256), dim3(256), 0, st, par,
-                     a->f.batch * pl.K, a->f.dim, a->dA, a->dD, a->ddelta_bias);
+                     a->f.batch * pl.K, a->f.dim, a->dA, a->dD, a->ddelta_bias, a->f.a_is_log ? a->f.A : nullptr);
   MTTS_LAUNCH_CHECK("selective_scan_bwd_reduce_par");
   return MTTS_OK;
 }

@@ -54,12 +54,14 @@ class MambaInnerFn(torch.autograd.Function):
         dt, Bm, Cm = x_dbl[..., :r], x_dbl[..., r:r + N], x_dbl[..., r + N:]
         dt2 = x_dbl.view(-1, r + 2 * N)[:, :r]
         delta = (G.mm_skinny(dt2, Wdt) if G.skinny_ok(dt2, Wdt) else dt2 @ Wdt.t()).view(*u.shape[:-1], di)
-        A = -torch.exp(A_log.float())
+        # A = -exp(A_log) is formed inside the scan kernels (a_is_log): no per-layer exp / neg launches
+        A_log32 = A_log.detach().float().contiguous()
         need = any(ctx.needs_input_grad)
-        y, last, ckpt = ops.scan_fwd(u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, want_last=True, want_ckpt=need)
+        y, last, ckpt = ops.scan_fwd(u, delta, A_log32, Bm, Cm, D, z, dt_bias, True, h0, want_last=True,
+                                     want_ckpt=need, a_is_log=True)
         if need:
             ctx.save_for_backward(xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt,
-                                  conv_state_in, h0, A)
+                                  conv_state_in, h0, A_log32)
         ctx.mark_non_differentiable(conv_state, last)
         ctx.set_materialize_grads(False)   # no zero-filled grads for the unused state outputs
         return y, conv_state, last
@@ -67,7 +69,7 @@ class MambaInnerFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dconv, _dlast):
         (xz, conv_w, conv_b, W_x, W_dt, A_log, D, dt_bias, u, x_dbl, delta, ckpt,
-         conv_state_in, h0, A) = ctx.saved_tensors
+         conv_state_in, h0, A_log32) = ctx.saved_tensors
         if dy is None:   # grads are not materialised: y unused downstream
             dy = torch.zeros(xz.shape[:-1] + (xz.shape[-1] // 2,), device=xz.device, dtype=xz.dtype)
         cd = u.dtype
@@ -81,9 +83,9 @@ class MambaInnerFn(torch.autograd.Function):
         dxz = torch.empty_like(xz)
         dx_dbl = torch.empty(Bsz, Ln, r + 2 * N, device=xz.device, dtype=torch.float32)
         need_dh0 = h0 is not None and ctx.needs_input_grad[9]
-        du, ddelta, _, _, _, dA, dD, dbias, dh0 = ops.scan_bwd(
-            u, delta, A, Bm, Cm, D, z, dt_bias, True, h0, ckpt, dy,
-            dz=dxz[..., di:], dB=dx_dbl[..., r:r + N], dC=dx_dbl[..., r + N:], need_dh0=need_dh0)
+        du, ddelta, _, _, _, dA_log, dD, dbias, dh0 = ops.scan_bwd(
+            u, delta, A_log32, Bm, Cm, D, z, dt_bias, True, h0, ckpt, dy,
+            dz=dxz[..., di:], dB=dx_dbl[..., r:r + N], dC=dx_dbl[..., r + N:], need_dh0=need_dh0, a_is_log=True)
         # dt_proj: delta = dt @ W_dt^T  ->  d(dt) = d(delta) W_dt (fp32, into d(x_dbl)), dW_dt
         dd2 = ddelta.reshape(-1, di)
         dxd2 = dx_dbl.view(-1, r + 2 * N)
@@ -108,7 +110,7 @@ class MambaInnerFn(torch.autograd.Function):
         dstate = None
         if conv_state_in is not None and ctx.needs_input_grad[8]:
             dstate = _conv_state_grad(x, conv_w, conv_b, conv_state_in, du)
-        dA_log = (dA * A).to(A_log.dtype)
+        dA_log = dA_log.to(A_log.dtype)
         return (dxz, dw.reshape(conv_w.shape).to(conv_w.dtype), db.to(conv_b.dtype), dW_x.to(W_x.dtype),
                 dW_dt.to(W_dt.dtype), dA_log, dD.to(D.dtype), dbias.to(dt_bias.dtype), dstate,
                 None if dh0 is None else dh0.to(h0.dtype))

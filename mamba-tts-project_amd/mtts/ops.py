@@ -46,7 +46,7 @@ def _bc(t):
 # ---------------------------------------------------------------------------
 # selective scan (channel-last)
 # ---------------------------------------------------------------------------
-def _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, ckpt):
+def _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, ckpt, a_is_log=False):
     Bsz, Ln, Dm = u.shape
     for t in (u, delta, out) + ((z,) if z is not None else ()):
         if t.stride(-1) != 1:
@@ -56,6 +56,7 @@ def _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, c
     a.dtype_io, a.dtype_bc = L.dtype_code(u), L.dtype_code(Bm)
     a.delta_softplus = int(bool(softplus))
     a.ckpt_chunk = SCAN_CKPT if ckpt is not None else 0
+    a.a_is_log = int(bool(a_is_log))
     a.u_bs, a.u_ls = u.stride(0), u.stride(1)
     a.delta_bs, a.delta_ls = delta.stride(0), delta.stride(1)
     if z is not None:
@@ -70,8 +71,9 @@ def _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, c
 
 
 def scan_fwd(u, delta, A, Bm, Cm, D=None, z=None, delta_bias=None, softplus=True, h0=None,
-             want_last=False, want_ckpt=False, out=None):
-    """u, delta, z: (B, L, D) channel-last; Bm, Cm: (B, L, N); A: (D, N) fp32.
+             want_last=False, want_ckpt=False, out=None, a_is_log=False):
+    """u, delta, z: (B, L, D) channel-last; Bm, Cm: (B, L, N); A: (D, N) fp32
+    (a_is_log: A holds A_log, the kernels use -exp(A_log)).
     Returns (out, last_state | None, ckpt | None)."""
     _check_cuda(u, delta, A, Bm, Cm, D, z, delta_bias, h0)
     Bsz, Ln, Dm = u.shape
@@ -87,7 +89,7 @@ def scan_fwd(u, delta, A, Bm, Cm, D=None, z=None, delta_bias=None, softplus=True
     last = torch.empty(Bsz, Dm, N, device=u.device, dtype=torch.float32) if want_last else None
     ckpt = (torch.empty(Bsz, (Ln + SCAN_CKPT - 1) // SCAN_CKPT, Dm, N, device=u.device, dtype=torch.float32)
             if want_ckpt else None)
-    a = _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, ckpt)
+    a = _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, out, last, ckpt, a_is_log)
     wsz = L.lib().mtts_selective_scan_fwd_workspace(Bsz, Dm, Ln, N)
     ws = torch.empty(wsz, device=u.device, dtype=torch.uint8) if wsz > 0 else None
     a.workspace = L.ptr(ws)
@@ -96,10 +98,11 @@ def scan_fwd(u, delta, A, Bm, Cm, D=None, z=None, delta_bias=None, softplus=True
 
 
 def scan_bwd(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, ckpt, dout,
-             du=None, ddelta=None, dz=None, dB=None, dC=None, need_dh0=False):
+             du=None, ddelta=None, dz=None, dB=None, dC=None, need_dh0=False, a_is_log=False):
     """Backward of scan_fwd.  du/ddelta/dz may be preallocated (strided)
     views to write into; dB/dC (B, L, N) fp32 views likewise.
-    Returns du, ddelta, dz, dB, dC, dA, dD, ddelta_bias, dh0."""
+    Returns du, ddelta, dz, dB, dC, dA, dD, ddelta_bias, dh0 (with a_is_log
+    the returned dA is the gradient w.r.t. A_log)."""
     Bsz, Ln, Dm = u.shape
     N = A.shape[1]
     dev = u.device
@@ -123,7 +126,7 @@ def scan_bwd(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, ckpt, dout,
     ws = torch.empty(L.lib().mtts_selective_scan_bwd_workspace(Bsz, Dm, Ln, N), device=dev, dtype=torch.uint8)
     dummy_out = dout  # the forward's `out` is not read by the backward
     b = L.ScanBwdArgs()
-    b.f = _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, dummy_out, None, ckpt)
+    b.f = _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, dummy_out, None, ckpt, a_is_log)
     b.dout, b.dout_bs, b.dout_ls = dout.data_ptr(), dout.stride(0), dout.stride(1)
     b.du, b.du_bs, b.du_ls = du.data_ptr(), du.stride(0), du.stride(1)
     b.ddelta, b.ddelta_bs, b.ddelta_ls = ddelta.data_ptr(), ddelta.stride(0), ddelta.stride(1)

@@ -819,3 +819,34 @@ def test_gemm_rows_packed_no_bias_wide_n_small_k(M, N, K):
     close(y, x.double() @ w.double().t(), rtol=2 ** -8, name="packed no-bias")
     yp = ops.gemm_rows(ops.PackedAct.pack(x), ops.pack_rows_weight(w), packed_out="only")
     assert torch.equal(yp.unpack(), y)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 100, 256), (1, 37, 100), (32, 48, 2048), (2, 300, 128)])
+def test_scan_a_is_log_matches_explicit_A(shape, dtype):
+    """a_is_log (A = -exp(A_log) formed in-kernel, the backward returning
+    dA_log = dA * A) equals passing the explicit A: every kernel family
+    (one-lane-per-channel at B*D >= 64k, LDS-DMA P = 4, narrow D, L-segment
+    backward)."""
+    from mtts import ops
+    torch.manual_seed(5)
+    B, L, D = shape
+    u = torch.randn(B, L, D, device=DEV).to(dtype)
+    delta = (torch.randn(B, L, D, device=DEV) * 0.5).to(dtype)
+    z = torch.randn(B, L, D, device=DEV).to(dtype)
+    Bm = torch.randn(B, L, 16, device=DEV).to(dtype)
+    Cm = torch.randn(B, L, 16, device=DEV).to(dtype)
+    A_log = torch.log(torch.arange(1, 17, device=DEV, dtype=torch.float32)).repeat(D, 1) + 0.1 * torch.randn(D, 16, device=DEV)
+    A = -torch.exp(A_log)
+    Dp = torch.randn(D, device=DEV)
+    bias = torch.randn(D, device=DEV) * 0.1
+    y1, _, ck1 = ops.scan_fwd(u, delta, A, Bm, Cm, Dp, z, bias, True, want_ckpt=True)
+    y2, _, ck2 = ops.scan_fwd(u, delta, A_log, Bm, Cm, Dp, z, bias, True, want_ckpt=True, a_is_log=True)
+    close(y2.float(), y1.float(), rtol=1e-5 if dtype == torch.float32 else 1e-2, name="out")
+    g = torch.randn(B, L, D, device=DEV).to(dtype)
+    r1 = ops.scan_bwd(u, delta, A, Bm, Cm, Dp, z, bias, True, None, ck1, g)
+    r2 = ops.scan_bwd(u, delta, A_log, Bm, Cm, Dp, z, bias, True, None, ck2, g, a_is_log=True)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    for name, i in (("du", 0), ("ddelta", 1), ("dz", 2), ("dB", 3), ("dC", 4), ("dD", 6), ("dbias", 7)):
+        close(r2[i].float(), r1[i].float(), rtol=tol, name=name)
+    close(r2[5], r1[5] * A, rtol=tol, name="dA_log")
