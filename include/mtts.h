@@ -203,6 +203,14 @@ typedef struct {
 
 int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* stream);
 
+/* Decode: x_proj fused into the state update (Mamba.step's
+ * x_db = x_proj(x); dt, B, C = split(x_db); state update).  `x` (B, D) bf16
+ * is the conv output u; x_dbl = u . wx^T with wx (n_xdbl, D) bf16 row-major,
+ * n_xdbl = dt_rank + 2 * 16, formed in-kernel (bf16-rounded as the unfused
+ * x_proj output); `dt`, `Bm`, `Cm` (and their strides) are not read;
+ * dt_rank % 32 == 0 and dt_w required; batch <= 32, dim % 128 == 0. */
+int mtts_xproj_state_update(const MttsStateUpdateArgs* a, const void* wx, int n_xdbl, void* stream);
+
 /* ------------------------------------------------------------------------
  * LayerNorm (eps) with optional fused FiLM, optional fused residual add.
  * Replaces torch nn.LayerNorm at mamba_decoder.py:59,67,81,184 and the FiLM

@@ -141,6 +141,7 @@ _SIGS = {
     "mtts_causal_conv1d_bwd": ([C.POINTER(ConvBwdArgs), vp], i32),
     "mtts_causal_conv1d_update": ([C.POINTER(ConvUpdateArgs), vp], i32),
     "mtts_selective_state_update": ([C.POINTER(StateUpdateArgs), vp], i32),
+    "mtts_xproj_state_update": ([C.POINTER(StateUpdateArgs), vp, i32, vp], i32),
     "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
     "mtts_gemm_rows": ([C.POINTER(RowsArgs), vp], i32),
     "mtts_pack_rows_bytes": ([i32, i32], i64),

@@ -249,6 +249,7 @@ class DecodeEngine:
         like its weights; the LayerNorm(+FiLM) prologues run on the packed
         rows.  9 launches per layer, as _step_rows."""
         m, c = self.m, self.ctx
+        fuse_xs = os.environ.get("MTTS_DECODE_XS", "0") != "0"   # measured slower (tools/decode_ab.py xs: 1.10 vs 0.77 ms): off
         xp = None   # packed image of the residual stream (none before layer 0)
         for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
             conv_state, ssm_state = states[i]
@@ -257,9 +258,13 @@ class DecodeEngine:
             xz, u, up = ops.gemm_rows(x if xp is None else xp, p["Win_p"],
                                       conv=(conv_state, p["conv_w"], p["conv_b"]), ln=ln(l.norm_mamba),
                                       u_packed=True)
-            x_dbl = ops.gemm_rows(up, p["Wx_p"])
-            y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
-                                 xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"], packed_out=True)
+            if fuse_xs and ops.xproj_state_ok(u, p["Wx"], p["Wdt"]):   # x_proj inside the state update: one launch
+                y = ops.xproj_state_update(ssm_state, u, p["Wx"], p["A"], p["D"], xz[:, di:], p["dt_bias"], True,
+                                           dt_w=p["Wdt"], packed_out=True)
+            else:
+                x_dbl = ops.gemm_rows(up, p["Wx_p"])
+                y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
+                                     xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"], packed_out=True)
             x, xp = ops.gemm_rows(y, p["Wout_p"], res=x, packed_out="also")
             q = ops.gemm_rows(xp, p["Wq_p"], p["bq"], ln=ln(l.norm_cross))
             o = attention_decode_packed(q, p["khm"], p["vhm"], l.cross_attn.num_heads, c["kpm"])

@@ -850,3 +850,33 @@ def test_scan_a_is_log_matches_explicit_A(shape, dtype):
     for name, i in (("du", 0), ("ddelta", 1), ("dz", 2), ("dB", 3), ("dC", 4), ("dD", 6), ("dbias", 7)):
         close(r2[i].float(), r1[i].float(), rtol=tol, name=name)
     close(r2[5], r1[5] * A, rtol=tol, name="dA_log")
+
+
+@pytest.mark.parametrize("B,Dm,R", [(32, 2048, 64), (7, 256, 32), (1, 128, 64)])
+def test_xproj_state_update_matches_unfused(B, Dm, R):
+    """Decode: x_proj fused into the state update (mtts_xproj_state_update)
+    equals x_dbl = bf16(u W_x^T) followed by the dt_proj-fused state update:
+    y (row-major and packed image) and the in-place state."""
+    from mtts import ops
+    torch.manual_seed(B + Dm + R)
+    bf = torch.bfloat16
+    u = torch.randn(B, Dm, device=DEV).to(bf)
+    wx = (torch.randn(R + 32, Dm, device=DEV) / Dm ** 0.5).to(bf)
+    wdt = (torch.randn(Dm, R, device=DEV) / R ** 0.5).to(bf)
+    A = -torch.exp(torch.randn(Dm, 16, device=DEV) * 0.5)
+    Dp = torch.randn(Dm, device=DEV)
+    z = torch.randn(B, Dm, device=DEV).to(bf)
+    bias = torch.randn(Dm, device=DEV) * 0.1
+    st0 = torch.randn(B, Dm, 16, device=DEV)
+    assert ops.xproj_state_ok(u, wx, wdt)
+    s1, s2 = st0.clone(), st0.clone()
+    x_dbl = (u.float() @ wx.float().t()).to(bf)
+    y1 = ops.state_update(s1, u, x_dbl[:, :R], A, x_dbl[:, R:R + 16], x_dbl[:, R + 16:], Dp, z, bias, True, dt_w=wdt)
+    y2 = ops.xproj_state_update(s2, u, wx, A, Dp, z, bias, True, dt_w=wdt)
+    close(y2.float(), y1.float(), rtol=2e-2, name="y")
+    close(s2, s1, rtol=2e-2, name="state")
+    if Dm % 32 == 0:
+        s3 = st0.clone()
+        yp = ops.xproj_state_update(s3, u, wx, A, Dp, z, bias, True, dt_w=wdt, packed_out=True)
+        close(yp.unpack().float(), y2.float(), rtol=0, name="packed y")
+        assert torch.equal(s3, s2)

@@ -110,6 +110,13 @@ if __name__ == "__main__":
                 print("xpacked", pk, end=" ", flush=True)
                 step((True,))
         os.environ.pop("MTTS_DECODE_XPACKED")
+    if "xs" in what:   # x_proj fused into the state update (mtts_xproj_state_update) vs two launches, interleaved
+        for _ in range(2):
+            for v in ("1", "0"):
+                os.environ["MTTS_DECODE_XS"] = v
+                print("xs", v, end=" ", flush=True)
+                step((True,))
+        os.environ.pop("MTTS_DECODE_XS")
     if "splitk" in what:   # rows kernels with / without the cross-workgroup K split, interleaved
         for _ in range(2):
             for sk in (True, False):
