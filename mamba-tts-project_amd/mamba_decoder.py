@@ -33,6 +33,39 @@ from mtts.decode import DecodeEngine
 from mtts.embed import embed_sum
 
 
+class StyleMLPAll(torch.autograd.Function):
+    """All layers' FiLM conditioning tanh(z W_l^T + b_l) at once (reference
+    mamba_decoder.py:52-55, 82-84): forward one baddbmm + tanh + cast; the
+    backward takes the n_layers gamma|beta gradients together (one stack),
+    one tanh-backward, one bmm for the weight gradients, one sum for the
+    biases and one for z -- instead of ~8 small launches per layer (and no
+    zero-filled per-layer slices of a stacked gradient)."""
+
+    @staticmethod
+    def forward(ctx, z, cd, *params):
+        ws, bs = params[0::2], params[1::2]
+        W = torch.stack(ws)                                               # (L, 2d, d_style)
+        b = torch.stack(bs)                                               # (L, 2d)
+        gb = torch.tanh(torch.baddbmm(b[:, None, :], z[None].expand(len(ws), -1, -1), W.transpose(1, 2)))
+        ctx.save_for_backward(z, W, gb)
+        out = gb.to(cd)
+        return tuple(out[i] for i in range(len(ws)))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        z, W, gb = ctx.saved_tensors
+        L = W.shape[0]
+        g = torch.stack([gi if gi is not None else torch.zeros_like(gb[0]) for gi in grads]).to(gb.dtype)
+        dpre = g * (1.0 - gb * gb)                                        # tanh'
+        dW = torch.bmm(dpre.transpose(1, 2), z[None].expand(L, -1, -1))   # (L, 2d, d_style)
+        db = dpre.sum(1)                                                  # (L, 2d)
+        dz = torch.bmm(dpre, W).sum(0) if ctx.needs_input_grad[0] else None
+        out = [dz, None]
+        for i in range(L):
+            out += [dW[i], db[i]]
+        return tuple(out)
+
+
 class MambaTTSDecoderLayer(nn.Module):
     def __init__(self, d_model, n_heads, d_ff, d_style):
         super().__init__()
@@ -168,20 +201,17 @@ class MambaTTSDecoder(nn.Module):
 
     def _style_all(self, z_style, cd):
         """Every layer's style_mlp(z_style) = tanh(z W_l^T + b_l) (:52-55, applied
-        at :82-84) as ONE batched GEMM over the stacked layer weights (fp32, the
-        parameters' dtype), cast to the compute dtype once: (n_layers, B, 2d).
-        Autograd splits the stacked gradients back to each layer's parameters.
-        None when the layers' style MLPs differ in shape / dtype."""
+        at :82-84) in ONE batched GEMM over the stacked layer weights (fp32, the
+        parameters' dtype), cast to the compute dtype once (StyleMLPAll).
+        Returns n_layers (B, 2d) tensors, or None when the layers' style MLPs
+        differ in shape / dtype."""
         lins = [l.style_mlp[0] for l in self.layers]
         w0 = lins[0].weight
         if (len(lins) < 2 or any(m.weight.shape != w0.shape or m.weight.dtype != w0.dtype or m.bias is None
-                                 for m in lins)):
+                                 or m.bias.dtype != w0.dtype for m in lins)):
             return None
-        W = torch.stack([m.weight for m in lins])                         # (L, 2d, d_style)
-        b = torch.stack([m.bias for m in lins])                           # (L, 2d)
-        z = z_style.to(w0.dtype)
-        gb = torch.tanh(torch.baddbmm(b[:, None, :], z[None].expand(len(lins), -1, -1), W.transpose(1, 2)))
-        return gb.to(cd)
+        params = [t for m in lins for t in (m.weight, m.bias)]
+        return StyleMLPAll.apply(z_style.to(w0.dtype), cd, *params)
 
     def _run_layers(self, x, text_hidden, z_style, text_mask, states):
         pending = None
