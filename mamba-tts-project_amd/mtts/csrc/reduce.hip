@@ -117,6 +117,14 @@ __global__ __launch_bounds__(256) void colsum_rows_kernel(const T* __restrict__ 
   };
   if (c < cols) {
     int r = r0 + w;
+    // 16 rows in flight per lane (a 64-row chunk is one batch of loads)
+    for (; r + 60 < r1; r += 64) {
+      uint4 v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = *reinterpret_cast<const uint4*>(in + (int64_t)(r + 4 * q) * ld + c);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) add(v[q]);
+    }
     for (; r + 12 < r1; r += 16) {
       uint4 v[4];
 #pragma unroll
@@ -139,7 +147,7 @@ __global__ __launch_bounds__(256) void colsum_rows_kernel(const T* __restrict__ 
 
 extern "C" int64_t mtts_colsum_workspace(int rows, int cols, int rows_per_group) {
   if (rows_per_group <= 1024 && !(rows_per_group >= rows && rows > 1024)) return 0;
-  const int64_t chunks = (int64_t)(rows + 127) / 128;   // the 128-row single-group path needs the most
+  const int64_t chunks = (int64_t)(rows + 15) / 16;     // the single-group path's chunks (>= 16 rows each)
   return chunks * cols * 4 + 256;
 }
 
@@ -159,7 +167,9 @@ extern "C" int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_
     // one group over many rows (bias gradients): 16-byte row pieces, 128-row
     // chunks -> fp32 partial slab -> sum of the chunks
     MTTS_CHECK(workspace, "colsum: workspace required (mtts_colsum_workspace)");
-    const int rchunk = 128;
+    // 128-row chunks (tools/bench_colsum.py: 64 / 32 measured equal at 1024 columns, slower at 2048+)
+    const char* e = getenv("MTTS_COLSUM_RCHUNK");
+    const int rchunk = e ? std::max(16, atoi(e)) : 128;
     const int chunks = (rows + rchunk - 1) / rchunk;
     float* part = (float*)workspace;
     if (dtype == MTTS_F32)

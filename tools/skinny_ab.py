@@ -25,41 +25,41 @@ def t(fn, it=30):
     return e0.elapsed_time(e1) / it * 1e3
 
 
-M, D, R = 16384, 2048, 64
-bf = torch.bfloat16
-u = torch.randn(M, D, device="cuda").to(bf)
-wx = torch.randn(R + 32, D, device="cuda").to(bf)
-wdt = torch.randn(D, R, device="cuda").to(bf)
-x_dbl = torch.randn(M, R + 32, device="cuda").to(bf)
-dd = torch.randn(M, D, device="cuda").to(bf)
-dx = torch.zeros(M, R + 32, device="cuda")
-du = torch.randn(M, D, device="cuda").to(bf)
-wdt_t, wx_t = wdt.t().contiguous(), wx.t().contiguous()
-gx = x_dbl
-ops = {
-    "x_proj fwd  (16384x96, K=2048)": (lambda: G.mm_skinny(u, wx), lambda: u @ wx.t()),
-    "dt_proj fwd (16384x2048, K=64)": (lambda: G.mm_skinny(x_dbl[:, :R], wdt), lambda: x_dbl[:, :R] @ wdt.t()),
-    "d(dt)       (16384x64, K=2048)": (lambda: G.mm_skinny(dd, wdt_t, out=dx[:, :R]),
-                                       lambda: dx[:, :R].copy_(dd @ wdt)),
-    "du += gx Wx (16384x2048, K=96)": (lambda: G.mm_skinny(gx, wx_t, out=du, beta=1.0), lambda: du.addmm_(gx, wx)),
-}
-for name, (a, b) in ops.items():
-    print(f"{name}: skinny {t(a):6.1f} us   torch {t(b):6.1f} us", flush=True)
-for mb in ("1", "2", "4"):
-    os.environ["MTTS_SKINNY_MB"] = mb
-    print(f"  MB={mb}: x_proj fwd {t(ops['x_proj fwd  (16384x96, K=2048)'][0]):6.1f} us   "
-          f"d(dt) {t(ops['d(dt)       (16384x64, K=2048)'][0]):6.1f} us", flush=True)
-os.environ.pop("MTTS_SKINNY_MB")
-for name, (dy_, x_) in {"dW_dt (2048x64)": (dd, x_dbl[:, :R]), "dW_x (96x2048)": (gx, u)}.items():
-    G.SKINNY_TN = True
-    a = t(lambda: LIN.wgrad(dy_, x_))
-    G.SKINNY_TN = False
-    b = t(lambda: LIN.wgrad(dy_, x_))
-    G.SKINNY_TN = True
-    print(f"{name}: TN {a:6.1f} us   bmm split {b:6.1f} us", flush=True)
+def op_bench():
+    M, D, R = 16384, 2048, 64
+    bf = torch.bfloat16
+    u = torch.randn(M, D, device="cuda").to(bf)
+    wx = torch.randn(R + 32, D, device="cuda").to(bf)
+    wdt = torch.randn(D, R, device="cuda").to(bf)
+    x_dbl = torch.randn(M, R + 32, device="cuda").to(bf)
+    dd = torch.randn(M, D, device="cuda").to(bf)
+    dx = torch.zeros(M, R + 32, device="cuda")
+    du = torch.randn(M, D, device="cuda").to(bf)
+    wdt_t, wx_t = wdt.t().contiguous(), wx.t().contiguous()
+    gx = x_dbl
+    ops = {
+        "x_proj fwd  (16384x96, K=2048)": (lambda: G.mm_skinny(u, wx), lambda: u @ wx.t()),
+        "dt_proj fwd (16384x2048, K=64)": (lambda: G.mm_skinny(x_dbl[:, :R], wdt), lambda: x_dbl[:, :R] @ wdt.t()),
+        "d(dt)       (16384x64, K=2048)": (lambda: G.mm_skinny(dd, wdt_t, out=dx[:, :R]),
+                                           lambda: dx[:, :R].copy_(dd @ wdt)),
+        "du += gx Wx (16384x2048, K=96)": (lambda: G.mm_skinny(gx, wx_t, out=du, beta=1.0), lambda: du.addmm_(gx, wx)),
+    }
+    for name, (a, b) in ops.items():
+        print(f"{name}: skinny {t(a):6.1f} us   torch {t(b):6.1f} us", flush=True)
+    for mb in ("1", "2", "4"):
+        os.environ["MTTS_SKINNY_MB"] = mb
+        print(f"  MB={mb}: x_proj fwd {t(ops['x_proj fwd  (16384x96, K=2048)'][0]):6.1f} us   "
+              f"d(dt) {t(ops['d(dt)       (16384x64, K=2048)'][0]):6.1f} us", flush=True)
+    os.environ.pop("MTTS_SKINNY_MB")
+    for name, (dy_, x_) in {"dW_dt (2048x64)": (dd, x_dbl[:, :R]), "dW_x (96x2048)": (gx, u)}.items():
+        G.SKINNY_TN = True
+        a = t(lambda: LIN.wgrad(dy_, x_))
+        G.SKINNY_TN = False
+        b = t(lambda: LIN.wgrad(dy_, x_))
+        G.SKINNY_TN = True
+        print(f"{name}: TN {a:6.1f} us   bmm split {b:6.1f} us", flush=True)
 
-if len(sys.argv) > 1 and sys.argv[1] == "ops":
-    sys.exit(0)
+
 import bench  # noqa: E402
 import mamba_decoder  # noqa: E402
 from mtts.optim import FusedClipAdam  # noqa: E402
@@ -92,10 +92,14 @@ def timeit(n=10):
     return (time.perf_counter() - t0) / n * 1e3
 
 
-res = {"skinny": [], "skinny+xproj": [], "off": []}
-for _ in range(3):
-    for kind in res:
-        G.SKINNY = kind != "off"
-        G.SKINNY_XPROJ = kind == "skinny+xproj"
-        res[kind].append(timeit())
-print({k: [round(x, 2) for x in v] for k, v in res.items()}, flush=True)
+if __name__ == "__main__":
+    op_bench()
+    if len(sys.argv) > 1 and sys.argv[1] == "ops":
+        sys.exit(0)
+    res = {"skinny": [], "skinny+xproj": [], "off": []}
+    for _ in range(3):
+        for kind in res:
+            G.SKINNY = kind != "off"
+            G.SKINNY_XPROJ = kind == "skinny+xproj"
+            res[kind].append(timeit())
+    print({k: [round(x, 2) for x in v] for k, v in res.items()}, flush=True)
