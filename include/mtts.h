@@ -594,11 +594,18 @@ int mtts_gemm(const MttsGemmArgs* a, void* stream);
  * k % 32 == 0, n % 4 == 0; A / B 16-byte aligned, lda / ldb multiples of 8;
  * C bf16 (8-byte aligned) or fp32 (16-byte aligned), ldc % 4 == 0;
  * beta 0 or 1 (accumulate into C, e.g. du += d(x_dbl) W_x).
+ *   mode SKINNY_TN : C[m,n] = A[k,m]^T . B[k,n] (both token-major), the
+ *                    x_proj / dt_proj weight gradients: n <= 128, n % 8 == 0,
+ *                    m % 128 == 0, fp32 C contiguous (ldc = n, or = m with
+ *                    trans_c: C^T (n x m) is written), beta = 0; chunk
+ *                    partials in `workspace` (mtts_gemm_skinny_workspace()
+ *                    bytes), summed in fixed order.
  * ------------------------------------------------------------------------ */
 #define MTTS_SKINNY_N 0
 #define MTTS_SKINNY_SMALL_K 1
+#define MTTS_SKINNY_TN 2
 typedef struct {
-  int mode;                  /* MTTS_SKINNY_N / MTTS_SKINNY_SMALL_K */
+  int mode;                  /* MTTS_SKINNY_N / MTTS_SKINNY_SMALL_K / MTTS_SKINNY_TN */
   int m, n, k;
   int c_dtype;               /* MTTS_F32 / MTTS_BF16 */
   float beta;
@@ -606,8 +613,12 @@ typedef struct {
   const void* a;
   const void* b;
   void* c;
+  void* workspace;           /* SKINNY_TN only */
+  int trans_c;               /* SKINNY_TN: write C^T */
+  int reserved_;
 } MttsSkinnyArgs;
 
+int64_t mtts_gemm_skinny_workspace(const MttsSkinnyArgs* a);
 int mtts_gemm_skinny(const MttsSkinnyArgs* a, void* stream);
 
 #ifdef __cplusplus

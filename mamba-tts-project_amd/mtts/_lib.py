@@ -90,7 +90,8 @@ class GemmArgs(C.Structure):
 
 class SkinnyArgs(C.Structure):
     _fields_ = [("mode", i32), ("m", i32), ("n", i32), ("k", i32), ("c_dtype", i32), ("beta", f32),
-                ("lda", i64), ("ldb", i64), ("ldc", i64), ("a", vp), ("b", vp), ("c", vp)]
+                ("lda", i64), ("ldb", i64), ("ldc", i64), ("a", vp), ("b", vp), ("c", vp), ("workspace", vp),
+                ("trans_c", i32), ("reserved_", i32)]
 
 
 class LNArgs(C.Structure):
@@ -153,6 +154,7 @@ _SIGS = {
     "mtts_gemm_workspace": ([C.POINTER(GemmArgs)], i64),
     "mtts_gemm": ([C.POINTER(GemmArgs), vp], i32),
     "mtts_gemm_skinny": ([C.POINTER(SkinnyArgs), vp], i32),
+    "mtts_gemm_skinny_workspace": ([C.POINTER(SkinnyArgs)], i64),
     "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),
     "mtts_layernorm_bwd": ([C.POINTER(LNBwdArgs), vp], i32),
     "mtts_colsum_workspace": ([i32, i32, i32], i64),

@@ -254,6 +254,119 @@ __global__ __launch_bounds__(256) void small_k_kernel(SkinnyP p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// SKINNY_TN: C[m, n] = A[k, m]^T . B[k, n] (fp32, optionally stored as C^T)
+// with n <= 128 narrow and m % 128 == 0 wide -- the x_proj / dt_proj weight
+// gradients (dW_dt = d(delta)^T dt: m = d_inner, n = dt_rank; dW_x^T =
+// u^T d(x_dbl): m = d_inner, n = dt_rank + 2 d_state), K = tokens.
+// Both operands are token-major (k = the row index), so the MFMA fragments
+// (8 consecutive k of one column per lane) come from ds_read_b64_tr_b16 over a
+// row-major LDS image: a workgroup (8 waves) owns 128 columns of A (one
+// 16-column block per wave) x all n and a chunk of kc tokens; 64-token tiles
+// of A (64 x 128) and B (64 x 128, zero-padded past n) are staged through a
+// double-buffered LDS image (plain 256-B rows, 16-B chunk swizzle
+// ch ^ (((row&3)<<2) | ((row>>2)&3)): conflict-free transposed reads), the
+// next tile's rows loaded into registers while the current one computes.
+// The chunks' fp32 partial tiles go to a slab summed in fixed order
+// (colsum).  HBM-bound: A is read once, B once per 128 columns (L2).
+constexpr int kTnRows = 64;   // tokens per LDS tile
+__device__ __forceinline__ int tn_off(int row, int ch) {   // byte offset of 16-B chunk ch of row `row`
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+// lane's transposed fragment of the image: column block cb (16 columns), k rows 32 ks + 8 g .. +7
+__device__ __forceinline__ uint4 tn_frag(const char* img, int cb, int ks, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  s16x4 r[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = ks * 32 + 8 * g + 4 * h + q;
+    const int off = tn_off(row, cb * 2 + (pp >> 1)) + 8 * (pp & 1);
+    r[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off));
+  }
+  s16x8 v{r[0][0], r[0][1], r[0][2], r[0][3], r[1][0], r[1][1], r[1][2], r[1][3]};
+  return __builtin_bit_cast(uint4, v);
+}
+
+struct TnP {
+  const bf16_t* a;   // (k, m) row stride lda
+  const bf16_t* b;   // (k, n) row stride ldb
+  float* slab;       // (chunks, m, n) or (chunks, n, m) with TRANS
+  int64_t lda, ldb;
+  int m, n, k, kc;
+};
+
+template <int NB, bool TRANS>
+__global__ __launch_bounds__(512) void tn_skinny_kernel(TnP p) {
+  __shared__ __attribute__((aligned(16))) char sa[2][kTnRows * 256];
+  __shared__ __attribute__((aligned(16))) char sb[2][kTnRows * 256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c0 = blockIdx.x * 128;
+  const int k0 = blockIdx.y * p.kc, k1 = min(p.k, k0 + p.kc);
+  const int ntile = (k1 - k0 + kTnRows - 1) / kTnRows;
+  // this thread's two 16-B chunks of each 64 x 128 tile: rows tid/16 and tid/16 + 32, chunk tid % 16
+  const int ch = tid & 15, r0 = tid >> 4;
+  const bool bok = ch * 8 < p.n;   // n % 8 == 0 (host): a chunk is all in or all out
+  uint4 ra[2], rb[2];
+  auto load = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int row = k0 + t * kTnRows + r0 + 32 * s;
+      const bool ok = row < k1;
+      const int rr = ok ? row : k0;
+      ra[s] = *(const uint4*)(p.a + (int64_t)rr * p.lda + c0 + ch * 8);
+      rb[s] = *(const uint4*)(p.b + (int64_t)rr * p.ldb + (bok ? ch * 8 : 0));
+      if (!ok) ra[s] = make_uint4(0, 0, 0, 0);
+      if (!ok || !bok) rb[s] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      *(uint4*)(sa[buf] + tn_off(r0 + 32 * s, ch)) = ra[s];
+      *(uint4*)(sb[buf] + tn_off(r0 + 32 * s, ch)) = rb[s];
+    }
+  };
+  f32x4 acc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (ntile > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  // (a two-deep register ring measured equal / slower: tools/skinny_ab.py)
+  for (int t = 0; t < ntile; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntile) load(t + 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint4 fa = tn_frag(sa[buf], wave, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const uint4 fb = tn_frag(sb[buf], j, ks, lane);
+        // !TRANS: lane ends with 4 consecutive n of one m; TRANS: 4 consecutive m of one n
+        acc[j] = TRANS ? mfma16(fa, fb, acc[j]) : mfma16(fb, fa, acc[j]);
+      }
+    }
+    if (t + 1 < ntile) store(buf ^ 1);
+    __syncthreads();
+  }
+  float* sl = p.slab + (int64_t)blockIdx.y * p.m * p.n;
+  const int li = lane & 15, g4 = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    if constexpr (TRANS) {   // C^T[n][m]: n = 16 j + li, m = c0 + 16 wave + g4 .. +3
+      const int nn = j * 16 + li;
+      if (nn < p.n) *(f32x4*)(sl + (int64_t)nn * p.m + c0 + wave * 16 + g4) = acc[j];
+    } else {                 // C[m][n]: m = c0 + 16 wave + li, n = 16 j + g4 .. +3
+      const int nn = j * 16 + g4;
+      if (nn < p.n) *(f32x4*)(sl + (int64_t)(c0 + wave * 16 + li) * p.n + nn) = acc[j];
+    }
+  }
+}
+
 template <int MB>
 void launch_skinny_n(const SkinnyP& p, hipStream_t st) {
   const int nb = (p.n + 15) / 16;
@@ -270,10 +383,52 @@ void launch_skinny_n(const SkinnyP& p, hipStream_t st) {
 
 using namespace mtts;
 
+static int tn_chunk(int k) { return k >= 8192 ? 512 : 256; }   // tokens per workgroup (>= 512 workgroups at C2)
+
+extern "C" int64_t mtts_gemm_skinny_workspace(const MttsSkinnyArgs* a) {
+  if (!a || a->mode != MTTS_SKINNY_TN || a->k <= 0) return 0;
+  const int kc = tn_chunk(a->k);
+  return (int64_t)((a->k + kc - 1) / kc) * a->m * a->n * 4 + 256;
+}
+
+static int skinny_tn(const MttsSkinnyArgs* a, hipStream_t st) {
+  MTTS_CHECK(a->m % 128 == 0 && a->n <= 128 && a->n % 8 == 0,
+             "gemm_skinny TN: needs m %% 128 == 0 and n <= 128, n %% 8 == 0 (m=%d n=%d)", a->m, a->n);
+  MTTS_CHECK(a->c_dtype == MTTS_F32 && a->beta == 0.f, "gemm_skinny TN: fp32 output, beta = 0");
+  MTTS_CHECK(a->workspace, "gemm_skinny TN: workspace required (mtts_gemm_skinny_workspace)");
+  MTTS_CHECK(a->ldc == (a->trans_c ? a->m : a->n), "gemm_skinny TN: C must be contiguous (ldc = %d)",
+             a->trans_c ? a->m : a->n);
+  MTTS_CHECK(a->lda >= a->m && a->ldb >= a->n, "gemm_skinny TN: leading dimension too small");
+  TnP p;
+  p.a = (const bf16_t*)a->a; p.b = (const bf16_t*)a->b; p.slab = (float*)a->workspace;
+  p.lda = a->lda; p.ldb = a->ldb; p.m = a->m; p.n = a->n; p.k = a->k; p.kc = tn_chunk(a->k);
+  const int chunks = (a->k + p.kc - 1) / p.kc;
+  const dim3 grid(a->m / 128, chunks);
+  const int nb = (a->n + 15) / 16;
+#define TN_(N)                                                                                        \
+  case N:                                                                                             \
+    if (a->trans_c) hipLaunchKernelGGL((tn_skinny_kernel<N, true>), grid, dim3(512), 0, st, p);      \
+    else hipLaunchKernelGGL((tn_skinny_kernel<N, false>), grid, dim3(512), 0, st, p);                \
+    break;
+  switch (nb) { TN_(1) TN_(2) TN_(3) TN_(4) TN_(5) TN_(6) TN_(7) TN_(8) }
+#undef TN_
+  MTTS_LAUNCH_CHECK("gemm_skinny TN");
+  const int ncols = a->m * a->n;
+  colsum(p.slab, chunks, chunks, ncols, ncols, (float*)a->c, 0, st);
+  MTTS_LAUNCH_CHECK("gemm_skinny TN chunk sum");
+  return MTTS_OK;
+}
+
 extern "C" int mtts_gemm_skinny(const MttsSkinnyArgs* a, void* stream) {
   MTTS_CHECK(a && a->a && a->b && a->c, "gemm_skinny: null pointer");
-  MTTS_CHECK(a->mode == MTTS_SKINNY_N || a->mode == MTTS_SKINNY_SMALL_K, "gemm_skinny: bad mode %d", a->mode);
+  MTTS_CHECK(a->mode == MTTS_SKINNY_N || a->mode == MTTS_SKINNY_SMALL_K || a->mode == MTTS_SKINNY_TN,
+             "gemm_skinny: bad mode %d", a->mode);
   MTTS_CHECK(a->m > 0 && a->n > 0 && a->k > 0, "gemm_skinny: m=%d n=%d k=%d must be positive", a->m, a->n, a->k);
+  if (a->mode == MTTS_SKINNY_TN) {
+    MTTS_CHECK(((uintptr_t)a->a | (uintptr_t)a->b | (uintptr_t)a->c) % 16 == 0 && a->lda % 8 == 0 && a->ldb % 8 == 0,
+               "gemm_skinny TN: A / B / C must be 16-byte aligned with row strides a multiple of 8 elements");
+    return skinny_tn(a, (hipStream_t)stream);
+  }
   MTTS_CHECK(a->k % 32 == 0, "gemm_skinny: k=%d must be a multiple of 32", a->k);
   MTTS_CHECK(a->n % 4 == 0, "gemm_skinny: n=%d must be a multiple of 4", a->n);
   MTTS_CHECK(a->mode != MTTS_SKINNY_N || a->n <= 128, "gemm_skinny: SKINNY_N needs n <= 128 (n=%d)", a->n);

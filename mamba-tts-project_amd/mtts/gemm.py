@@ -159,3 +159,30 @@ def mm_skinny(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, beta: 
     args.a, args.b, args.c = a.data_ptr(), b.data_ptr(), out.data_ptr()
     L.call("mtts_gemm_skinny", args)
     return out
+
+
+SKINNY_TN_MODE = 2
+
+
+def skinny_tn_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """a (k, m) wide (m % 128 == 0), b (k, n) narrow (n <= 128, n % 8 == 0),
+    both token-major bf16 with 16-byte rows: the SKINNY_TN weight gradient."""
+    return (SKINNY and _skinny_operand(a) and _skinny_operand(b) and a.shape[0] == b.shape[0] and a.shape[0] > 0
+            and a.shape[1] % 128 == 0 and b.shape[1] <= 128 and b.shape[1] % 8 == 0)
+
+
+def mm_skinny_tn(a: torch.Tensor, b: torch.Tensor, trans_c: bool = False) -> torch.Tensor:
+    """fp32 a^T b (m x n), or its transpose (n x m) with trans_c, on the
+    SKINNY_TN kernel (chunk partials summed in fixed order)."""
+    k, m = a.shape
+    n = b.shape[1]
+    out = torch.empty((n, m) if trans_c else (m, n), device=a.device, dtype=torch.float32)
+    args = L.SkinnyArgs()
+    args.mode, args.m, args.n, args.k = SKINNY_TN_MODE, m, n, k
+    args.c_dtype, args.beta, args.trans_c = L.F32, 0.0, int(trans_c)
+    args.lda, args.ldb, args.ldc = a.stride(0), b.stride(0), out.stride(0)
+    args.a, args.b, args.c = a.data_ptr(), b.data_ptr(), out.data_ptr()
+    ws = torch.empty(L.lib().mtts_gemm_skinny_workspace(args), device=a.device, dtype=torch.uint8)
+    args.workspace = ws.data_ptr()
+    L.call("mtts_gemm_skinny", args)
+    return out

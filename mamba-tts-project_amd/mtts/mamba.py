@@ -94,7 +94,8 @@ class MambaInnerFn(torch.autograd.Function):
             G.mm_skinny(dd2, WdtT, out=dxd2[:, :r])
         else:
             dx_dbl[..., :r] = (ddelta @ Wdt).float()
-        dW_dt = wgrad(dd2, x_dbl.view(-1, r + 2 * N)[:, :r])
+        dt2 = x_dbl.view(-1, r + 2 * N)[:, :r]
+        dW_dt = G.mm_skinny_tn(dd2, dt2) if G.skinny_tn_ok(dd2, dt2) else wgrad(dd2, dt2)
         # x_proj: x_dbl = u @ W_x^T  ->  du += d(x_dbl) W_x (accumulated by the GEMM), dW_x
         gx = dx_dbl.to(cd).view(-1, r + 2 * N)
         du2 = du.view(-1, di)
@@ -103,7 +104,8 @@ class MambaInnerFn(torch.autograd.Function):
             G.mm_skinny(gx, WxT, out=du2, beta=1.0)
         else:
             du2.addmm_(gx, Wx)
-        dW_x = wgrad(gx, u.reshape(-1, di))
+        u2 = u.reshape(-1, di)
+        dW_x = G.mm_skinny_tn(u2, gx, trans_c=True) if G.skinny_tn_ok(u2, gx) else wgrad(gx, u2)
         # the conv's left history (a prefilled conv_state) enters the
         # recomputed pre-activations and the weight gradient
         _, dw, db = ops.conv_bwd(x, conv_w, conv_b, du, True, dx=dxz[..., :di], state_in=conv_state_in)

@@ -257,3 +257,22 @@ def test_tn_skinny_weight_gradients(shape):
     out = LIN.wgrad(dy, x)
     ref = dy.float().t() @ x.float()
     assert rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("k,m,n,trans", [(16384, 2048, 64, False), (16384, 2048, 96, True), (1000, 256, 40, False),
+                                         (77, 128, 8, True), (4096, 384, 128, False)])
+def test_skinny_tn_weight_gradient(k, m, n, trans):
+    """SKINNY_TN (x_proj / dt_proj weight gradients): fp32 a^T b over k
+    token rows (ragged k, n < 16 * blocks), or its transpose, vs fp32 torch;
+    the narrow operand as a strided column slice like x_dbl[:, :dt_rank]."""
+    torch.manual_seed(k + m + n)
+    a = rnd(k, m)
+    bb = rnd(k, n + 32)
+    b = bb[:, :n]
+    assert G.skinny_tn_ok(a, b)
+    out = G.mm_skinny_tn(a, b, trans_c=trans)
+    ref = a.float().t() @ b.float()
+    if trans:
+        ref = ref.t()
+    assert out.shape == ref.shape
+    assert rel(out, ref) < 1e-5

@@ -58,6 +58,8 @@ def op_bench():
         b = t(lambda: LIN.wgrad(dy_, x_))
         G.SKINNY_TN = True
         print(f"{name}: TN {a:6.1f} us   bmm split {b:6.1f} us", flush=True)
+    for name, (a_, b_, tr) in {"dW_dt skinny-TN": (dd, x_dbl[:, :R], False), "dW_x^T skinny-TN": (u, gx, True)}.items():
+        print(f"{name}: {t(lambda: G.mm_skinny_tn(a_, b_, trans_c=tr)):6.1f} us", flush=True)
 
 
 import bench  # noqa: E402
