@@ -13,7 +13,11 @@ applies the 1/world averaging.  Large buckets (default 128 MB) suit xGMI's
 point-to-point links: few, large ring collectives.  The FIRST bucket (the
 parameters whose gradients the backward finishes first: the head and the
 last layer) is capped at `first_bucket_mb` so the first all-reduce starts
-early in the backward.
+early in the backward.  Gradients are not accumulated in place: each step
+starts with p.grad = None, autograd allocates every gradient fresh and the
+post-accumulate hook copies it into its view (one copy instead of a zero-fill
+of the whole buffer plus an in-place add per parameter); with RCCL the
+collective averages (ReduceOp.AVG).
 
 `comm_dtype=torch.bfloat16` all-reduces a bf16 image of each bucket (half
 the bytes on the links; the fp32 gradients are rounded once to bf16 before
@@ -68,11 +72,13 @@ class GradAllReduce:
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
 
     def zero_grad(self):
-        """Zero the flat buffer and re-bind every p.grad to its view (the
-        contract: call this, not optimizer.zero_grad(), between steps)."""
-        self.flat.zero_()
-        for p, v in self.views.items():
-            p.grad = v
+        """Start a step: drop the gradients (p.grad = None).  Autograd then
+        hands each parameter a fresh gradient (no zero-fill of the flat buffer,
+        no in-place accumulation into it) and the hook folds it into its view
+        with one copy; parameters that receive no gradient are zeroed at
+        finish().  optimizer.zero_grad(set_to_none=True) is equivalent."""
+        for p in self.views:
+            p.grad = None
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
 
@@ -90,17 +96,36 @@ class GradAllReduce:
         if self.pending[b] == self.buckets[b][2]:
             self._launch(b)
 
+    def _avg_op(self):
+        """RCCL averages in the collective (ReduceOp.AVG: no separate 1/world
+        pass over the buffer); gloo sums and finish() scales."""
+        if not hasattr(self, "_avg"):
+            self._avg = dist.get_backend(self.group) == "nccl"
+        return self._avg
+
     def _launch(self, b):
         s, e, _ = self.buckets[b]
-        if self.cbuf is None:
-            self.handles[b] = dist.all_reduce(self.flat[s:e], group=self.group, async_op=True)
-        else:
-            self.cbuf[s:e].copy_(self.flat[s:e])          # one rounding to the wire dtype
-            self.handles[b] = dist.all_reduce(self.cbuf[s:e], group=self.group, async_op=True)
+        buf = self.flat[s:e]
+        if self.cbuf is not None:
+            self.cbuf[s:e].copy_(buf)          # one rounding to the wire dtype
+            buf = self.cbuf[s:e]
+        if self._avg_op():
+            try:
+                self.handles[b] = dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+                return
+            except (RuntimeError, ValueError):   # a backend build without AVG: sum + scale in finish()
+                if any(h is not None for h in self.handles):
+                    raise
+                self._avg = False
+        self.handles[b] = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finish(self):
         """Wait for every bucket (launching any whose hooks did not all fire,
         e.g. unused parameters) and average over ranks."""
+        for p, v in self.views.items():   # no gradient this step: contributes zeros
+            if p.grad is None:
+                v.zero_()
+                p.grad = v
         for b in range(len(self.buckets)):
             if self.handles[b] is None:
                 self._launch(b)
@@ -113,7 +138,7 @@ class GradAllReduce:
             if p.grad is not None and p.grad is not v and p.grad.data_ptr() != v.data_ptr():
                 raise RuntimeError("GradAllReduce: a gradient left the flat buffer after its hook; "
                                    "zero gradients with GradAllReduce.zero_grad()")
-        if self.world > 1:
+        if self.world > 1 and not self._avg_op():
             self.flat.mul_(1.0 / self.world)
         self.handles = [None] * len(self.buckets)
         self.pending = [0] * len(self.buckets)

@@ -105,3 +105,37 @@ def test_decoder_dp_world2_fused_adam_matches_single_process():
             # sign on one side (<= 2 lr per step); every other element agrees
             assert err.max().item() <= 4 * lr, f"rank {rank} {n}: {err.max().item():.3e}"
             assert (err > 1e-5).float().mean().item() <= 1e-3, f"rank {rank} {n}: too many differing elements"
+
+
+def _nccl_worker(port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mamba-tts-project_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    from mtts.dp import GradAllReduce
+    w = torch.nn.Parameter(torch.randn(300, device="cuda"))
+    b = torch.nn.Parameter(torch.randn(7, device="cuda"))
+    dp = GradAllReduce([w, b], bucket_mb=0.001, first_bucket_mb=0.0005)
+    dp.zero_grad()
+    ((w * 3.0).sum() + (b * b).sum()).backward()
+    dp.finish()
+    ok = torch.allclose(w.grad, torch.full_like(w, 3.0)) and torch.allclose(b.grad, 2 * b.detach())
+    q.put((bool(ok), dp._avg_op(), dist.get_backend()))
+    dist.destroy_process_group()
+
+
+def test_rccl_avg_all_reduce_world1():
+    """The RCCL path of GradAllReduce (backend "nccl" = RCCL): one rank on
+    cuda:0, the buckets all-reduced with ReduceOp.AVG (no separate averaging
+    pass), fresh gradients folded into the flat buffer by the hooks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    ok, avg, backend = q.get(timeout=240)
+    p.join(60)
+    assert p.exitcode == 0
+    assert backend == "nccl" and ok, (ok, avg, backend)
