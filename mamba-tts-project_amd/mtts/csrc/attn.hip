@@ -265,6 +265,177 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(MttsAttnFwdArgs a) {
   }
 }
 
+// Long key side, bf16, 4 waves (128 queries) per workgroup: attn_fwd_kernel
+// with the K / V blocks double-buffered in LDS -- block j+1's rows are loaded
+// into registers before block j's MFMAs and written to the other buffer
+// after them, one barrier per 64-key block instead of a load -> barrier ->
+// compute -> barrier round trip (train.py's 5248-key side: 82 blocks).
+constexpr float kDeferMax = 8.f;
+
+// One 32-key step of the online softmax on a swapped S tile (lane = query
+// row r, 16 keys of half h): mask, running max, P = exp2(c*S - m) in place,
+// l += sum P.  Masking only for tiles that hold padded keys (the mask word
+// is wave-uniform: one scalar test per 32 keys).  Deferred max: the running
+// max m (log2 units) moves only when some row of the wave grows past it by
+// more than kDeferMax, so in the steady state the O accumulators are not
+// touched by VALU (P <= 2^8 before its bf16 rounding; lse = m + log l holds
+// for any m).
+template <int ND>
+__device__ __forceinline__ void softmax_step(f32x16& S, uint32_t mask_word, int h, int lane, float c, float& m,
+                                             float& l, f32x16 (&O)[ND]) {
+  const uint32_t wm = __builtin_amdgcn_readfirstlane(mask_word);
+  if (wm != 0xffffffffu) {
+    const uint32_t w = wm >> (4 * h);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (!((w >> ((i & 3) + 8 * (i >> 2))) & 1u)) S[i] = -INFINITY;
+  }
+  float tmax = S[0];
+#pragma unroll
+  for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, S[i]);
+  tmax = fmaxf(tmax, mtts::xor32(tmax, lane)) * c;
+  if (!__all(tmax <= m + kDeferMax)) {
+    const float mn = fmaxf(m, tmax);
+    const float alpha = exp2_raw(m - (mn == -INFINITY ? 0.f : mn));
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) O[dt][i] *= alpha;
+    m = mn;
+  }
+  const float ms = m == -INFINITY ? 0.f : m;
+  float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) {
+    S[i] = exp2_raw(fmaf(S[i], c, -ms));
+    S[i + 1] = exp2_raw(fmaf(S[i + 1], c, -ms));
+    ps0 += S[i];
+    ps1 += S[i + 1];
+  }
+  l += ps0 + ps1;
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd_db_kernel(MttsAttnFwdArgs a) {
+  constexpr int KP = HD + 8;
+  constexpr int VP = tr_pitch(HD);
+  constexpr int ND = (HD + 31) / 32;
+  constexpr int CH = 8;
+  constexpr int NQ = HD / 16;
+  constexpr int NPF = kKB * HD / CH / 256;   // 16-byte K (and V) chunks per thread per block
+  static_assert(NPF >= 1 && kKB * HD / CH % 256 == 0, "block staging");
+  __shared__ __attribute__((aligned(16))) bf16_t sK[2][kKB * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[2][kKB * VP + 32];
+  __shared__ uint32_t sMask[2][kKB / 32];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int b = blockIdx.z, hh = blockIdx.y;
+  const int q = (blockIdx.x * 4 + wave) * 32 + r;
+  const bool qv = q < a.q_len;
+  const bf16_t* qp = (const bf16_t*)a.q + b * a.q_bs + (int64_t)(qv ? q : 0) * a.q_ls + hh * HD;
+  const bf16_t* kbase = (const bf16_t*)a.k + b * a.k_bs + hh * HD;
+  const bf16_t* vbase = (const bf16_t*)a.v + b * a.v_bs + hh * HD;
+  const uint8_t* mb = a.key_padding_mask ? a.key_padding_mask + b * a.mask_bs : nullptr;
+  const float c = a.scale * kLog2e;
+
+  s16x8 QF[NQ];
+#pragma unroll
+  for (int s = 0; s < NQ; ++s) QF[s] = qv ? *(const s16x8*)(qp + 16 * s + 8 * h) : s16x8{};
+
+  // Loads are issued unconditionally and consumed only in put(): a select or
+  // branch on the loaded data in fetch() would make the compiler wait for
+  // them before the block's MFMAs, which is exactly what this kernel avoids.
+  f32x4 pk[NPF], pv[NPF];
+  uint32_t praw = 0;
+  int pk0 = 0;
+  const uint8_t* mbase = mb ? mb : (const uint8_t*)kbase;
+  auto fetch = [&](int k0) __attribute__((always_inline)) {
+    pk0 = k0;
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / (HD / CH), cc = (idx % (HD / CH)) * CH;
+      const int kc = min(k0 + row, a.kv_len - 1);
+      pk[i] = *(const f32x4*)(kbase + kc * a.k_ls + cc);
+      pv[i] = *(const f32x4*)(vbase + kc * a.v_ls + cc);
+    }
+    praw = mbase[mb ? min(k0 + lane, a.kv_len - 1) : 0];
+  };
+  auto put = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / (HD / CH), cc = (idx % (HD / CH)) * CH;
+      const bool in = pk0 + row < a.kv_len;
+      *(f32x4*)(sK[buf] + row * KP + cc) = in ? pk[i] : f32x4{};
+      *(f32x4*)(sV[buf] + row * VP + cc) = in ? pv[i] : f32x4{};
+    }
+    const bool ok = pk0 + lane < a.kv_len && !(mb && praw);
+    const uint64_t bal = __ballot(ok);
+    if (tid == 0) {
+      sMask[buf][0] = (uint32_t)bal;
+      sMask[buf][1] = (uint32_t)(bal >> 32);
+    }
+  };
+
+  float m = -INFINITY, l = 0.f;
+  f32x16 O[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) O[dt] = f32x16{};
+  const int nblk = (a.kv_len + kKB - 1) / kKB;
+  if (nblk > 0) {
+    fetch(0);
+    put(0);
+  }
+  __syncthreads();
+  for (int j = 0; j < nblk; ++j) {
+    const int buf = j & 1, k0 = j * kKB;
+    fetch(min(k0 + kKB, (nblk - 1) * kKB));   // in flight under this block's math
+#pragma unroll
+    for (int t = 0; t < kKB / 32; ++t) {
+      if (k0 + t * 32 >= a.kv_len) break;
+      f32x16 S = {};
+      const bf16_t* kr = sK[buf] + (t * 32 + r) * KP + 8 * h;
+#pragma unroll
+      for (int s = 0; s < NQ; ++s) S = mfma_bf16(*(const s16x8*)(kr + 16 * s), QF[s], S);
+      softmax_step<ND>(S, sMask[buf][t], h, lane, c, m, l, O);
+      const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const s16x8 pb = pack8(S, s);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          const bf16_t* p0 = sV[buf] + (t * 32 + 16 * s + 4 * h + qq) * VP + dt * 32 + 16 * g + 4 * pp;
+          O[dt] = mfma_bf16(cat(tr_read(p0), tr_read(p0 + 8 * VP)), pb, O[dt]);
+        }
+      }
+    }
+    if (j + 1 < nblk) put(buf ^ 1);
+    __syncthreads();
+  }
+
+  const float lt = mtts::sum_xor32(l);
+  const float inv = 1.f / lt;  // fully masked: 0 * inf = NaN (torch MHA)
+  if (qv) {
+    bf16_t* op = (bf16_t*)a.out + b * a.o_bs + (int64_t)q * a.o_ls + hh * HD;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = dt * 32 + 8 * g4 + 4 * h;
+        if (d0 < HD) {
+          s16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = bfbits(O[dt][4 * g4 + e] * inv);
+          *(s16x4*)(op + d0) = v;
+        }
+      }
+    if (a.lse && h == 0) a.lse[((int64_t)b * a.heads + hh) * a.q_len + q] = (m + __builtin_amdgcn_logf(lt)) * kLn2;
+  }
+}
+
 // Short key side (kv_len <= 128, bf16: C2's 128 text keys): the whole K / V
 // of the (batch, head) staged in LDS ONCE per workgroup (one barrier), then
 // every wave runs NSL 32-query slices back to back with no further barrier,
@@ -340,30 +511,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_short_kernel(MttsAttnFwdArgs 
       const bf16_t* kr = sK + (t * 32 + r) * KP + 8 * h;
 #pragma unroll
       for (int s = 0; s < NQ; ++s) S = mfma_bf16(*(const s16x8*)(kr + 16 * s), QF[s], S);
-      const uint32_t w = sMask[t] >> (4 * h);
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const bool ok = (w >> ((i & 3) + 8 * (i >> 2))) & 1u;
-        S[i] = ok ? S[i] * c : -INFINITY;
-        tmax = fmaxf(tmax, S[i]);
-      }
-      tmax = fmaxf(tmax, mtts::xor32(tmax, lane));
-      const float mn = fmaxf(m, tmax);
-      const float ms = mn == -INFINITY ? 0.f : mn;
-      const float alpha = exp2_raw(m - ms);
-      float ps = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        S[i] = exp2_raw(S[i] - ms);
-        ps += S[i];
-      }
-      l = l * alpha + ps;
-      m = mn;
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) O[dt][i] *= alpha;
+      softmax_step<ND>(S, sMask[t], h, lane, c, m, l, O);
       const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -938,6 +1086,13 @@ void launch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
   }
   const int nw = a->q_len >= 128 ? 4 : (a->q_len + 31) / 32;
   dim3 grid((a->q_len + 32 * nw - 1) / (32 * nw), a->heads, a->batch);
+  if constexpr (sizeof(T) == 2 && HD >= 32) {
+    const char* e = getenv("MTTS_ATTN_FWD_DB");
+    if (nw == 4 && (!e || atoi(e) != 0)) {
+      attn_fwd_db_kernel<HD><<<grid, 256, 0, st>>>(*a);
+      return;
+    }
+  }
   attn_fwd_kernel<T, HD><<<grid, 64 * nw, 0, st>>>(*a);
 }
 

@@ -21,8 +21,10 @@ def timed(fn, it=20):
     return e[0].elapsed_time(e[1]) / it
 
 
-for name, (B, T, S) in {"C2": (8, 2048, 128), "C5": (4, 5120, 5248)}.items():
-    H, hd = 8, 128
+SHAPES = {"C2": (8, 2048, 128, 128), "C5": (4, 5120, 5248, 128), "C5m": (8, 5120, 5248, 64)}
+for name in os.environ.get("SHAPES", "C2,C5,C5m").split(","):
+    B, T, S, hd = SHAPES[name]
+    H = 8
     d = H * hd
     g = torch.Generator(device="cuda").manual_seed(0)
     q = torch.randn(B, T, d, device="cuda", generator=g).to(torch.bfloat16)
@@ -35,6 +37,13 @@ for name, (B, T, S) in {"C2": (8, 2048, 128), "C5": (4, 5120, 5248)}.items():
     fl = 4 * B * T * S * d
     tf = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
     print(f"{name} fwd {tf * 1e3:.1f} us {fl / tf / 1e9:.0f} TF/s", flush=True)
+    if name != "C2":
+        os.environ["MTTS_ATTN_FWD_DB"] = "0"
+        tf0 = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
+        o0, l0 = A.attention_fwd(q, k, v, H, kpm, want_lse=True)
+        os.environ.pop("MTTS_ATTN_FWD_DB")
+        print(f"{name} fwd single-buffered {tf0 * 1e3:.1f} us {fl / tf0 / 1e9:.0f} TF/s; max|diff| out "
+              f"{(o0.float() - out.float()).abs().max().item():.2e} lse {(l0 - lse).abs().max().item():.2e}", flush=True)
     if name == "C2":
         os.environ["MTTS_ATTN_FWD_SHORT"] = "0"
         tf0 = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
