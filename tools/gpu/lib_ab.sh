@@ -1,12 +1,8 @@
 #!/bin/bash
-# A/B of a diag library build against the default one, alternated:
-#   tools/gpu/lib_ab.sh NAME "<python command>" [rounds]
+# op A/B of two builds of libmtts.so: $ALT (path) vs the in-tree library; CMD = python script + args
 set -e -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-for i in $(seq ${3:-3}); do
-  echo "== round $i base"
-  timeout -k 10 150 $2
-  echo "== round $i $1"
-  MTTS_LIB=$GRAFT_REPO_ROOT/mamba-tts-project_amd/mtts/libmtts_$1.so timeout -k 10 150 $2
+for i in 1 2; do
+  echo "== in-tree"; timeout -k 10 300 python -u $CMD 2>&1 | grep -v amdgpu.ids
+  echo "== $ALT"; MTTS_LIB=$ALT timeout -k 10 300 python -u $CMD 2>&1 | grep -v amdgpu.ids
 done
