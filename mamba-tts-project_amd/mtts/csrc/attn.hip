@@ -761,9 +761,11 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
             dK[dt] = mfma_bf16(da, cat(tr_read(pq), tr_read(pq + 8 * P)), dK[dt]);
           }
         }
-        // dS^T image: lane (key) stores query rows 8g4+4h..+3
+        // dS^T image: lane (key) stores query rows 8g4+4h..+3 (read by the dQ
+        // product only: not in the dK/dV pass)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
+          if constexpr (MODE == kBwdKV) break;
           s16x4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = bfbits(D[4 * g4 + e]);
@@ -784,7 +786,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
         }
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4)
-          *(f32x4*)((float*)sS + key * PS + 8 * g4 + 4 * h) =
+          if constexpr (MODE != kBwdKV) *(f32x4*)((float*)sS + key * PS + 8 * g4 + 4 * h) =
               f32x4{D[4 * g4], D[4 * g4 + 1], D[4 * g4 + 2], D[4 * g4 + 3]};
       }
       if constexpr (MODE == kBwdKV) continue;   // dQ comes from the mode-2 launch
@@ -889,24 +891,41 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
 }
 
 // Long key side, bf16, dQ pass (replaces mode 2 for hd 64 / 128): a
-// workgroup owns 128 queries, one 32-query slice per WAVE (so every staged
-// key group feeds 4x the MFMAs of mode 2's key-split waves).  Q and dO stay
-// in registers as MFMA A fragments for the whole sweep; per key group of 128
-// (K / V images in LDS, shared by the waves) and per 32-key tile:
-//   S = Q K^T - lse/scale, dP = dO V^T - delta  (query rows, key on the lane)
-//   P = exp2(c S) (masked keys 0), dS = P dP -> the wave's own dS^T image ->
-//   dQ += dS K  (transposed LDS reads of dS^T and K), in registers.
-// delta = rowsum(dO * O) is computed once per query and written for the
-// dK/dV pass (mode 1).
+// workgroup owns 128 queries, one 32-query slice per WAVE; Q and dO stay in
+// registers as MFMA B fragments for the whole sweep.  Everything is computed
+// TRANSPOSED (query on the lane, keys / dims in registers), so dS never
+// leaves registers:
+//   S^T = K Q^T - lse/scale, dP^T = V dO^T - delta   (key rows, query lane)
+//   P = exp2(c S) (masked keys 0), dS^T = P dP^T
+//   dQ^T += K^T dS^T  (K^T by transposed LDS reads; dS^T's accumulator
+//                      registers are directly the B operand, see pack8)
+// K / V blocks of 64 keys are double-buffered in LDS (kimg layout: row and
+// transposed reads conflict-free), block j+1 loaded into registers under
+// block j's MFMAs, one barrier per block.  delta = rowsum(dO * O) is
+// computed once per query and written for the dK/dV pass (mode 1).
+// One LDS image of a bf16 [rows][HD] tile for BOTH row reads (ds_read_b128
+// of 16-byte chunk ch) and transposed reads (ds_read_b64_tr_b16 of 4 rows x
+// 16 columns): unpadded rows, 16-byte chunk index XORed with a function of
+// the row.  Row reads: the 8 (HD 64: same-parity) rows of a 16-lane phase hit
+// distinct chunks; transposed reads: 4 consecutive rows x 4 chunks land on
+// 16 distinct 4-bank groups.
+template <int HD>
+__device__ __forceinline__ int kswz(int row) {
+  if constexpr (HD == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+}
+template <int HD>
+__device__ __forceinline__ int kimg(int row, int ch) { return row * HD + 8 * (ch ^ kswz<HD>(row)); }
+
 template <int HD>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
-  constexpr int KG = 128, P = HD + 8, PS = 32;
+  static_assert(HD == 64 || HD == 128, "dq kernel head dims");
+  constexpr int KB = 64;
   constexpr int NQ = HD / 16, ND = HD / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t sK[KG * P + 32];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[KG * P + 32];
-  __shared__ __attribute__((aligned(16))) bf16_t sS[4][32 * PS + 32];
-  __shared__ float sLq[4][32], sDq[4][32];
-  __shared__ uint32_t sMask[KG / 32];
+  constexpr int NPF = KB * HD / 8 / 256;   // 16-byte K (and V) chunks per thread per block
+  __shared__ __attribute__((aligned(16))) bf16_t sK[2][KB * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[2][KB * HD];
+  __shared__ uint32_t sMask[2][KB / 32];
   const MttsAttnBwdArgs& a = p.a;
   const MttsAttnFwdArgs& f = a.f;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -919,7 +938,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   const bf16_t* qb = (const bf16_t*)f.q + b * f.q_bs + hh * HD;
   const bf16_t* gb = (const bf16_t*)a.dout + b * a.do_bs + hh * HD;
   const bf16_t* ob = (const bf16_t*)f.out + b * f.o_bs + hh * HD;
-  // ---- A fragments of Q / dO (query row r, dims 16s + 8h .. +7), delta, -lse/scale
+  const bf16_t* kbase = (const bf16_t*)f.k + b * f.k_bs + hh * HD;
+  const bf16_t* vbase = (const bf16_t*)f.v + b * f.v_bs + hh * HD;
+  // ---- B fragments of Q^T / dO^T (query r, dims 16s + 8h .. +7), delta, -lse/scale
   const int qi = q0 + r;
   const bool qv = qi < f.q_len;
   s16x8 Qf[NQ], Gf[NQ];
@@ -933,100 +954,290 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
     for (int e = 0; e < 8; ++e) dl += mtts::bf2f((bf16_t)Gf[s][e]) * mtts::bf2f((bf16_t)o8[e]);
   }
   dl += __shfl_xor(dl, 32);
-  if (h == 0) {
-    float L = 0.f;
-    if (qv) {
-      L = -f.lse[((int64_t)b * f.heads + hh) * f.q_len + qi] * inv_scale;
-      p.delta[((int64_t)b * f.heads + hh) * f.q_len + qi] = -dl;
-    }
-    sLq[wave][r] = L;
-    sDq[wave][r] = qv ? -dl : 0.f;
+  float Lq = 0.f;
+  if (qv) {
+    Lq = -f.lse[((int64_t)b * f.heads + hh) * f.q_len + qi] * inv_scale;
+    if (h == 0) p.delta[((int64_t)b * f.heads + hh) * f.q_len + qi] = -dl;
   }
-  __syncthreads();
-  float Lr[16], Dr[16];
+  const float Dq = qv ? -dl : 0.f;
+
+  // lane-constant offsets (elements) into the kimg images: A-fragment row
+  // reads (key r, chunk 2s + h) and K^T transposed reads (keys 4h + qq
+  // (+8) of a 16-key step, dims of tile dt); a tile base that is a multiple
+  // of 16 rows leaves the swizzle unchanged
+  int oR[NQ], oT[2][ND];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    Lr[i] = sLq[wave][acc_row(i, h)];
-    Dr[i] = sDq[wave][acc_row(i, h)];
-  }
+  for (int s = 0; s < NQ; ++s) oR[s] = kimg<HD>(r, 2 * s + h);
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) oT[u][dt] = kimg<HD>(4 * h + qq + 8 * u, 4 * dt + 2 * g + (pp >> 1)) + 4 * (pp & 1);
+
+  // block staging: loads issued unconditionally, consumed only in put()
+  f32x4 pk[NPF], pv[NPF];
+  uint32_t praw = 0;
+  int pk0 = 0;
+  const uint8_t* mbase = mb ? mb : (const uint8_t*)kbase;
+  auto fetch = [&](int k0) __attribute__((always_inline)) {
+    pk0 = k0;
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / (HD / 8), cc = (idx % (HD / 8)) * 8;
+      const int kc = min(k0 + row, f.kv_len - 1);
+      pk[i] = *(const f32x4*)(kbase + (int64_t)kc * f.k_ls + cc);
+      pv[i] = *(const f32x4*)(vbase + (int64_t)kc * f.v_ls + cc);
+    }
+    praw = mbase[mb ? min(k0 + lane, f.kv_len - 1) : 0];
+  };
+  auto put = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / (HD / 8), ch = idx % (HD / 8);
+      const bool in = pk0 + row < f.kv_len;
+      *(f32x4*)(sK[buf] + kimg<HD>(row, ch)) = in ? pk[i] : f32x4{};
+      *(f32x4*)(sV[buf] + kimg<HD>(row, ch)) = in ? pv[i] : f32x4{};
+    }
+    const bool ok = pk0 + lane < f.kv_len && !(mb && praw);
+    const uint64_t bal = __ballot(ok);
+    if (tid == 0) {
+      sMask[buf][0] = (uint32_t)bal;
+      sMask[buf][1] = (uint32_t)(bal >> 32);
+    }
+  };
+
   f32x16 QA[ND];
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) QA[dt] = f32x16{};
-  const int nkg = (f.kv_len + KG - 1) / KG;
-  const bf16_t* kb = (const bf16_t*)f.k + b * f.k_bs + hh * HD;
-  const bf16_t* vb = (const bf16_t*)f.v + b * f.v_bs + hh * HD;
-  bf16_t* sSw = sS[wave];
-  for (int kg = 0; kg < nkg; ++kg) {
-    const int kg0 = kg * KG;
-    __syncthreads();  // previous key group's images consumed
-    for (int i = tid; i < KG * HD / 8; i += 256) {
-      const int row = i / (HD / 8), cc = (i % (HD / 8)) * 8;
-      const int key = kg0 + row;
-      f32x4 kv = {}, vv = {};
-      if (key < f.kv_len) {
-        kv = *(const f32x4*)(kb + (int64_t)key * f.k_ls + cc);
-        vv = *(const f32x4*)(vb + (int64_t)key * f.v_ls + cc);
-      }
-      *(f32x4*)(sK + row * P + cc) = kv;
-      *(f32x4*)(sV + row * P + cc) = vv;
-    }
-    if (wave < KG / 64) {
-      const int key = kg0 + 64 * wave + lane;
-      const bool ok = key < f.kv_len && !(mb && mb[key]);
-      const uint64_t bal = __ballot(ok);
-      if (lane == 0) {
-        sMask[2 * wave] = (uint32_t)bal;
-        sMask[2 * wave + 1] = (uint32_t)(bal >> 32);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kt = 0; kt < KG / 32; ++kt) {
+  const int nblk = (f.kv_len + KB - 1) / KB;
+  if (nblk > 0) {
+    fetch(0);
+    put(0);
+  }
+  __syncthreads();
+  // hd 128: the next block's 32 staging registers do not fit beside Q / dO /
+  // dQ (256 VGPRs); it is loaded after this block's math instead
+  constexpr bool kPrefetch = HD == 64;
+  for (int j = 0; j < nblk; ++j) {
+    const int buf = j & 1, k0 = j * KB;
+    if constexpr (kPrefetch) fetch(min(k0 + KB, (nblk - 1) * KB));   // in flight under this block's math
+#pragma unroll(kPrefetch ? 2 : 1)
+    for (int t = 0; t < KB / 32; ++t) {
+      if (k0 + t * 32 >= f.kv_len) break;
+      const bf16_t* kt = sK[buf] + t * 32 * HD;
+      const bf16_t* vt = sV[buf] + t * 32 * HD;
       f32x16 S, D;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        S[i] = Lr[i];
-        D[i] = Dr[i];
+        S[i] = Lq;
+        D[i] = Dq;
       }
-      const bf16_t* kr = sK + (kt * 32 + r) * P + 8 * h;
-      const bf16_t* vr = sV + (kt * 32 + r) * P + 8 * h;
 #pragma unroll
       for (int s = 0; s < NQ; ++s) {
-        S = mfma_bf16(Qf[s], *(const s16x8*)(kr + 16 * s), S);
-        D = mfma_bf16(Gf[s], *(const s16x8*)(vr + 16 * s), D);
+        S = mfma_bf16(*(const s16x8*)(kt + oR[s]), Qf[s], S);
+        D = mfma_bf16(*(const s16x8*)(vt + oR[s]), Gf[s], D);
       }
-      const bool kvalid = (sMask[kt] >> r) & 1u;
+      const uint32_t wm = __builtin_amdgcn_readfirstlane(sMask[buf][t]);
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        s16x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g4 + e;
-          const float pv = kvalid ? exp2_raw(c * S[i]) : 0.f;
-          v[e] = bfbits(pv * D[i]);                    // dS (unscaled), bf16
-        }
-        *(s16x4*)(sSw + r * PS + 8 * g4 + 4 * h) = v;  // dS^T [key][query]
+      for (int i = 0; i < 16; ++i) {
+        float pr = exp2_raw(c * S[i]);
+        if (wm != 0xffffffffu) pr = ((wm >> acc_row(i, h)) & 1u) ? pr : 0.f;
+        S[i] = pr * D[i];   // dS^T (unscaled)
       }
-      // dQ[q][dims] += dS[q][32 keys of tile kt] K[keys][dims]
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16_t* ps = sSw + (16 * s + 8 * h + qq) * PS + 16 * g + 4 * pp;
-        const s16x8 A = cat(tr_read(ps), tr_read(ps + 4 * PS));
+        const s16x8 pb = pack8(S, s);
+        const bf16_t* ks = kt + 16 * s * HD;
 #pragma unroll
-        for (int dt = 0; dt < ND; ++dt) {
-          const bf16_t* pk = sK + (kt * 32 + 16 * s + 8 * h + qq) * P + dt * 32 + 16 * g + 4 * pp;
-          QA[dt] = mfma_bf16(A, cat(tr_read(pk), tr_read(pk + 4 * P)), QA[dt]);
-        }
+        for (int dt = 0; dt < ND; ++dt)
+          QA[dt] = mfma_bf16(cat(tr_read(ks + oT[0][dt]), tr_read(ks + oT[1][dt])), pb, QA[dt]);
       }
     }
+    if (j + 1 < nblk) {
+      if constexpr (!kPrefetch) fetch(k0 + KB);
+      put(buf ^ 1);
+    }
+    __syncthreads();
   }
+  // ---- dQ^T tile dt: lane = query, registers = dims dt*32 + acc_row(i, h)
+  if (qv) {
+    bf16_t* dqp = (bf16_t*)a.dq + b * a.dq_bs + (int64_t)qi * a.dq_ls + hh * HD;
+    const bool vec = ((uintptr_t)dqp & 7) == 0;
 #pragma unroll
-  for (int dt = 0; dt < ND; ++dt) {
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = dt * 32 + 8 * g4 + 4 * h;
+        s16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = bfbits(QA[dt][4 * g4 + e] * f.scale);
+        if (vec) {
+          *(s16x4*)(dqp + d0) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dqp[d0 + e] = (bf16_t)v[e];
+        }
+      }
+  }
+}
+
+// Long key side, bf16 hd 64, dK / dV pass (replaces mode 1): a workgroup
+// owns 128 keys, 32 per wave, and sweeps the queries of its chunk in 32-query
+// slices.  The wave's K / V rows stay in registers as MFMA B fragments (they
+// are the same for every slice); a slice's Q / dO rows are staged ONCE per
+// workgroup in LDS (kimg layout: A-fragment row reads and the transposed
+// reads of the dV / dK products are both conflict-free), double-buffered with
+// the next slice loaded into registers under this one's MFMAs: one barrier
+// per slice.
+//   S = Q K^T - lse/scale, dP = dO V^T - delta     (query rows, key lane)
+//   P = exp2(c S) (masked keys 0), dS = P dP
+//   dV += P^T dO, dK += dS^T Q   (the accumulators' registers as A operands)
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(BwdParams p) {
+  static_assert(HD == 64, "kv kernel: hd 64 (its K / V / dK / dV registers)");
+  constexpr int KG = 128, NQ = HD / 16, ND = HD / 32;
+  constexpr int QS = 32;                   // queries per staged slice
+  constexpr int NPF = QS * HD / 8 / 256;   // 16-byte Q (and dO) chunks per thread per slice
+  static_assert(NPF >= 1, "slice staging");
+  __shared__ __attribute__((aligned(16))) bf16_t sQ[2][QS * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t sG[2][QS * HD];
+  __shared__ __attribute__((aligned(16))) float sL[2][QS], sD[2][QS];
+  const MttsAttnBwdArgs& a = p.a;
+  const MttsAttnFwdArgs& f = a.f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int b = blockIdx.z, hh = blockIdx.y;
+  const int d = f.heads * HD;
+  const int nkg = (f.kv_len + KG - 1) / KG;
+  const int kg = blockIdx.x % nkg, qc = blockIdx.x / nkg;
+  const int qbeg = qc * p.qchunk, qend = min(f.q_len, qbeg + p.qchunk);
+  const float c = f.scale * kLog2e, inv_scale = 1.f / f.scale;
+  const uint8_t* mb = f.key_padding_mask ? f.key_padding_mask + b * f.mask_bs : nullptr;
+  const float* dbuf = p.delta + ((int64_t)b * f.heads + hh) * f.q_len;
+  const float* lbuf = f.lse + ((int64_t)b * f.heads + hh) * f.q_len;
+  const bf16_t* qb = (const bf16_t*)f.q + b * f.q_bs + hh * HD;
+  const bf16_t* gb = (const bf16_t*)a.dout + b * a.do_bs + hh * HD;
+
+  // ---- this lane's key: B fragments of K / V (dims 16s + 8h .. +7), mask
+  const int key = kg * KG + wave * 32 + r;
+  const bool kin = key < f.kv_len;
+  const bool kvalid = kin && !(mb && mb[key]);
+  s16x8 Kf[NQ], Vf[NQ];
+  {
+    const bf16_t* kr = (const bf16_t*)f.k + b * f.k_bs + (int64_t)(kin ? key : 0) * f.k_ls + hh * HD;
+    const bf16_t* vr = (const bf16_t*)f.v + b * f.v_bs + (int64_t)(kin ? key : 0) * f.v_ls + hh * HD;
+#pragma unroll
+    for (int s = 0; s < NQ; ++s) {
+      Kf[s] = kin ? *(const s16x8*)(kr + 16 * s + 8 * h) : s16x8{};
+      Vf[s] = kin ? *(const s16x8*)(vr + 16 * s + 8 * h) : s16x8{};
+    }
+  }
+  // lane-constant image offsets: A-fragment rows (query r, chunk 2s + h) and
+  // the transposed B reads (queries 4h + qq (+8) of a 16-query step, dims of tile dt)
+  int oR[NQ], oT[2][ND];
+#pragma unroll
+  for (int s = 0; s < NQ; ++s) oR[s] = kimg<HD>(r, 2 * s + h);
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) oT[u][dt] = kimg<HD>(4 * h + qq + 8 * u, 4 * dt + 2 * g + (pp >> 1)) + 4 * (pp & 1);
+
+  // ---- slice staging: loads issued unconditionally (clamped), consumed in put()
+  f32x4 pq[NPF], pg[NPF];
+  float pl = 0.f, pd = 0.f;
+  int ps0 = qbeg;
+  auto fetch = [&](int q0) __attribute__((always_inline)) {
+    ps0 = q0;
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / (HD / 8), cc = (idx % (HD / 8)) * 8;
+      const int qc_ = min(q0 + row, qend - 1);
+      pq[i] = *(const f32x4*)(qb + (int64_t)qc_ * f.q_ls + cc);
+      pg[i] = *(const f32x4*)(gb + (int64_t)qc_ * a.do_ls + cc);
+    }
+    const int ql = min(q0 + (tid & (QS - 1)), qend - 1);
+    pl = lbuf[ql];
+    pd = dbuf[ql];
+  };
+  auto put = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / (HD / 8), ch = idx % (HD / 8);
+      const bool in = ps0 + row < qend;
+      *(f32x4*)(sQ[buf] + kimg<HD>(row, ch)) = in ? pq[i] : f32x4{};
+      *(f32x4*)(sG[buf] + kimg<HD>(row, ch)) = in ? pg[i] : f32x4{};
+    }
+    if (tid < QS) {
+      const bool in = ps0 + tid < qend;
+      sL[buf][tid] = in ? -pl * inv_scale : 0.f;   // P = exp2(c (S + L))
+      sD[buf][tid] = in ? pd : 0.f;
+    }
+  };
+
+  f32x16 dK[ND], dV[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) dK[dt] = dV[dt] = f32x16{};
+  const int nsl = qend > qbeg ? (qend - qbeg + QS - 1) / QS : 0;
+  if (nsl > 0) {
+    fetch(qbeg);
+    put(0);
+  }
+  __syncthreads();
+  for (int j = 0; j < nsl; ++j) {
+    const int buf = j & 1, q0 = qbeg + QS * j;
+    fetch(min(q0 + QS, qbeg + QS * (nsl - 1)));   // in flight under this slice's math
+    const bf16_t* qs = sQ[buf];
+    const bf16_t* gs = sG[buf];
+    f32x16 S, D;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int qo = q0 + acc_row(i, h);
-      if (qo < f.q_len)
-        mtts::stf((bf16_t*)a.dq + b * a.dq_bs + (int64_t)qo * a.dq_ls + hh * HD + dt * 32 + r, QA[dt][i] * f.scale);
+      S[i] = sL[buf][acc_row(i, h)];
+      D[i] = sD[buf][acc_row(i, h)];
+    }
+#pragma unroll
+    for (int s = 0; s < NQ; ++s) {
+      S = mfma_bf16(*(const s16x8*)(qs + oR[s]), Kf[s], S);
+      D = mfma_bf16(*(const s16x8*)(gs + oR[s]), Vf[s], D);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      S[i] = kvalid ? exp2_raw(c * S[i]) : 0.f;  // P
+      D[i] = S[i] * D[i];                         // dS (unscaled)
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const s16x8 pa = pack8(S, s), da = pack8(D, s);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        const int o0 = 16 * s * HD + oT[0][dt], o1 = 16 * s * HD + oT[1][dt];
+        dV[dt] = mfma_bf16(pa, cat(tr_read(gs + o0), tr_read(gs + o1)), dV[dt]);
+        dK[dt] = mfma_bf16(da, cat(tr_read(qs + o0), tr_read(qs + o1)), dK[dt]);
+      }
+    }
+    if (j + 1 < nsl) put(buf ^ 1);
+    __syncthreads();
+  }
+  // ---- dK (scaled), dV: rows = keys (registers), cols = dims (lanes)
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) {
+    const int dim = dt * 32 + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = kg * KG + wave * 32 + acc_row(i, h);
+      if (kk >= f.kv_len) continue;
+      const float vk = dK[dt][i] * f.scale, vv = dV[dt][i];
+      if (p.nchunk > 1) {
+        float* pr = p.part + (((int64_t)qc * f.batch + b) * f.kv_len + kk) * (2 * d) + hh * HD + dim;
+        pr[0] = vk;
+        pr[d] = vv;
+      } else {
+        mtts::stf((bf16_t*)a.dk + b * a.dk_bs + (int64_t)kk * a.dk_ls + hh * HD + dim, vk);
+        mtts::stf((bf16_t*)a.dv + b * a.dv_bs + (int64_t)kk * a.dv_ls + hh * HD + dim, vv);
+      }
     }
   }
 }
@@ -1370,6 +1581,12 @@ void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
         attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
     } else {
       attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
+    }
+    if constexpr (std::is_same<T, bf16_t>::value && HD == 64) {
+      if (!getenv("MTTS_ATTN_KV_V1")) {
+        attn_bwd_kv_kernel<HD><<<dim3((f.kv_len + 127) / 128 * p.nchunk, f.heads, f.batch), 256, 0, st>>>(p);
+        return;
+      }
     }
     attn_bwd_kernel<T, HD, kBwdKV><<<dim3((f.kv_len + KG - 1) / KG * p.nchunk, f.heads, f.batch), NT, 0, st>>>(p);
     return;

@@ -219,20 +219,24 @@ def test_north_star_shape_bf16():
     close(dkv[:2], rkv, 3e-2)
 
 
-@pytest.mark.parametrize("path", ["split", "split_dq_v1", "fused"])
+@pytest.mark.parametrize("path", ["split", "split_dq_v1", "split_kv_v1", "fused"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", [(1, 100, 1100, 2, 128), (2, 64, 777, 4, 64), (2, 33, 129, 2, 32),
-                                  (1, 300, 260, 2, 128)])
+                                  (1, 300, 260, 2, 128), (1, 300, 700, 2, 64), (2, 160, 300, 8, 64)])
 def test_backward_long_key_side(case, dtype, path, monkeypatch):
     """Key side longer than one key group (the train.py shape: 5k reference
     keys): the split backward (dQ launch -- wave-per-query-slice kernel for
     bf16 hd 64/128, or the key-split mode-2 kernel (MTTS_ATTN_DQ_V1) -- then
-    the per-key-group dK/dV launch) and the fused chunked one
+    the per-key-group dK/dV launch: register-resident K / V kernel for bf16
+    hd 64, or mode 1 (MTTS_ATTN_KV_V1); (1, 300, 700, 2, 64) runs it over
+    query chunks into partials) and the fused chunked one
     (MTTS_ATTN_BWD_FUSED) all match."""
     if path == "fused":
         monkeypatch.setenv("MTTS_ATTN_BWD_FUSED", "1")
     if path == "split_dq_v1":
         monkeypatch.setenv("MTTS_ATTN_DQ_V1", "1")
+    if path == "split_kv_v1":
+        monkeypatch.setenv("MTTS_ATTN_KV_V1", "1")
     B, T, S, H, hd = case
     q, kv, kpm = make(B, T, S, H, hd, dtype, seed=5)
     o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
@@ -242,11 +246,12 @@ def test_backward_long_key_side(case, dtype, path, monkeypatch):
     close(dkv, rkv, tol)
 
 
-def test_backward_c5_shape_bf16():
+@pytest.mark.parametrize("hd", [128, 64])
+def test_backward_c5_shape_bf16(hd):
     """train.py decoder shape: T_audio = 5120 queries, 5120 reference keys +
-    128 text keys, d=1024, H=8 (reference gradients on a query subset via
-    the full-key float64 restatement of one batch)."""
-    B, T, S, H, hd = 1, 5120, 5248, 8, 128
+    128 text keys, H=8, d = 1024 or train.py's 512 (reference gradients of
+    one batch by the full-key float64 restatement)."""
+    B, T, S, H = 1, 5120, 5248, 8
     q, kv, kpm = make(B, T, S, H, hd, torch.bfloat16, seed=13)
     o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
     assert torch.isfinite(dq).all() and torch.isfinite(dkv).all()

@@ -4,7 +4,7 @@ import csv
 import sys
 from collections import defaultdict
 
-files = [a for a in sys.argv[1:] if not a.startswith("--")]
+files = [a for a in sys.argv[1:] if a.endswith(".csv")]
 match = sys.argv[sys.argv.index("--match") + 1] if "--match" in sys.argv else None
 tot = defaultdict(lambda: defaultdict(float))
 calls = defaultdict(set)
