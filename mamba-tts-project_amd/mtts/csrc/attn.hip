@@ -316,33 +316,57 @@ __device__ __forceinline__ void softmax_step(f32x16& S, uint32_t mask_word, int 
   l += ps0 + ps1;
 }
 
+// One LDS image of a bf16 [rows][HD] tile for BOTH row reads (ds_read_b128
+// of 16-byte chunk ch) and transposed reads (ds_read_b64_tr_b16 of 4 rows x
+// 16 columns): unpadded rows, 16-byte chunk index XORed with a function of
+// the row.  Row reads: the 8 (HD 64: same-parity) rows of a 16-lane phase hit
+// distinct chunks; transposed reads: 4 consecutive rows x 4 chunks land on
+// 16 distinct 4-bank groups.
 template <int HD>
+__device__ __forceinline__ int kswz(int row) {
+  if constexpr (HD == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+}
+template <int HD>
+__device__ __forceinline__ int kimg(int row, int ch) { return row * HD + 8 * (ch ^ kswz<HD>(row)); }
+
+// QT = query tiles of 32 per wave: with 2 (hd <= 64) every K / V fragment
+// read from LDS feeds two MFMAs, halving the LDS bytes per MFMA.
+template <int HD, int QT>
 __global__ __launch_bounds__(256) void attn_fwd_db_kernel(MttsAttnFwdArgs a) {
-  constexpr int KP = HD + 8;
-  constexpr int VP = tr_pitch(HD);
+  // hd 64 / 128: K and V in the unpadded swizzled kimg image (row reads of K,
+  // transposed reads of V, both conflict-free; 32 KiB per workgroup at hd 64
+  // instead of 43, so 4 workgroups fit a CU); other head dims padded pitches
+  constexpr bool SWZ = HD == 64 || HD == 128;
+  constexpr int KP = SWZ ? HD : HD + 8;
+  constexpr int VP = SWZ ? HD : tr_pitch(HD);
   constexpr int ND = (HD + 31) / 32;
   constexpr int CH = 8;
   constexpr int NQ = HD / 16;
   constexpr int NPF = kKB * HD / CH / 256;   // 16-byte K (and V) chunks per thread per block
   static_assert(NPF >= 1 && kKB * HD / CH % 256 == 0, "block staging");
   __shared__ __attribute__((aligned(16))) bf16_t sK[2][kKB * KP];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[2][kKB * VP + 32];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[2][kKB * VP + (SWZ ? 0 : 32)];
   __shared__ uint32_t sMask[2][kKB / 32];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int b = blockIdx.z, hh = blockIdx.y;
-  const int q = (blockIdx.x * 4 + wave) * 32 + r;
-  const bool qv = q < a.q_len;
-  const bf16_t* qp = (const bf16_t*)a.q + b * a.q_bs + (int64_t)(qv ? q : 0) * a.q_ls + hh * HD;
+  const int qw = (blockIdx.x * 4 + wave) * 32 * QT + r;   // query of tile u: qw + 32 u
   const bf16_t* kbase = (const bf16_t*)a.k + b * a.k_bs + hh * HD;
   const bf16_t* vbase = (const bf16_t*)a.v + b * a.v_bs + hh * HD;
   const uint8_t* mb = a.key_padding_mask ? a.key_padding_mask + b * a.mask_bs : nullptr;
   const float c = a.scale * kLog2e;
 
-  s16x8 QF[NQ];
+  s16x8 QF[QT][NQ];
 #pragma unroll
-  for (int s = 0; s < NQ; ++s) QF[s] = qv ? *(const s16x8*)(qp + 16 * s + 8 * h) : s16x8{};
+  for (int u = 0; u < QT; ++u) {
+    const int q = qw + 32 * u;
+    const bool qv = q < a.q_len;
+    const bf16_t* qp = (const bf16_t*)a.q + b * a.q_bs + (int64_t)(qv ? q : 0) * a.q_ls + hh * HD;
+#pragma unroll
+    for (int s = 0; s < NQ; ++s) QF[u][s] = qv ? *(const s16x8*)(qp + 16 * s + 8 * h) : s16x8{};
+  }
 
   // Loads are issued unconditionally and consumed only in put(): a select or
   // branch on the loaded data in fetch() would make the compiler wait for
@@ -369,8 +393,10 @@ __global__ __launch_bounds__(256) void attn_fwd_db_kernel(MttsAttnFwdArgs a) {
       const int idx = tid + 256 * i;
       const int row = idx / (HD / CH), cc = (idx % (HD / CH)) * CH;
       const bool in = pk0 + row < a.kv_len;
-      *(f32x4*)(sK[buf] + row * KP + cc) = in ? pk[i] : f32x4{};
-      *(f32x4*)(sV[buf] + row * VP + cc) = in ? pv[i] : f32x4{};
+      const int ko = SWZ ? kimg<HD>(row, cc / CH) : row * KP + cc;
+      const int vo = SWZ ? kimg<HD>(row, cc / CH) : row * VP + cc;
+      *(f32x4*)(sK[buf] + ko) = in ? pk[i] : f32x4{};
+      *(f32x4*)(sV[buf] + vo) = in ? pv[i] : f32x4{};
     }
     const bool ok = pk0 + lane < a.kv_len && !(mb && praw);
     const uint64_t bal = __ballot(ok);
@@ -380,10 +406,27 @@ __global__ __launch_bounds__(256) void attn_fwd_db_kernel(MttsAttnFwdArgs a) {
     }
   };
 
-  float m = -INFINITY, l = 0.f;
-  f32x16 O[ND];
+  // lane-constant image offsets: K A-fragment rows (key r, chunk 2s + h) and
+  // the V^T transposed reads (keys 4h + qq (+8) of a 16-key step, dims of tile dt)
+  const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+  int oR[NQ], oT[2][ND];
 #pragma unroll
-  for (int dt = 0; dt < ND; ++dt) O[dt] = f32x16{};
+  for (int s = 0; s < NQ; ++s) oR[s] = SWZ ? kimg<HD>(r, 2 * s + h) : r * KP + 16 * s + 8 * h;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+      oT[u][dt] = SWZ ? kimg<HD>(4 * h + qq + 8 * u, 4 * dt + 2 * g + (pp >> 1)) + 4 * (pp & 1)
+                      : (4 * h + qq + 8 * u) * VP + dt * 32 + 16 * g + 4 * pp;
+  float m[QT], l[QT];
+  f32x16 O[QT][ND];
+#pragma unroll
+  for (int u = 0; u < QT; ++u) {
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) O[u][dt] = f32x16{};
+  }
   const int nblk = (a.kv_len + kKB - 1) / kKB;
   if (nblk > 0) {
     fetch(0);
@@ -396,43 +439,66 @@ __global__ __launch_bounds__(256) void attn_fwd_db_kernel(MttsAttnFwdArgs a) {
 #pragma unroll
     for (int t = 0; t < kKB / 32; ++t) {
       if (k0 + t * 32 >= a.kv_len) break;
-      f32x16 S = {};
-      const bf16_t* kr = sK[buf] + (t * 32 + r) * KP + 8 * h;
+      f32x16 S[QT];
 #pragma unroll
-      for (int s = 0; s < NQ; ++s) S = mfma_bf16(*(const s16x8*)(kr + 16 * s), QF[s], S);
-      softmax_step<ND>(S, sMask[buf][t], h, lane, c, m, l, O);
-      const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+      for (int u = 0; u < QT; ++u) S[u] = f32x16{};
+      const bf16_t* kt = sK[buf] + t * 32 * KP;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const s16x8 pb = pack8(S, s);
+      for (int s = 0; s < NQ; ++s) {
+        const s16x8 kf = *(const s16x8*)(kt + oR[s]);
+#pragma unroll
+        for (int u = 0; u < QT; ++u) S[u] = mfma_bf16(kf, QF[u][s], S[u]);
+      }
+      // V^T fragments of the tile read before the softmax, so their LDS
+      // latency hides under its VALU instead of stalling each PV MFMA
+      s16x8 vf[2][ND];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt) {
-          const bf16_t* p0 = sV[buf] + (t * 32 + 16 * s + 4 * h + qq) * VP + dt * 32 + 16 * g + 4 * pp;
-          O[dt] = mfma_bf16(cat(tr_read(p0), tr_read(p0 + 8 * VP)), pb, O[dt]);
+          const bf16_t* vs = sV[buf] + (t * 32 + 16 * s) * VP;
+          vf[s][dt] = cat(tr_read(vs + oT[0][dt]), tr_read(vs + oT[1][dt]));
         }
+      const uint32_t mw = sMask[buf][t];
+#pragma unroll
+      for (int u = 0; u < QT; ++u) softmax_step<ND>(S[u], mw, h, lane, c, m[u], l[u], O[u]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        s16x8 pb[QT];
+#pragma unroll
+        for (int u = 0; u < QT; ++u) pb[u] = pack8(S[u], s);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+          for (int u = 0; u < QT; ++u) O[u][dt] = mfma_bf16(vf[s][dt], pb[u], O[u][dt]);
       }
     }
     if (j + 1 < nblk) put(buf ^ 1);
     __syncthreads();
   }
 
-  const float lt = mtts::sum_xor32(l);
-  const float inv = 1.f / lt;  // fully masked: 0 * inf = NaN (torch MHA)
-  if (qv) {
-    bf16_t* op = (bf16_t*)a.out + b * a.o_bs + (int64_t)q * a.o_ls + hh * HD;
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+  for (int u = 0; u < QT; ++u) {
+    const int q = qw + 32 * u;
+    const float lt = mtts::sum_xor32(l[u]);
+    const float inv = 1.f / lt;  // fully masked: 0 * inf = NaN (torch MHA)
+    if (q < a.q_len) {
+      bf16_t* op = (bf16_t*)a.out + b * a.o_bs + (int64_t)q * a.o_ls + hh * HD;
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = dt * 32 + 8 * g4 + 4 * h;
-        if (d0 < HD) {
-          s16x4 v;
+      for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = bfbits(O[dt][4 * g4 + e] * inv);
-          *(s16x4*)(op + d0) = v;
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = dt * 32 + 8 * g4 + 4 * h;
+          if (d0 < HD) {
+            s16x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = bfbits(O[u][dt][4 * g4 + e] * inv);
+            *(s16x4*)(op + d0) = v;
+          }
         }
-      }
-    if (a.lse && h == 0) a.lse[((int64_t)b * a.heads + hh) * a.q_len + q] = (m + __builtin_amdgcn_logf(lt)) * kLn2;
+      if (a.lse && h == 0)
+        a.lse[((int64_t)b * a.heads + hh) * a.q_len + q] = (m[u] + __builtin_amdgcn_logf(lt)) * kLn2;
+    }
   }
 }
 
@@ -903,19 +969,6 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
 // transposed reads conflict-free), block j+1 loaded into registers under
 // block j's MFMAs, one barrier per block.  delta = rowsum(dO * O) is
 // computed once per query and written for the dK/dV pass (mode 1).
-// One LDS image of a bf16 [rows][HD] tile for BOTH row reads (ds_read_b128
-// of 16-byte chunk ch) and transposed reads (ds_read_b64_tr_b16 of 4 rows x
-// 16 columns): unpadded rows, 16-byte chunk index XORed with a function of
-// the row.  Row reads: the 8 (HD 64: same-parity) rows of a 16-lane phase hit
-// distinct chunks; transposed reads: 4 consecutive rows x 4 chunks land on
-// 16 distinct 4-bank groups.
-template <int HD>
-__device__ __forceinline__ int kswz(int row) {
-  if constexpr (HD == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
-  else return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
-}
-template <int HD>
-__device__ __forceinline__ int kimg(int row, int ch) { return row * HD + 8 * (ch ^ kswz<HD>(row)); }
 
 template <int HD>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
@@ -1019,10 +1072,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   // hd 128: the next block's 32 staging registers do not fit beside Q / dO /
   // dQ (256 VGPRs); it is loaded after this block's math instead
   constexpr bool kPrefetch = HD == 64;
+  constexpr int kTileUnroll = kPrefetch ? 2 : 1;
   for (int j = 0; j < nblk; ++j) {
     const int buf = j & 1, k0 = j * KB;
     if constexpr (kPrefetch) fetch(min(k0 + KB, (nblk - 1) * KB));   // in flight under this block's math
-#pragma unroll(kPrefetch ? 2 : 1)
+#pragma unroll kTileUnroll
     for (int t = 0; t < KB / 32; ++t) {
       if (k0 + t * 32 >= f.kv_len) break;
       const bf16_t* kt = sK[buf] + t * 32 * HD;
@@ -1300,7 +1354,14 @@ void launch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
   if constexpr (sizeof(T) == 2 && HD >= 32) {
     const char* e = getenv("MTTS_ATTN_FWD_DB");
     if (nw == 4 && (!e || atoi(e) != 0)) {
-      attn_fwd_db_kernel<HD><<<grid, 256, 0, st>>>(*a);
+      if constexpr (HD <= 64) {
+        const char* eq = getenv("MTTS_ATTN_FWD_QT");   // 2: measured equal to 1 (C5 shape), off
+        if (a->q_len >= 256 && eq && atoi(eq) == 2) {
+          attn_fwd_db_kernel<HD, 2><<<dim3((a->q_len + 255) / 256, a->heads, a->batch), 256, 0, st>>>(*a);
+          return;
+        }
+      }
+      attn_fwd_db_kernel<HD, 1><<<grid, 256, 0, st>>>(*a);
       return;
     }
   }

@@ -86,16 +86,20 @@ def test_forward_matches_reference(case, dtype):
     close(lse, ref_lse, 1e-5 if dtype == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("qt", ["2", "1"])
 @pytest.mark.parametrize("pattern", ["ramp", "steps", "late_spike"])
 @pytest.mark.parametrize("case", [(2, 256, 1100, 4, 64), (1, 128, 700, 2, 128), (2, 256, 128, 4, 64),
-                                  (1, 256, 100, 2, 128)])
-def test_forward_deferred_max_rescales(case, pattern):
+                                  (1, 256, 100, 2, 128), (2, 300, 700, 4, 64), (1, 520, 333, 2, 32)])
+def test_forward_deferred_max_rescales(case, pattern, qt, monkeypatch):
     """The bf16 forward kernels defer the running-max update until a row's
     max grows by more than 2^8 (attn.hip softmax_step).  Scores that grow
     along the key axis -- smoothly, in jumps at 32/64-key tile seams, or as
     one late spike -- force rescales on some rows of a wave and deferrals
-    on others; the result must still match the float64 reference."""
+    on others; the result must still match the float64 reference.  qt: two
+    32-query tiles per wave (long keys, hd <= 64, >= 256 queries) or one
+    (MTTS_ATTN_FWD_QT=1)."""
     from mtts import attn_kernels as A
+    monkeypatch.setenv("MTTS_ATTN_FWD_QT", qt)
     B, T, S, H, hd = case
     q, kv, kpm = make(B, T, S, H, hd, torch.float32, seed=3)
     d = H * hd
