@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 7
+#define MTTS_ABI_VERSION 8
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -44,6 +44,30 @@ enum {
 
 int mtts_abi_version(void);
 const char* mtts_last_error(void);
+
+/* Kernel-path overrides (test and measurement hooks; no reference
+ * counterpart).  Every key defaults to MTTS_OVR_AUTO (-1): the library picks
+ * the path from the shapes.  A value forces a path so the tests can reach
+ * kernels the C2 / north-star shapes never select (the narrow-stride scan,
+ * the P-lane scan at large B*D, the generic attention kernels, ...).  The
+ * table is process-wide: set it between launches, never while another
+ * thread launches.  Returns the previous value, or MTTS_EINVAL for an
+ * unknown key. */
+enum {
+  MTTS_OVR_AUTO = -1,
+  MTTS_OVR_SCAN_PATH = 0,     /* forward: 1 one-lane-per-channel (c1), 2 LDS-DMA P-lane (w2), 3 narrow */
+  MTTS_OVR_SCAN_P = 1,        /* lanes per channel of the P-lane kernels: 2 or 4 */
+  MTTS_OVR_SCAN_SEGS = 2,     /* forward L segments (>= 1) */
+  MTTS_OVR_SCAN_BWD_SEGS = 3, /* backward L segments (>= 1) */
+  MTTS_OVR_GEMM_NARROW = 4,   /* 1: the single-group GEMM kernel with 8-byte epilogue stores */
+  MTTS_OVR_ATTN_CHUNKS = 5,   /* attention backward query chunks (>= 1) */
+  MTTS_OVR_ATTN_BWD = 6,      /* attention backward: 1 fused one-pass kernel, 2 split dQ + dK/dV passes */
+  MTTS_OVR_ATTN_GENERIC = 7,  /* 1: generic MFMA attention kernels only (no short-key / long-key / q_len-1 kernels) */
+  MTTS_OVR_CONV_UNTILED = 8,  /* 1: the untiled causal-conv kernels */
+  MTTS_OVR_COUNT = 9
+};
+int mtts_set_override(int key, int value);
+int mtts_get_override(int key);
 
 /* ------------------------------------------------------------------------
  * Selective scan.  Replaces [upstream] selective_scan_cuda.fwd / .bwd
@@ -203,13 +227,6 @@ typedef struct {
 
 int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* stream);
 
-/* Decode: x_proj fused into the state update (Mamba.step's
- * x_db = x_proj(x); dt, B, C = split(x_db); state update).  `x` (B, D) bf16
- * is the conv output u; x_dbl = u . wx^T with wx (n_xdbl, D) bf16 row-major,
- * n_xdbl = dt_rank + 2 * 16, formed in-kernel (bf16-rounded as the unfused
- * x_proj output); `dt`, `Bm`, `Cm` (and their strides) are not read;
- * dt_rank % 32 == 0 and dt_w required; batch <= 32, dim % 128 == 0. */
-int mtts_xproj_state_update(const MttsStateUpdateArgs* a, const void* wx, int n_xdbl, void* stream);
 
 /* ------------------------------------------------------------------------
  * LayerNorm (eps) with optional fused FiLM, optional fused residual add.

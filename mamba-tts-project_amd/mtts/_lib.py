@@ -9,6 +9,7 @@ torch bundles (libamdhip64.so.7) is the one the library binds to.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 
@@ -16,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -133,6 +134,8 @@ class AdamTensor(C.Structure):
 _SIGS = {
     "mtts_abi_version": ([], i32),
     "mtts_last_error": ([], C.c_char_p),
+    "mtts_set_override": ([i32, i32], i32),
+    "mtts_get_override": ([i32], i32),
     "mtts_selective_scan_fwd_workspace": ([i32, i32, i32, i32], i64),
     "mtts_selective_scan_fwd": ([C.POINTER(ScanFwdArgs), vp], i32),
     "mtts_selective_scan_bwd_workspace": ([i32, i32, i32, i32], i64),
@@ -142,7 +145,6 @@ _SIGS = {
     "mtts_causal_conv1d_bwd": ([C.POINTER(ConvBwdArgs), vp], i32),
     "mtts_causal_conv1d_update": ([C.POINTER(ConvUpdateArgs), vp], i32),
     "mtts_selective_state_update": ([C.POINTER(StateUpdateArgs), vp], i32),
-    "mtts_xproj_state_update": ([C.POINTER(StateUpdateArgs), vp, i32, vp], i32),
     "mtts_layernorm_fwd": ([C.POINTER(LNArgs), vp], i32),
     "mtts_gemm_rows": ([C.POINTER(RowsArgs), vp], i32),
     "mtts_pack_rows_bytes": ([i32, i32], i64),
@@ -214,6 +216,29 @@ def call_raw(name, *args):
     rc = getattr(L, name)(*args, C.c_void_p(torch.cuda.current_stream().cuda_stream))
     if rc != 0:
         raise RuntimeError(f"{name} failed ({rc}): {L.mtts_last_error().decode()}")
+
+
+# kernel-path override keys (include/mtts.h MTTS_OVR_*): test / measurement hooks
+OVERRIDES = {"scan_path": 0, "scan_p": 1, "scan_segs": 2, "scan_bwd_segs": 3, "gemm_narrow": 4,
+             "attn_chunks": 5, "attn_bwd": 6, "attn_generic": 7, "conv_untiled": 8}
+SCAN_C1, SCAN_W2, SCAN_NARROW = 1, 2, 3
+ATTN_BWD_FUSED, ATTN_BWD_SPLIT = 1, 2
+
+
+@contextlib.contextmanager
+def override(**paths):
+    """Force kernel paths for the duration of the block (mtts_set_override),
+    e.g. ``with override(scan_path=SCAN_W2, scan_segs=3): ...``; None leaves a
+    key automatic.  The previous values are restored on exit."""
+    L = lib()
+    old = {}
+    try:
+        for k, v in paths.items():
+            old[k] = L.mtts_set_override(OVERRIDES[k], -1 if v is None else int(v))
+        yield
+    finally:
+        for k, v in old.items():
+            L.mtts_set_override(OVERRIDES[k], v)
 
 
 def dtype_code(t: torch.Tensor) -> int:

@@ -1339,8 +1339,7 @@ int check_fwd(const MttsAttnFwdArgs* a, const char* who) {
 template <typename T, int HD>
 void launch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
   if constexpr (sizeof(T) == 2 && HD % 32 == 0) {
-    const char* e = getenv("MTTS_ATTN_FWD_SHORT");
-    if (a->kv_len <= kShortKV && a->q_len >= 128 && (!e || atoi(e) != 0)) {
+    if (a->kv_len <= kShortKV && a->q_len >= 128 && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1) {
       // >= 512 workgroups (two per CU), as many query slices per wave as that allows
       const int64_t blocks128 = (int64_t)((a->q_len + 127) / 128) * a->heads * a->batch;
       int nsl = (int)std::max<int64_t>(1, std::min<int64_t>(8, blocks128 / 512));
@@ -1352,15 +1351,9 @@ void launch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
   const int nw = a->q_len >= 128 ? 4 : (a->q_len + 31) / 32;
   dim3 grid((a->q_len + 32 * nw - 1) / (32 * nw), a->heads, a->batch);
   if constexpr (sizeof(T) == 2 && HD >= 32) {
-    const char* e = getenv("MTTS_ATTN_FWD_DB");
-    if (nw == 4 && (!e || atoi(e) != 0)) {
-      if constexpr (HD <= 64) {
-        const char* eq = getenv("MTTS_ATTN_FWD_QT");   // 2: measured equal to 1 (C5 shape), off
-        if (a->q_len >= 256 && eq && atoi(eq) == 2) {
-          attn_fwd_db_kernel<HD, 2><<<dim3((a->q_len + 255) / 256, a->heads, a->batch), 256, 0, st>>>(*a);
-          return;
-        }
-      }
+    if (nw == 4 && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1) {
+      // (two 32-query tiles per wave sharing every K / V fragment read, QT = 2,
+      // measured equal to QT = 1 at the C5 shape: 717 vs 680-720 us)
       attn_fwd_db_kernel<HD, 1><<<grid, 256, 0, st>>>(*a);
       return;
     }
@@ -1598,7 +1591,7 @@ BwdPlan plan_bwd(int batch, int heads, int head_dim, int q_len, int kv_len, int 
   const int slices = (q_len + 31) / 32;
   const int base = batch * heads;
   int nchunk = base >= 256 ? 1 : (256 + base - 1) / base;
-  if (const char* e = getenv("MTTS_ATTN_CHUNKS")) nchunk = atoi(e);
+  if (mtts::override_of(MTTS_OVR_ATTN_CHUNKS) >= 1) nchunk = mtts::override_of(MTTS_OVR_ATTN_CHUNKS);
   nchunk = nchunk < 1 ? 1 : (nchunk > slices ? (slices > 0 ? slices : 1) : nchunk);
   const int per = (slices + nchunk - 1) / nchunk;
   pl.qchunk = 32 * (per > 0 ? per : 1);
@@ -1609,12 +1602,13 @@ BwdPlan plan_bwd(int batch, int heads, int head_dim, int q_len, int kv_len, int 
   // group; the dK/dV pass may be chunked over queries into partials.  (For
   // one key group, C2's 128 text keys, the split form measured 112 us against
   // the fused mode-0 kernel's 106 us per call and is not used.)
-  pl.split = (kv_len > pl.kg || getenv("MTTS_ATTN_BWD_SPLIT")) && !getenv("MTTS_ATTN_BWD_FUSED");
+  const int force = mtts::override_of(MTTS_OVR_ATTN_BWD);
+  pl.split = force == 2 || (kv_len > pl.kg && force != 1);
   if (pl.split) {
     const int nkg = (kv_len + pl.kg - 1) / pl.kg;
     const int wgs = nkg * base;
     int nc = wgs >= 256 ? 1 : (256 + wgs - 1) / wgs;
-    if (const char* e = getenv("MTTS_ATTN_CHUNKS")) nc = atoi(e);
+    if (mtts::override_of(MTTS_OVR_ATTN_CHUNKS) >= 1) nc = mtts::override_of(MTTS_OVR_ATTN_CHUNKS);
     nc = nc < 1 ? 1 : (nc > slices ? (slices > 0 ? slices : 1) : nc);
     const int per2 = (slices + nc - 1) / nc;
     pl.qchunk = 32 * (per2 > 0 ? per2 : 1);
@@ -1636,7 +1630,7 @@ void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
   if (split) {
     constexpr int KG = BwdCfg<T, HD>::KG;
     if constexpr (std::is_same<T, bf16_t>::value && (HD == 64 || HD == 128)) {
-      if (!getenv("MTTS_ATTN_DQ_V1"))
+      if (mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1)
         attn_bwd_dq_kernel<HD><<<dim3((f.q_len + 127) / 128, f.heads, f.batch), 256, 0, st>>>(p);
       else
         attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
@@ -1644,7 +1638,7 @@ void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
       attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
     }
     if constexpr (std::is_same<T, bf16_t>::value && HD == 64) {
-      if (!getenv("MTTS_ATTN_KV_V1")) {
+      if (mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1) {
         attn_bwd_kv_kernel<HD><<<dim3((f.kv_len + 127) / 128 * p.nchunk, f.heads, f.batch), 256, 0, st>>>(p);
         return;
       }
@@ -1677,16 +1671,16 @@ void dispatch_bwd(const BwdParams& p, bool split, hipStream_t st) {
 extern "C" int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream) {
   int rc = check_fwd(a, "attention_fwd");
   if (rc) return rc;
-  MTTS_CHECK(a->kv_hs == 0 || (a->q_len == 1 && a->kv_hs % 8 == 0 && !getenv("MTTS_ATTN_DECODE_OFF")),
+  MTTS_CHECK(a->kv_hs == 0 || (a->q_len == 1 && a->kv_hs % 8 == 0 && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1),
              "attention_fwd: a k / v head stride is taken by the single-query kernels only (q_len 1)");
   // the packed image is written by the single-pass decode kernel only
   MTTS_CHECK(!a->out_packed || (a->q_len == 1 && a->dtype == MTTS_BF16 && a->batch <= 32 &&
                                 (a->heads * a->head_dim) % 32 == 0 && a->kv_len <= 8 * (256 / (a->head_dim / 8)) &&
-                                !getenv("MTTS_ATTN_DECODE_OFF")),
+                                mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1),
              "attention_fwd: packed output needs q_len 1, bf16, batch <= 32, kv_len <= %d", 8 * (256 / (a->head_dim / 8)));
   if (a->batch == 0 || a->q_len == 0) return MTTS_OK;
   hipStream_t st = (hipStream_t)stream;
-  const bool one = a->q_len == 1 && !getenv("MTTS_ATTN_DECODE_OFF");   // decode step: single-query kernel
+  const bool one = a->q_len == 1 && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1;   // decode step: single-query kernel
   if (a->dtype == MTTS_BF16)
     one ? dispatch_decode<bf16_t>(a, st) : dispatch_fwd<bf16_t>(a, st);
   else

@@ -11,6 +11,8 @@ namespace mtts {
 
 // ---------------------------------------------------------------- errors
 void set_error(const char* fmt, ...);
+// kernel-path override (mtts_set_override; MTTS_OVR_AUTO = -1 when unset)
+int override_of(int key);
 
 // out[g * out_gstride + c] = sum over partials p in [g*ppg, (g+1)*ppg) of part[p * pstride + c]
 void colsum(const float* part, int nparts, int ppg, int64_t pstride, int ncols, float* out, int64_t out_gstride,

@@ -445,7 +445,7 @@ static int check_conv(const MttsConvFwdArgs* a) {
 constexpr int kFwdTT = 16;   // tiled forward: steps per thread
 constexpr int kBwdTT = 8;    // tiled backward: steps per wave (8 waves = 64 steps per block)
 
-static bool tiled_off() { return getenv("MTTS_CONV_UNTILED") != nullptr; }
+static bool tiled_off() { return override_of(MTTS_OVR_CONV_UNTILED) == 1; }
 
 template <typename T, int CPT>
 static void launch_fwd(const MttsConvFwdArgs* a, hipStream_t st) {

@@ -118,42 +118,40 @@ __device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
                                                  0, 0);
 }
 
-// erf for the GELU epilogues without ocml's divergent branches and
-// range-reduced expf: |x| <= 0.9: x P(x^2) (degree 5 in x^2), else
-// sign(x) (1 - exp(Q(|x|) - x^2)) with Q a degree-8 fit of log erfc(t) + t^2
-// on [0.85, 4.5] (t clamped there; erf = 1 in fp32 beyond 3.92); both arms
-// computed and selected.  Max relative error 2.4e-7 (x P) / 1.1e-7 (erf arm),
-// erfc relative error 5.4e-6 (the GELU's negative side), checked in float64
-// against math.erf over the whole range (fit and check: DESIGN.md §3).
-__device__ __forceinline__ float erf_fast(float x) {
-  const float s = x * x;
-  float p = -6.175214075e-04f;
-  p = fmaf(p, s, 5.027941428e-03f);
-  p = fmaf(p, s, -2.678935602e-02f);
-  p = fmaf(p, s, 1.128241718e-01f);
-  p = fmaf(p, s, -3.761254847e-01f);
-  p = fmaf(p, s, 1.128379107e+00f);
-  const float small = x * p;
-  const float t = fminf(fabsf(x), 4.5f);
-  float q = 1.430673365e-06f;
-  q = fmaf(q, t, -4.196325972e-05f);
-  q = fmaf(q, t, 5.622986355e-04f);
-  q = fmaf(q, t, -4.598612431e-03f);
-  q = fmaf(q, t, 2.596756257e-02f);
-  q = fmaf(q, t, -1.092917621e-01f);
-  q = fmaf(q, t, 3.673504889e-01f);
-  q = fmaf(q, t, -1.129761577e+00f);
-  q = fmaf(q, t, 2.067339810e-04f);
-  const float e = __builtin_amdgcn_exp2f(fmaf(-t, t, q) * kLog2e);
-  const float big = __builtin_copysignf(1.f - e, x);
-  return fabsf(x) <= 0.9f ? small : big;
+// GELU epilogues (exact-erf F.gelu and its derivative) with one polynomial
+// and one exp2, no branches: the tail h(x) = Phi(-|x|) = erfc(|x|/sqrt2)/2 is
+// exp2(S(a) - a^2 log2(e)/2), a = min(|x|, 5.5), S a degree-10 polynomial
+// (least-squares fit of log2 h + a^2 log2(e)/2 on [0, 5.5], reweighted to an
+// equi-ripple error: 1.4e-7 relative in float64, 2.8e-6 evaluated in fp32,
+// where exp2 of the ~-26 argument at a = 5.5 sets the floor); Phi(x) = x >= 0 ?
+// 1 - h : h.  18 VALU per GELU (was 27: erf as two polynomial arms and a
+// select), 21 per derivative (was 31).  Fit and check: DESIGN.md §3.
+__device__ __forceinline__ float gelu_tail_s(float a) {
+  float s = -1.7774024116e-08f;
+  s = fmaf(s, a, 5.6194854933e-07f);
+  s = fmaf(s, a, -7.6223902631e-06f);
+  s = fmaf(s, a, 5.5893204013e-05f);
+  s = fmaf(s, a, -2.0454518331e-04f);
+  s = fmaf(s, a, -1.6655060660e-04f);
+  s = fmaf(s, a, 7.1668288485e-03f);
+  s = fmaf(s, a, -5.2604280745e-02f);
+  s = fmaf(s, a, 2.6218665810e-01f);
+  s = fmaf(s, a, -1.1511125488e+00f);
+  s = fmaf(s, a, -9.9999981719e-01f);
+  return s;
 }
-// F.gelu (approximate='none') and its derivative (torch's GeluBackward):
-// 0.5 x (1 + erf(x/sqrt2)); cdf + x exp(-x^2/2) / sqrt(2 pi)
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_f(float x) {
+  const float a = fminf(fabsf(x), 5.5f);
+  const float h = __builtin_amdgcn_exp2f(fmaf(x * (-0.5f * kLog2e), x, gelu_tail_s(a)));
+  return x * (x >= 0.f ? 1.f - h : h);
+}
+// torch's GeluBackward: Phi(x) + x exp(-x^2/2) / sqrt(2 pi)
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f));
-  return cdf + x * 0.3989422804014327f * __builtin_amdgcn_exp2f(-0.5f * x * x * kLog2e);
+  const float a = fminf(fabsf(x), 5.5f);
+  const float m = x * (-0.5f * kLog2e) * x;
+  const float e = __builtin_amdgcn_exp2f(m);
+  const float h = __builtin_amdgcn_exp2f(m + gelu_tail_s(a));
+  return fmaf(x * 0.3989422804014327f, e, x >= 0.f ? 1.f - h : h);
 }
 
 // Per-thread source offsets (elements) of one region's two DMAs, relative to
@@ -575,17 +573,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(GemmParams p) {
 // the needed one (q0 -> B1(g): 6, q1 -> A1(g): 10, q3 -> A0/B0(g+1): 8, fewer
 // at the end of the stream), and the barrier after it orders every wave's
 // wait before any read.
-//
-// PERSISTENT: a workgroup runs tiles (work items) wid, wid + grid, ... and g
-// counts K-tiles over all of them, so the staging above simply continues into
-// the next tile (its first regions land while the current tile finishes: no
-// per-tile prologue) and the tile's epilogue runs inside the next tile's
-// first read segment, beside the partner group's last MFMA segment, its
-// stores overlapping the next tile's main loop.  Every epilogue memory
-// operation is a single-instruction buffer load / store (out-of-range rows and
-// columns are dropped by the buffer's range check, not by branches), so the
-// number of VMEM operations an epilogue adds to the first K-tile's waits is
-// a compile-time constant (kEpiOps).
+// Every epilogue memory operation is a single-instruction buffer load /
+// store: out-of-range rows and columns are dropped by the buffer's range
+// check, not by branches.
 template <int N>
 __device__ __forceinline__ void wait_ops() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -620,15 +610,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
 
-// VMEM operations of one tile's epilogue (stores + loads), and the bias loads
-// made at a tile's start: exact instruction counts of store_tile_buf / load_bias
-template <int EPI, bool OUT_F32>
-struct EpiOps {
-  static constexpr int bias = (EPI & MTTS_GEMM_EPI_BIAS) ? 4 : 0;
-  static constexpr int epi = OUT_F32 ? 32 : 16 + ((EPI & MTTS_GEMM_EPI_GELU) ? 16 : 0) +
-                                             ((EPI & MTTS_GEMM_EPI_DGELU) ? 32 : 0);
-};
-
 template <int EPI>
 __device__ __forceinline__ void load_bias(const GemmParams& p, int n0, int wc, int lane, f32x4 (&bias)[4]) {
   if constexpr ((EPI & MTTS_GEMM_EPI_BIAS) != 0) {
@@ -650,8 +631,8 @@ __device__ __forceinline__ void load_bias(const GemmParams& p, int n0, int wc, i
   }
 }
 
-// store_tile with buffer stores (beta == 0 for fp32 out): exactly EpiOps::epi
-// VMEM instructions whatever the bounds
+// store_tile with buffer stores (beta == 0 for fp32 out): the same VMEM
+// instructions whatever the bounds
 template <int EPI, bool OUT_F32>
 __device__ __forceinline__ void store_tile_buf(const GemmParams& p, f32x4 (&acc)[8][4], const f32x4 (&bias)[4],
                                                int m0, int n0, int wr, int wc, int lane, int split) {
@@ -794,7 +775,7 @@ struct PLoader {
   }
 };
 
-template <bool AK, bool BKM, int EPI, bool OUT_F32, bool PERSIST>
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
 __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char lds[kLds];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -805,10 +786,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   const int bid = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int total = p.tiles_m * p.tiles_n * p.splits;
-  const int nitems = PERSIST ? (total - wid + nwg - 1) / nwg : 1;   // items wid, wid + nwg, ...
   const int nk = p.k / kBK;
-  const int G = nitems * nk;                                         // K-tiles of the whole stream
+  const int G = nk;                                                  // K-tiles of the item
 
   PLoader<AK, true> la;
   PLoader<BKM, false> lb;
@@ -818,10 +797,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   const int64_t bstep = BKM ? kBK * 2 : kBK * p.ldb * 2;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
 
-  // an item's K-tile-0 operand origins (wave-uniform) and 8 per-thread DMA
-  // offsets (A0/A1 x 2, B0/B1 x 2), made once per item: a DMA's address
-  // register is never recomputed right behind the DMA that reads it.  With
-  // PERSIST the stream stages up to two K-tiles ahead, into the next item.
+  // the item's K-tile-0 operand origins (wave-uniform) and 8 per-thread DMA
+  // offsets (A0/A1 x 2, B0/B1 x 2), made once: a DMA's address register is
+  // never recomputed right behind the DMA that reads it.  (A persistent form
+  // looping over items, the next item's K-tiles staged into the current
+  // item's tail, measured 0-7 % slower and was removed in round 4.)
   struct Src {
     const char* a;
     const char* b;
@@ -839,29 +819,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
         sr.o[4 + s * 2 + i] = lb.off(it.n0, p.n, p.ldb, s, i);
       }
   };
-  WorkItem cur = work_item(p, wid), nxt = cur;
-  Src scur, snxt;
+  const WorkItem cur = work_item(p, wid);
+  Src scur;
   source(cur, scur);
-  if constexpr (PERSIST) {
-    if (nitems > 1) nxt = work_item(p, wid + nwg);
-    source(nxt, snxt);
-  }
-  int kbase = 0;   // stream index of the current item's K-tile 0
-  auto stage = [&](int g, int r) {
-    bool next = false;
-    if constexpr (PERSIST) next = g >= kbase + nk;
-    const int kt = g - (next ? kbase + nk : kbase);
-    const uint32_t reg = lds0 + (g & 1) * kBuf + r * kRegion;
+  auto stage = [&](int kt, int r) {
+    const uint32_t reg = lds0 + (kt & 1) * kBuf + r * kRegion;
     const int oi = (r == R_A0 ? 0 : r == R_A1 ? 2 : r == R_B0 ? 4 : 6);
     const bool isa = r == R_A0 || r == R_A1;
-    const char* base = isa ? (next ? snxt.a : scur.a) + kt * astep : (next ? snxt.b : scur.b) + kt * bstep;
-    const uint32_t o0 = next ? snxt.o[oi] : scur.o[oi], o1 = next ? snxt.o[oi + 1] : scur.o[oi + 1];
-    glds16(base, o0, reg + wave * 1024);
-    glds16(base, o1, reg + 8192 + wave * 1024);
+    const char* base = isa ? scur.a + kt * astep : scur.b + kt * bstep;
+    glds16(base, scur.o[oi], reg + wave * 1024);
+    glds16(base, scur.o[oi + 1], reg + 8192 + wave * 1024);
   };
 
-  constexpr int kBiasOps = EpiOps<EPI, OUT_F32>::bias;
-  constexpr int kEpiOps = EpiOps<EPI, OUT_F32>::epi + kBiasOps;   // a tile boundary's extra VMEM ops
   f32x4 bias[4] = {};
   load_bias<EPI>(p, cur.n0, wc, lane, bias);   // older than every DMA: outside the counts
 
@@ -893,32 +862,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   __builtin_amdgcn_sched_barrier(0);                                                        \
   sbar();
   // Wait counts (VMEM ops younger than the needed region): steady 6 / 10 / 8;
-  // the stream's first K-tile 8 / 8 / 8; its last two fewer; + kEpiOps in a
-  // tile's first K-tile after an epilogue.  One uniform branch per wait.
+  // the first K-tile 8 / 8 / 8; the last two fewer.  One uniform branch per wait.
   for (int g = 0; g < G; ++g) {
-    const int t = g - kbase;
-    if constexpr (PERSIST) {
-      if (t == nk) {
-        // ---- the finished tile's epilogue, then the next tile's bias: in the
-        // read segment of the next K-tile's first phase, beside the partner
-        // group's last MFMA segment
-        store_tile_buf<EPI, OUT_F32>(p, acc, bias, cur.m0, cur.n0, wr, wc, lane, cur.split);
-        kbase += nk;
-        cur = nxt;
-        scur = snxt;
-        if (kbase + nk < G) {
-          nxt = work_item(p, wid + (kbase / nk + 1) * nwg);
-          source(nxt, snxt);
-        }
-        load_bias<EPI>(p, cur.n0, wc, lane, bias);
-#pragma unroll
-        for (int a = 0; a < 8; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-    const int ex = (PERSIST && g == kbase && g > 0) ? kEpiOps : 0;
-    const bool steady = g > 0 && g + 2 < G && ex == 0;
+    const bool steady = g > 0 && g + 2 < G;
     const bool n1 = g + 1 < G, n2 = g + 2 < G;
     const char* bufp = lbase + (g & 1) * kBuf;
     // ---- q0: A0 x B0 | stage A1(g+1) | wait B1(g)
@@ -931,7 +877,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
     }
     if (n1) stage(g + 1, R_A1);
     if (steady) wait_ops<6>();
-    else wait_ops_rt<6>(g == 0 ? (n1 ? 8 : 2) : (n1 ? 6 : 0) + ex);
+    else wait_ops_rt<6>(g == 0 ? (n1 ? 8 : 2) : (n1 ? 6 : 0));
     sbar();
     PP_MFMA(b0f, 0, 0)
     // ---- q1: A0 x B1 | stage B1(g+1) | wait A1(g)
@@ -941,7 +887,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
       for (int nb = 0; nb < 2; ++nb) b1f[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
     if (n1) stage(g + 1, R_B1);
     if (steady) wait_ops<10>();
-    else wait_ops_rt<10>(g == 0 ? (n1 ? 8 : 0) : (n1 ? 10 : 2) + ex);
+    else wait_ops_rt<10>(g == 0 ? (n1 ? 8 : 0) : (n1 ? 10 : 2));
     sbar();
     PP_MFMA(b1f, 0, 2)
     // ---- q2: A1 x B1 | stage A0(g+2)
@@ -955,145 +901,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
     // ---- q3: A1 x B0 | stage B0(g+2) | wait A0 / B0(g+1)
     if (n2) stage(g + 2, R_B0);
     if (steady) wait_ops<8>();
-    else if (n1) wait_ops_rt<8>((n2 ? 8 : 4) + ex);
+    else if (n1) wait_ops_rt<8>((n2 ? 8 : 4));
     sbar();
     PP_MFMA(b0f, 4, 0)
   }
 #undef PP_MFMA
   if (wr == 0) sbar();   // the same barrier count for both groups
   store_tile_buf<EPI, OUT_F32>(p, acc, bias, cur.m0, cur.n0, wr, wc, lane, cur.split);
-}
-
-// round-3 first ping-pong form (one tile per workgroup, compiler-visible
-// global-store epilogue): kept as MTTS_GEMM_PP=3 for in-process A/B
-template <int N>
-__device__ __forceinline__ void wait_regions() { wait_vm<2 * N>(); }
-__device__ __forceinline__ void wait_regions_rt(int n) {
-  switch (n) {
-    case 0: wait_regions<0>(); break;
-    case 1: wait_regions<1>(); break;
-    case 2: wait_regions<2>(); break;
-    case 3: wait_regions<3>(); break;
-    case 4: wait_regions<4>(); break;
-    default: wait_regions<5>(); break;
-  }
-}
-
-template <bool AK, bool BKM, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(kThreads, 1) void gemm_pp1_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char lds[kLds];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int tiles = p.tiles_m * p.tiles_n;
-  const int split = id / tiles;
-  const int tile = id % tiles;
-  const int gsz = p.group * p.tiles_n;
-  const int g0 = (tile / gsz) * p.group;
-  const int gr = min(p.group, p.tiles_m - g0);
-  const int tm = g0 + (tile % gsz) % gr, tn = (tile % gsz) / gr;
-  const int m0 = tm * kTile, n0 = tn * kTile;
-
-  const int64_t k0 = (int64_t)split * p.k;
-  const char* abase;
-  const char* bbase;
-  int64_t astep, bstep;
-  if constexpr (AK) { abase = (const char*)(p.a + k0); astep = kBK * 2; }
-  else { abase = (const char*)(p.a + k0 * p.lda); astep = kBK * p.lda * 2; }
-  if constexpr (BKM) { bbase = (const char*)(p.b + k0); bstep = kBK * 2; }
-  else { bbase = (const char*)(p.b + k0 * p.ldb); bstep = kBK * p.ldb * 2; }
-
-  Loader<AK, true> la;
-  Loader<BKM, false> lb;
-  la.init(tid, m0, p.m, p.lda);
-  lb.init(tid, n0, p.n, p.ldb);
-
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
-  auto stage = [&](int kt, int r) {
-    const uint32_t reg = lds0 + (kt & 1) * kBuf + r * kRegion;
-    if (r == R_A0 || r == R_A1) {
-      la.stage1(abase + kt * astep, r - R_A0, reg, wave, 0);
-      la.stage1(abase + kt * astep, r - R_A0, reg, wave, 1);
-    } else {
-      lb.stage1(bbase + kt * bstep, r - R_B0, reg, wave, 0);
-      lb.stage1(bbase + kt * bstep, r - R_B0, reg, wave, 1);
-    }
-  };
-
-  const int nk = p.k / kBK;
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: all of K-tile 0, A0 / B0 of K-tile 1 (A1 / B1 of K-tile 1 are
-  // staged by K-tile 0's phases 0 / 1)
-  stage(0, R_A0); stage(0, R_B0); stage(0, R_B1); stage(0, R_A1);
-  if (nk > 1) { stage(1, R_A0); stage(1, R_B0); }
-  if (nk > 1) wait_regions<4>(); else wait_regions<2>();   // A0(0), B0(0) landed
-  sbar();
-  if (wr == 1) sbar();   // group 1 runs one barrier behind
-
-  const char* lbase = lds;
-  s16x8 af[2][4], b0f[2][2], b1f[2][2];   // [ks][block]
-#define PP_MFMA(BF, MO, NO)                                                                   \
-  __builtin_amdgcn_sched_barrier(0);                                                        \
-  __builtin_amdgcn_s_waitcnt(0xC07F);                                                        \
-  __builtin_amdgcn_sched_barrier(0);                                                        \
-  __builtin_amdgcn_s_setprio(1);                                                            \
-  _Pragma("unroll") for (int ks_ = 0; ks_ < 2; ++ks_)                                        \
-  _Pragma("unroll") for (int mb_ = 0; mb_ < 4; ++mb_)                                        \
-  _Pragma("unroll") for (int nb_ = 0; nb_ < 2; ++nb_)                                        \
-      acc[(MO) + mb_][(NO) + nb_] = mfma(BF[ks_][nb_], af[ks_][mb_], acc[(MO) + mb_][(NO) + nb_]); \
-  __builtin_amdgcn_s_setprio(0);                                                            \
-  __builtin_amdgcn_sched_barrier(0);                                                        \
-  sbar();
-  for (int t = 0; t < nk; ++t) {
-    const char* bufp = lbase + (t & 1) * kBuf;
-    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
-    // ---- q0: A0 x B0 | stage A1(t+1) | wait B1(t)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) b0f[ks][nb] = frag<BKM>(bufp + R_B0 * kRegion, wc * 32 + nb * 16, ks, lane);
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A0 * kRegion, wr * 64 + mb * 16, ks, lane);
-    }
-    if (n1) stage(t + 1, R_A1);
-    if (t == 0) wait_regions_rt(n1 ? 4 : 1); else wait_regions_rt(n1 ? 3 : 0);
-    sbar();
-    PP_MFMA(b0f, 0, 0)
-    // ---- q1: A0 x B1 | stage B1(t+1) | wait A1(t)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) b1f[ks][nb] = frag<BKM>(bufp + R_B1 * kRegion, wc * 32 + nb * 16, ks, lane);
-    if (n1) stage(t + 1, R_B1);
-    if (t == 0) wait_regions_rt(n1 ? 4 : 0); else wait_regions_rt(n1 ? 5 : 1);
-    sbar();
-    PP_MFMA(b1f, 0, 2)
-    // ---- q2: A1 x B1 | stage A0(t+2)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) af[ks][mb] = frag<AK>(bufp + R_A1 * kRegion, wr * 64 + mb * 16, ks, lane);
-    if (n2) stage(t + 2, R_A0);
-    sbar();
-    PP_MFMA(b1f, 4, 2)
-    // ---- q3: A1 x B0 | stage B0(t+2) | wait A0 / B0(t+1)
-    if (n2) stage(t + 2, R_B0);
-    if (n1) wait_regions_rt(n2 ? 4 : 2);
-    sbar();
-    PP_MFMA(b0f, 4, 0)
-  }
-#undef PP_MFMA
-  if (wr == 0) sbar();   // the same barrier count for both groups
-  store_tile<EPI, OUT_F32>(p, acc, m0, n0, wr, wc, lane, split);
 }
 
 // out[i] = beta*out[i] + sum_s slab[s][i] (fixed order); rows x cols with row strides
@@ -1112,50 +926,23 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restri
   }
 }
 
-// MTTS_GEMM_PP: 0 = the round-2 single-group kernel, 1 (default) = ping-pong
-// with one tile per workgroup, 2 = ping-pong persistent, 3 = the first
-// ping-pong form (read per launch: in-process A/B).  Measured on the C2
-// shapes (tools/gemm_pp_ab.py, same box, interleaved): ping-pong 1078-1339
-// TF/s NT, 696-1110 TN, vs 997-1321 / 684-1128 for the round-2 kernel; the
-// persistent form (epilogue inside the next tile's first read segment) 0-7 %
-// slower than one tile per workgroup: the two groups' epilogues serialise
-// on the barrier and cost what a fresh workgroup's prologue does.
-static int pp_mode() {
-  const char* e = getenv("MTTS_GEMM_PP");
-  return e ? atoi(e) : 1;
-}
-static int num_cus() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      v = 256;
-    return v > 0 ? v : 256;
-  }();
-  return n;
-}
+// Ping-pong kernel, one tile per workgroup (tools/gemm_pp_ab.py, C2 shapes,
+// same box: 1078-1339 TF/s NT, 696-1110 TN vs 997-1321 / 684-1128 for the
+// round-2 single-group kernel, which remains the fallback for 8-byte-aligned
+// outputs, C / aux spans past 2 GiB and beta accumulate with split-K).
 template <bool AK, bool BKM, int EPI, bool F32>
 void launch(const GemmParams& p, int nwg, hipStream_t st) {
-  const int mode = pp_mode();
   // the ping-pong epilogue stores 16-byte bf16 pieces (wide_out) and
   // addresses C / aux / each slab with 31-bit buffer offsets
   const int64_t cbytes = F32 ? (int64_t)p.m * p.ldc * 4 : (int64_t)p.m * p.ldc * 2;
   const int64_t abytes = (EPI & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) ? (int64_t)p.m * p.ld_aux * 2 : 0;
   const bool pp_ok = (F32 || p.wide_out) && cbytes < (1ll << 31) && abytes < (1ll << 31) &&
-                     (!F32 || p.beta == 0.f || p.splits == 1);
-  if (mode == 3) {
-    hipLaunchKernelGGL((gemm_pp1_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
-    return;
-  }
-  if (mode == 0 || !pp_ok) {
+                     (!F32 || p.beta == 0.f || p.splits == 1) && override_of(MTTS_OVR_GEMM_NARROW) != 1;
+  if (!pp_ok) {
     hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
     return;
   }
-  // persistent: one workgroup per CU looping over the work items, when the
-  // stream has >= 2 K-tiles per item and the epilogue needs no C reads
-  int grid = nwg;
-  if (mode >= 2 && p.k / kBK >= 2 && !(F32 && p.beta != 0.f)) grid = std::min(nwg, num_cus());
-  if (grid < nwg) hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32, true>), dim3(grid), dim3(kThreads), 0, st, p);
-  else hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32, false>), dim3(grid), dim3(kThreads), 0, st, p);
+  hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
 }
 
 }  // namespace
@@ -1212,14 +999,13 @@ extern "C" int mtts_gemm(const MttsGemmArgs* a, void* stream) {
   p.tiles_m = (M + kTile - 1) / kTile; p.tiles_n = (N + kTile - 1) / kTile;
   p.splits = splits; p.epi = epi;
   p.group = std::min(p.tiles_m, 4);
-  if (const char* e = getenv("MTTS_GEMM_GROUP")) p.group = std::max(1, std::min(p.tiles_m, atoi(e)));
   if (splits > 1) {
     p.c = a->workspace; p.ldc = N; p.split_stride = (int64_t)M * N; p.beta = 0.f;
   } else {
     p.c = a->c; p.ldc = a->ldc; p.split_stride = 0; p.beta = a->beta;
   }
   p.wide_out = !f32out && a->ldc % 8 == 0 && (!(epi & (MTTS_GEMM_EPI_GELU | MTTS_GEMM_EPI_DGELU)) || a->ld_aux % 8 == 0) &&
-               (!a->aux || (uintptr_t)a->aux % 16 == 0) && !getenv("MTTS_GEMM_NARROW_OUT");
+               (!a->aux || (uintptr_t)a->aux % 16 == 0) && override_of(MTTS_OVR_GEMM_NARROW) != 1;
   const int nwg = p.tiles_m * p.tiles_n * splits;
   hipStream_t st = (hipStream_t)stream;
   if (!nt) {

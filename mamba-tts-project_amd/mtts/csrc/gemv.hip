@@ -411,10 +411,6 @@ int gemv_split(int K, int* ks_out, int* s_out) {
   const int nsteps = K / 32;
   int ks = 1;
   while (ks < kMaxKS && nsteps % (2 * ks) == 0) ks *= 2;
-  if (const char* e = getenv("MTTS_GEMV_KS")) {   // tuning override
-    const int f = atoi(e);
-    if (f >= 1 && f <= kMaxKS && (f & (f - 1)) == 0 && nsteps % f == 0) ks = f;
-  }
   const int s = nsteps / ks;
   if (s != 1 && s != 2 && s != 4 && s != 8 && s != 16) return 0;
   *ks_out = ks;

@@ -168,8 +168,7 @@ extern "C" int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_
     // chunks -> fp32 partial slab -> sum of the chunks
     MTTS_CHECK(workspace, "colsum: workspace required (mtts_colsum_workspace)");
     // 128-row chunks (tools/bench_colsum.py: 64 / 32 measured equal at 1024 columns, slower at 2048+)
-    const char* e = getenv("MTTS_COLSUM_RCHUNK");
-    const int rchunk = e ? std::max(16, atoi(e)) : 128;
+    const int rchunk = 128;
     const int chunks = (rows + rchunk - 1) / rchunk;
     float* part = (float*)workspace;
     if (dtype == MTTS_F32)

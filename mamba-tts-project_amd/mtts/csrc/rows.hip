@@ -350,10 +350,6 @@ extern "C" int mtts_gemm_rows(const MttsRowsArgs* a, void* stream) {
   const int Kw = K / KG;   // per-workgroup K range
   int U = 4;
   int ks = Kw % (64 * 8) == 0 ? 8 : Kw % (64 * 4) == 0 ? 4 : Kw % (64 * 2) == 0 ? 2 : 1;
-  if (const char* e = getenv("MTTS_ROWS_KS")) {   // tuning override
-    const int f = atoi(e);
-    if ((f == 1 || f == 2 || f == 4 || f == 8 || f == 16) && Kw % (64 * f) == 0) ks = f;
-  }
   int u8 = U == 8;
   if (a->ln_w) {   // LayerNorm prologue: exactly one trip per wave (Kw == ks * 16 * U), ks <= 8
     int f = 0;

@@ -496,234 +496,10 @@ constexpr int wide_pitch_dw(int P, int rowdw, int W) {
   return rowdw + 4;
 }
 
-template <int P, typename Tio, typename Tbc, int MODE, bool SP>
-__global__ __launch_bounds__(kBlock, 4) void scan_fwd_wide_kernel(const MttsScanFwdArgs a, const int seg_len,
-                                                                  float* __restrict__ seg) {
-  constexpr int NS = kN / P;
-  constexpr int CPB = kBlock / P;           // channels per block
-  constexpr int ES = (int)sizeof(Tio);
-  constexpr int ROWB = CPB * ES;            // bytes of a block's timestep row
-  constexpr int TT = 4096 / ROWB;           // timesteps per tile (one 16-B chunk per thread per array)
-  constexpr int G = TT / P;                 // P-step groups per tile
-  constexpr int CPR = ROWB / 16;            // chunks per row
-  constexpr int EPC = 16 / ES;              // elements per chunk
-  constexpr int NA = MODE == kFull ? 3 : 2; // staged arrays: u, delta (, z)
-  constexpr int PIT = wide_pitch_dw(P, ROWB / 4, (64 / P) * ES / 4) * 4 / ES;  // row pitch (elements)
-  constexpr int VPT = TT * 2 * kN / kBlock;
-  static_assert(G >= 1 && TT % P == 0 && (TT * 2 * kN) % kBlock == 0, "tile shape");
-  __shared__ __attribute__((aligned(16))) Tio sX[2][NA][TT * PIT];
-  __shared__ __attribute__((aligned(16))) float sBC[2][TT * 2 * kN];
-
-  const int tid = threadIdx.x;
-  const int j = tid % P, cl = tid / P;
-  const int c0 = blockIdx.x * CPB;
-  const bool cvalid = c0 + cl < a.dim;
-  const int c = cvalid ? c0 + cl : a.dim - 1;
-  const int b = blockIdx.y;
-  const int k = blockIdx.z;
-  const int L = a.seqlen;
-  const int K = (L + seg_len - 1) / seg_len;
-  const int t_begin = k * seg_len;
-  const int t_end = min(L, t_begin + seg_len);
-  const bool has_z = MODE == kFull && a.z != nullptr;
-
-  // chunk this thread moves: row lrow, local channels [lcol, lcol + EPC)
-  const int lrow = tid / CPR, lcol = (tid % CPR) * EPC;
-  const bool lvalid = c0 + lcol < a.dim;  // whole chunk (dim % EPC == 0)
-  const Tio* __restrict__ gu = (const Tio*)a.u + (int64_t)b * a.u_bs + c0 + lcol;
-  const Tio* __restrict__ gd = (const Tio*)a.delta + (int64_t)b * a.delta_bs + c0 + lcol;
-  const Tio* __restrict__ gz = has_z ? (const Tio*)a.z + (int64_t)b * a.z_bs + c0 + lcol : gu;
-  const int64_t z_ls = has_z ? a.z_ls : a.u_ls;
-  Tio* __restrict__ go = (Tio*)a.out + (int64_t)b * a.out_bs + c0 + lcol;
-
-  // B/C staging slice (as in the narrow kernel)
-  const int e0 = tid * VPT;
-  const int st_s = e0 / (2 * kN), st_col = e0 % (2 * kN);
-  const Tbc* __restrict__ st0 = st_col < kN ? (const Tbc*)a.Bm + (int64_t)b * a.B_bs
-                                            : (const Tbc*)a.Cm + (int64_t)b * a.C_bs;
-  const int64_t st_ls = st_col < kN ? a.B_ls : a.C_ls;
-
-  float A2[NS], h[NS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) A2[i] = ld_A(a, (int64_t)c * kN + j * NS + i) * kLog2e;
-  const float Dc = a.D ? a.D[c] : 0.f;
-  const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
-  float S = 0.f;
-  if constexpr (MODE == kFull) {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) h[i] = a.h0 ? a.h0[((int64_t)b * a.dim + c) * kN + j * NS + i] : 0.f;
-    for (int kk = 0; kk < k; ++kk) {
-      const float* sp = seg + (((int64_t)b * K + kk) * a.dim + c) * (kN + 1);
-      const float Sk = sp[kN];
-#pragma unroll
-      for (int i = 0; i < NS; ++i) h[i] = fmaf(__builtin_amdgcn_exp2f(A2[i] * Sk), h[i], sp[j * NS + i]);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) h[i] = 0.f;
-  }
-  const int nck = (MODE == kFull && a.ckpt) ? (L + kSub - 1) / kSub : 0;
-  float* __restrict__ ck0 = nck ? a.ckpt + (int64_t)b * nck * a.dim * kN : nullptr;
-  const uint32_t lck = (uint32_t)(c * kN + j * NS);
-
-  struct TileRegs {
-    uint4 x[NA];
-    RawVec<Tbc, VPT> st;
-  };
-  auto load_tile = [&](int t0, TileRegs& R) __attribute__((always_inline)) {
-#ifndef MTTS_DIAG_NOMEM
-    R.st.load(st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN));
-#else
-#pragma unroll
-    for (int q = 0; q < RawVec<Tbc, VPT>::W; ++q) R.st.w[q] = 0x3f003f00u + (t0 & 3) + q;
-#endif
-    const int t = t0 + lrow;
-    const bool ok = lvalid && t < t_end;
-    const int tc = ok ? t : t_begin;  // any in-range row; the value is discarded
-#ifdef MTTS_DIAG_NOMEM
-    // timing-only build: no HBM reads (values depend on t0 so nothing hoists)
-#pragma unroll
-    for (int q = 0; q < NA; ++q) R.x[q] = make_uint4(0x3f003f00u + (t0 & 7), 0x3e003e00u + q, 0x3f003f00u, 0xbe003e00u);
-    return;
-#endif
-    R.x[0] = *reinterpret_cast<const uint4*>(gu + (int64_t)tc * a.u_ls);
-    R.x[1] = *reinterpret_cast<const uint4*>(gd + (int64_t)tc * a.delta_ls);
-    if constexpr (NA == 3) R.x[2] = *reinterpret_cast<const uint4*>(gz + (int64_t)tc * z_ls);
-    if (!ok) {
-#pragma unroll
-      for (int q = 0; q < NA; ++q) R.x[q] = make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto write_tile = [&](int buf, const TileRegs& R) __attribute__((always_inline)) {
-#pragma unroll
-    for (int q = 0; q < NA; ++q) *reinterpret_cast<uint4*>(&sX[buf][q][lrow * PIT + lcol]) = R.x[q];
-    float v[VPT];
-    R.st.unpack(v);
-#pragma unroll
-    for (int q = 0; q < VPT; ++q) sBC[buf][e0 + q] = v[q];
-  };
-  auto compute_tile = [&](auto tail, int t0, int buf) __attribute__((always_inline)) {
-    constexpr bool TAIL = decltype(tail)::value;
-#ifdef MTTS_DIAG_NOCOMPUTE
-    return;  // timing-only build: the tile image (u) goes straight back out
-#endif
-    static_for<G>([&](auto gc) {
-      constexpr int g = decltype(gc)::value;
-      const int tg = t0 + g * P;
-      if constexpr ((TT % kSub) != 0 || (g * P) % kSub == 0) {
-        if (nck && cvalid && (tg & (kSub - 1)) == 0 && (!TAIL || tg < t_end))
-          store_vec<NS>(ck0 + (int64_t)(tg / kSub) * a.dim * kN + lck, h);
-      }
-      const int sx = (g * P + j) * PIT + cl;  // this lane's (step, channel) in the tile
-      const bool tv = !TAIL || (tg + j < t_end);
-      float dt = cvt_raw((raw_t<Tio>)sX[buf][1][sx]) + bias;
-      if constexpr (SP) dt = softplus_f(dt);
-      if constexpr (TAIL) dt = tv ? dt : 0.f;  // padded steps are the identity map
-      const float ug = cvt_raw((raw_t<Tio>)sX[buf][0][sx]);
-      const float dtu = dt * ug;
-      if constexpr (MODE == kState) S += dt;
-      float yp[P];
-#pragma unroll
-      for (int s = 0; s < P; ++s) {
-        float dts, dtus;
-        if constexpr (P == 2) {
-          dts = s == 0 ? group_bcast<2, 0>(dt) : group_bcast<2, 1>(dt);
-          dtus = s == 0 ? group_bcast<2, 0>(dtu) : group_bcast<2, 1>(dtu);
-        } else {
-          dts = s == 0 ? group_bcast<4, 0>(dt) : s == 1 ? group_bcast<4, 1>(dt)
-              : s == 2 ? group_bcast<4, 2>(dt) : group_bcast<4, 3>(dt);
-          dtus = s == 0 ? group_bcast<4, 0>(dtu) : s == 1 ? group_bcast<4, 1>(dtu)
-               : s == 2 ? group_bcast<4, 2>(dtu) : group_bcast<4, 3>(dtu);
-        }
-        asm volatile("" : "+v"(dts), "+v"(dtus));
-        const f2 dts2 = {dts, dts}, dtus2 = {dtus, dtus};
-        const float* bc = &sBC[buf][(g * P + s) * 2 * kN];
-        f2 y2 = {0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < NS / 4; ++q) {
-          const f4 vb = *reinterpret_cast<const f4*>(bc + j * NS + 4 * q);
-          f4 vc = {};
-          if constexpr (MODE == kFull) vc = *reinterpret_cast<const f4*>(bc + kN + j * NS + 4 * q);
-#pragma unroll
-          for (int p2 = 0; p2 < 2; ++p2) {
-            const int i = 4 * q + 2 * p2;
-            const f2 x = dts2 * f2{A2[i], A2[i + 1]};
-            const f2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
-            const f2 bv = p2 ? f2{vb[2], vb[3]} : f2{vb[0], vb[1]};
-            const f2 hn = __builtin_elementwise_fma(e, f2{h[i], h[i + 1]}, dtus2 * bv);
-            h[i] = hn[0];
-            h[i + 1] = hn[1];
-            if constexpr (MODE == kFull) {
-              const f2 cv = p2 ? f2{vc[2], vc[3]} : f2{vc[0], vc[1]};
-              y2 = __builtin_elementwise_fma(cv, hn, y2);
-            }
-          }
-        }
-        yp[s] = y2[0] + y2[1];
-      }
-      if constexpr (MODE == kFull) {
-        float y = group_reduce_scatter<P>(yp, j);
-        y = fmaf(Dc, ug, y);
-        if (has_z) y *= silu_f(cvt_raw((raw_t<Tio>)sX[buf][2][sx]));
-        stf(&sX[buf][0][sx], y);  // the output replaces u in the tile image
-      }
-#ifndef MTTS_WIDE_FREE_SCHED
-#pragma unroll
-      for (int i = 0; i < NS; ++i) asm volatile("" : "+v"(h[i]));
-      __builtin_amdgcn_sched_barrier(0);
-#endif
-    });
-  };
-  auto store_tile = [&](int t0, int buf) __attribute__((always_inline)) {
-    if constexpr (MODE == kFull) {
-      const int t = t0 + lrow;
-#ifdef MTTS_DIAG_NOMEM
-      const uint4 v = *reinterpret_cast<const uint4*>(&sX[buf][0][lrow * PIT + lcol]);
-      if (v.x == 0x12345u && v.y == 0x777u) go[0] = (Tio)0;  // keep the tile alive, never true
-#else
-      if (lvalid && t < t_end)
-        *reinterpret_cast<uint4*>(go + (int64_t)t * a.out_ls) =
-            *reinterpret_cast<const uint4*>(&sX[buf][0][lrow * PIT + lcol]);
-#endif
-    }
-  };
-
-  const int nfull = (t_end - t_begin) / TT;
-  const int ntiles = (t_end - t_begin + TT - 1) / TT;
-  TileRegs R;
-  load_tile(t_begin, R);
-  write_tile(0, R);
-  for (int it = 0; it < ntiles; ++it) {
-    const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
-    const int buf = it & 1;
-    __syncthreads();                                  // tile it in LDS; buffer buf^1 free
-    if (it + 1 < ntiles) load_tile(t0 + TT, R);       // in flight during the compute
-    if (it < nfull) compute_tile(FalseT{}, t0, buf);
-    else compute_tile(TrueT{}, t0, buf);
-    if (it + 1 < ntiles) write_tile(buf ^ 1, R);
-    if constexpr (MODE == kFull) {
-      __syncthreads();                                // outputs of tile it complete
-      store_tile(t0, buf);
-    }
-  }
-  if constexpr (MODE == kFull) {
-    if (k == K - 1 && a.last_state && cvalid)
-      store_vec<NS>(a.last_state + ((int64_t)b * a.dim + c) * kN + j * NS, h);
-  } else {
-    S = group_allreduce<P>(S);
-    if (cvalid) {
-      float* sp = seg + (((int64_t)b * K + k) * a.dim + c) * (kN + 1);
-#pragma unroll
-      for (int i = 0; i < NS; ++i) sp[j * NS + i] = h[i];
-      if (j == 0) sp[kN] = S;
-    }
-  }
-}
-
 // ------------------------------------------------------------- forward, LDS-DMA tiles, software-pipelined
 // Same tensors, lane mapping (P lanes per channel, NS = 16/P states each),
-// tile image and L-segmentation as scan_fwd_wide_kernel, restructured after
-// profiling that kernel at ~5.7 SIMD cycles per VALU instruction (its groups
+// tile image and L-segmentation as the round-1 wide kernel (removed), restructured after
+// profiling it at ~5.7 SIMD cycles per VALU instruction (its groups
 // were serial chains: B/C LDS read -> wait -> state update -> y, per step):
 //  * u / delta / z tiles go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4,
 //    1 KiB per wave-instruction): no staging VGPRs, no ds_write, no VALU;
@@ -818,6 +594,16 @@ __device__ __forceinline__ void wait_vmem() {
 #define MTTS_DIAG_NOEXP 0
 #endif
 
+// softplus(x) / ln2 for xl = x log2(e): the forward kernels carry dt' = dt / ln2
+// and h' = h / ln2 (see scan_fwd_c1_kernel); torch's x > 20 -> x threshold
+// falls out of the max, log1p's small-argument series covers e < 1e-3
+__device__ __forceinline__ float softplus_l2(float xl) {
+  const float e = __builtin_amdgcn_exp2f(fminf(xl, 64.f));
+  const float lg = __builtin_amdgcn_logf(1.f + e);                  // log2(1 + e)
+  const float sm = e * fmaf(e, -0.5f * kLog2e, kLog2e);              // log2(1 + e) for tiny e
+  return fmaxf(e < 1e-3f ? sm : lg, xl);
+}
+
 template <int P, int ES>
 struct DmaTile {
   static constexpr int CPB = kBlock / P;          // channels per block
@@ -841,7 +627,7 @@ struct DmaTile {
   }
 };
 
-template <int P, typename Tio, typename Tbc, int MODE, bool SP, bool XL>
+template <int P, typename Tio, typename Tbc, int MODE, bool SP>
 __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFwdArgs a, const int seg_len,
                                                                 float* __restrict__ seg) {
   constexpr int NS = kN / P;
@@ -863,13 +649,13 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
 #ifdef MTTS_FWD_NB
   constexpr int NB = MTTS_FWD_NB;  // timing builds: buffer count forced (LDS then sets blocks per CU)
 #else
-  constexpr int NB = (3 * NA * IMG * ES + 2 * TT * 2 * kN * 4 + (XL ? 4096 : 0)) <= 40960 ? 3 : 2;
+  constexpr int NB = (3 * NA * IMG * ES + 2 * TT * 2 * kN * 4 + 4096) <= 40960 ? 3 : 2;
 #endif
   __shared__ __attribute__((aligned(16))) Tio sX[NB][NA][IMG];
   __shared__ __attribute__((aligned(16))) float sBC[2][TT * 2 * kN];
   // per-wave (delta, delta*u) exchange: the lane that formed step s of a
   // group writes its pair, every lane of the channel reads all P pairs
-  __shared__ __attribute__((aligned(16))) float sS[XL ? kBlock / 64 : 1][2][64 / P][P][2];
+  __shared__ __attribute__((aligned(16))) float sS[kBlock / 64][2][64 / P][P][2];
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -907,16 +693,16 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
 #pragma unroll
   for (int p = 0; p < NP2; ++p) {
     const int64_t ai = (int64_t)c * kN + j * NS + 2 * p;
-    A2[p] = f2{ld_A(a, ai) * kLog2e, ld_A(a, ai + 1) * kLog2e};
+    A2[p] = f2{ld_A(a, ai), ld_A(a, ai + 1)};   // log2 domain (scan_fwd_c1_kernel): exp2(dt' A)
   }
-  const float Dc = a.D ? a.D[c] : 0.f;
-  const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
+  const float Dc2 = a.D ? a.D[c] * kLog2e : 0.f;
+  const float bias2 = a.delta_bias ? a.delta_bias[c] * kLog2e : 0.f;
   float S = 0.f;
   if constexpr (MODE == kFull) {
 #pragma unroll
     for (int p = 0; p < NP2; ++p) {
       const int64_t o = ((int64_t)b * a.dim + c) * kN + j * NS + 2 * p;
-      h[p] = a.h0 ? f2{a.h0[o], a.h0[o + 1]} : f2{0.f, 0.f};
+      h[p] = a.h0 ? f2{a.h0[o] * kLog2e, a.h0[o + 1] * kLog2e} : f2{0.f, 0.f};   // h' = h / ln2
     }
     for (int kk = 0; kk < k; ++kk) {
       const float* sp = seg + (((int64_t)b * K + kk) * a.dim + c) * (kN + 1);
@@ -994,16 +780,17 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
   auto scalar = [&](auto tail, int t0, int buf, int g, Scal& o) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail)::value;
     const int sx = at(g * P + j, cl);
-    float dt = cvt_raw((raw_t<Tio>)sX[buf][1][sx]) + bias;
-    if constexpr (SP && !MTTS_DIAG_NOSCALAR) dt = softplus_f(dt);
+    float dt = fmaf(cvt_raw((raw_t<Tio>)sX[buf][1][sx]), kLog2e, bias2);   // dt / ln2
+    if constexpr (SP && !MTTS_DIAG_NOSCALAR) dt = softplus_l2(dt);
     const bool tv = !TAIL || (t0 + g * P + j < t_end);
     o.dt = tv ? dt : 0.f;                             // padded steps: identity map
     o.ug = cvt_raw((raw_t<Tio>)sX[buf][0][sx]);
     o.dtu = tv ? o.dt * o.ug : 0.f;
     if constexpr (MODE == kFull) {
       // branch-free: without z the z image holds u (never used), the gate is 1
-      const float gz = MTTS_DIAG_NOSCALAR ? cvt_raw((raw_t<Tio>)sX[buf][2][sx]) : silu_f(cvt_raw((raw_t<Tio>)sX[buf][2][sx]));
-      o.gate = has_z ? gz : 1.f;
+      const float zv = cvt_raw((raw_t<Tio>)sX[buf][2][sx]);
+      const float gz = MTTS_DIAG_NOSCALAR ? zv : zv * fast_rcp(fmaf(__builtin_amdgcn_exp2f(-zv * kLog2e), kLog2e, kLog2e));
+      o.gate = has_z ? gz : kLn2;   // ln2 silu(z): y = ln2 (C.h' + D log2(e) u) silu(z)
     }
   };
 
@@ -1012,9 +799,11 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
 #ifdef MTTS_DIAG_NOCOMPUTE
     return;
 #endif
-    // publish a group's (delta, delta*u) pairs (XL) for the lanes of the channel
+    // publish a group's (delta, delta*u) pairs for the lanes of the channel
+    // (one ds_write_b64 + two ds_read_b128 per group; the DPP-broadcast form
+    // measured equal on bf16 and 2 % slower on fp32)
     auto put = [&](int pb, const Scal& v) __attribute__((always_inline)) {
-      if constexpr (XL) *reinterpret_cast<float2*>(&sS[wave][pb][cw][j][0]) = make_float2(v.dt, v.dtu);
+      *reinterpret_cast<float2*>(&sS[wave][pb][cw][j][0]) = make_float2(v.dt, v.dtu);
     };
     Scal cur;
     scalar(tail, t0, buf, 0, cur);
@@ -1026,27 +815,18 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
         if (nck && cvalid && (tg & (kSub - 1)) == 0 && (!TAIL || tg < t_end)) {
           float hv[NS];
 #pragma unroll
-          for (int p = 0; p < NP2; ++p) { hv[2 * p] = h[p][0]; hv[2 * p + 1] = h[p][1]; }
+          for (int p = 0; p < NP2; ++p) { hv[2 * p] = h[p][0] * kLn2; hv[2 * p + 1] = h[p][1] * kLn2; }
           store_vec<NS>(ck0 + (int64_t)(tg / kSub) * a.dim * kN + lck, hv);
         }
       }
-      // (2) first: delta / delta*u of the group's P steps to every lane of the channel:
-      // XL from the LDS exchange (published one group ahead), else DPP broadcasts
+      // (2) first: delta / delta*u of the group's P steps to every lane of the
+      // channel, from the LDS exchange (published one group ahead)
       float dts[P], dtus[P];
-      if constexpr (XL) {
-        __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int q = 0; q < P / 2; ++q) {
-          const f4 v = *reinterpret_cast<const f4*>(&sS[wave][g & 1][cw][2 * q][0]);
-          dts[2 * q] = v[0]; dtus[2 * q] = v[1]; dts[2 * q + 1] = v[2]; dtus[2 * q + 1] = v[3];
-        }
-      } else {
-        static_for<P>([&](auto sc) {
-          constexpr int s = decltype(sc)::value;
-          dts[s] = MTTS_DIAG_NODPP ? cur.dt : group_bcast<P, s>(cur.dt);
-          dtus[s] = MTTS_DIAG_NODPP ? cur.dtu + s : group_bcast<P, s>(cur.dtu);
-          asm volatile("" : "+v"(dts[s]), "+v"(dtus[s]));
-        });
+      for (int q = 0; q < P / 2; ++q) {
+        const f4 v = *reinterpret_cast<const f4*>(&sS[wave][g & 1][cw][2 * q][0]);
+        dts[2 * q] = v[0]; dtus[2 * q] = v[1]; dts[2 * q + 1] = v[2]; dtus[2 * q + 1] = v[3];
       }
       // (1) this group's B / C rows (their latency hides under the exponentials)
       f4 Bq[P][NS / 4], Cq[P][NS / 4];
@@ -1068,9 +848,9 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
           const f2 x = f2{dts[s], dts[s]} * A2[p];
           e[s][p] = MTTS_DIAG_NOEXP ? x : f2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
         }
-      // (4) next group's scalar work, off the chain (XL: kept behind the
+      // (4) next group's scalar work, off the chain (kept behind the
       // exponentials so its LDS reads do not wait on this group's B/C reads)
-      if constexpr (XL) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
       Scal nxt;
       if constexpr (g + 1 < G) {
         scalar(tail, t0, buf, g + 1, nxt);
@@ -1096,7 +876,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
       }
       if constexpr (MODE == kFull) {
         float y = MTTS_DIAG_NODPP ? yp[0] + yp[1] + yp[P - 1] : group_reduce_scatter<P>(yp, j);
-        y = fmaf(Dc, cur.ug, y) * cur.gate;
+        y = fmaf(Dc2, cur.ug, y) * cur.gate;
         stf(&sX[buf][0][at(g * P + j, cl)], y);     // the output replaces u in the tile image
       } else {
         S += cur.dt;
@@ -1145,7 +925,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
     if (k == K - 1 && a.last_state && cvalid) {
       float hv[NS];
 #pragma unroll
-      for (int p = 0; p < NP2; ++p) { hv[2 * p] = h[p][0]; hv[2 * p + 1] = h[p][1]; }
+      for (int p = 0; p < NP2; ++p) { hv[2 * p] = h[p][0] * kLn2; hv[2 * p + 1] = h[p][1] * kLn2; }
       store_vec<NS>(a.last_state + ((int64_t)b * a.dim + c) * kN + j * NS, hv);
     }
   } else {
@@ -1416,7 +1196,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
 }
 
 // WIDE: u / delta / z / dout chunks arrive as 16-byte row pieces through LDS
-// and du / ddelta / dz leave the same way (see scan_fwd_wide_kernel).
+// and du / ddelta / dz leave the same way (16-byte row chunks).
 template <typename Tio, typename Tbc, bool SP, bool WIDE>
 __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdArgs a, float* __restrict__ slab,
                                                              float* __restrict__ par, const int seg_len,
@@ -1697,8 +1477,9 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
         const bool q3 = lane & 8;
         float a1 = (q3 ? a2[1] : a2[0]) + xor8(q3 ? a2[0] : a2[1]);
         a1 += xor4(a1, lane);
-        if (!(lane & 4))
-          red[wave][(tl * 2 + (lane >> 5)) * kN + j * kNSB + (((lane >> 4) & 1) << 1) + ((lane >> 3) & 1)] = a1;
+        // lanes l and l^4 hold the same sum and write it to the same slot
+        // (no exec-mask round trip around the store)
+        red[wave][(tl * 2 + (lane >> 5)) * kN + j * kNSB + (((lane >> 4) & 1) << 1) + ((lane >> 3) & 1)] = a1;
       }
       // per-channel results for lane j's timestep: ddt = sum_n A t1 + u * sum_n dh B
       const float dus_j = group_reduce_scatter<kPB>(du_p, j);
@@ -1770,34 +1551,64 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   }
 }
 
-// dB[b,t,n] / dC[b,t,n] = sum over channel blocks of the slab
-__global__ void scan_bwd_reduce_bc(const float* __restrict__ slab, int batch, int nblk, int L, float* dB,
-                                   int64_t dB_bs, int64_t dB_ls, float* dC, int64_t dC_bs, int64_t dC_ls) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)batch * L * 2 * kN;
-  if (idx >= total) return;
-  const int k = idx % (2 * kN);
-  const int t = (idx / (2 * kN)) % L;
-  const int b = idx / (2 * kN * (int64_t)L);
-  const float* p = slab + ((int64_t)b * nblk * L + t) * (2 * kN) + k;
+// One launch for both fixed-order sums of the backward's partials:
+//  * blocks [0, nbc): dB[b,t,n] / dC[b,t,n] = sum over the channel blocks'
+//    slabs, one float4 (4 consecutive n of B|C) per thread, the nblk loads
+//    issued 8 at a time (sums stay in block order);
+//  * blocks [nbc, ..): dA[c,n], dD[c], ddelta_bias[c] = sum over batch x
+//    segments of the per-(b, k, c) partials (A_log given: dA_log = dA * A,
+//    A = -exp(A_log)).
+struct BwdReduceArgs {
+  const float* slab;
+  const float* par;
+  int batch, nblk, L, dim, npar, nbc;
+  float *dB, *dC, *dA, *dD, *dbias;
+  int64_t dB_bs, dB_ls, dC_bs, dC_ls;
+  const float* a_log;
+};
+__global__ __launch_bounds__(256) void scan_bwd_reduce(const BwdReduceArgs r) {
+  if ((int)blockIdx.x < r.nbc) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (b, t, k4)
+    const int64_t total = (int64_t)r.batch * r.L * (2 * kN / 4);
+    if (idx >= total) return;
+    const int k4 = (int)(idx % (2 * kN / 4));
+    const int t = (int)((idx / (2 * kN / 4)) % r.L);
+    const int b = (int)(idx / ((2 * kN / 4) * (int64_t)r.L));
+    const int64_t qs = (int64_t)r.L * 2 * kN;
+    const float* p = r.slab + ((int64_t)b * r.nblk * r.L + t) * (2 * kN) + 4 * k4;
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    int q = 0;
+    for (; q + 8 <= r.nblk; q += 8) {
+      f4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f4*>(p + (q + i) * qs);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc += v[i];
+    }
+    for (; q < r.nblk; ++q) acc += *reinterpret_cast<const f4*>(p + q * qs);
+    const int k = 4 * k4;
+    float* d = k < kN ? r.dB + b * r.dB_bs + t * r.dB_ls + k : r.dC + b * r.dC_bs + t * r.dC_ls + (k - kN);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = acc[i];
+    return;
+  }
+  const int idx = ((int)blockIdx.x - r.nbc) * 256 + threadIdx.x;
+  if (idx >= r.dim * (kN + 2)) return;
+  const int64_t st = (int64_t)r.dim * (kN + 2);
   float s = 0.f;
-  for (int q = 0; q < nblk; ++q) s += p[(int64_t)q * L * 2 * kN];
-  if (k < kN) dB[b * dB_bs + t * dB_ls + k] = s;
-  else dC[b * dC_bs + t * dC_ls + (k - kN)] = s;
-}
-
-// dA[c,n], dD[c], ddelta_bias[c] = sum over batch of the per-(b,c) partials
-// (A_log given: dA_log = dA * A, A = -exp(A_log))
-__global__ void scan_bwd_reduce_par(const float* __restrict__ par, int batch, int dim, float* dA, float* dD,
-                                    float* dbias, const float* __restrict__ a_log) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= dim * (kN + 2)) return;
-  float s = 0.f;
-  for (int b = 0; b < batch; ++b) s += par[(int64_t)b * dim * (kN + 2) + idx];
+  int b = 0;
+  for (; b + 8 <= r.npar; b += 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = r.par[(b + i) * st + idx];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+  }
+  for (; b < r.npar; ++b) s += r.par[b * st + idx];
   const int c = idx / (kN + 2), q = idx % (kN + 2);
-  if (q < kN) dA[c * kN + q] = a_log ? s * -expf(a_log[c * kN + q]) : s;
-  else if (q == kN) { if (dD) dD[c] = s; }
-  else if (dbias) dbias[c] = s;
+  if (q < kN) r.dA[c * kN + q] = r.a_log ? s * -expf(r.a_log[c * kN + q]) : s;
+  else if (q == kN) { if (r.dD) r.dD[c] = s; }
+  else if (r.dbias) r.dbias[c] = s;
 }
 
 // ------------------------------------------------------------- host side
@@ -1821,11 +1632,8 @@ static int check_fwd(const MttsScanFwdArgs* a) {
 }
 
 static int pick_p(int batch, int dim) {
-  const char* e = getenv("MTTS_SCAN_P");
-  if (e) {
-    int p = atoi(e);
-    if (p == 2 || p == 4) return p;
-  }
+  const int p = override_of(MTTS_OVR_SCAN_P);
+  if (p == 2 || p == 4) return p;
   const int64_t ch = (int64_t)batch * dim;
   // aim for >= 4 waves per SIMD on 256 CUs (1024 SIMDs * 4 * 64 lanes)
   if (ch >= 131072) return 2;
@@ -1845,7 +1653,7 @@ static FwdPlan plan_fwd(int batch, int dim, int seqlen) {
   // (C2, B*D = 16384: one pass 0.181 ms vs K = 4 0.195 ms, tools/scan_segs.py)
   int K = (int)((65536 + lanes - 1) / lanes);
   K = std::max(1, std::min(K, seqlen / 128));
-  if (const char* e = getenv("MTTS_SCAN_SEGS")) K = std::max(1, atoi(e));
+  if (override_of(MTTS_OVR_SCAN_SEGS) >= 1) K = override_of(MTTS_OVR_SCAN_SEGS);
   int seg = (seqlen + K - 1) / K;
   seg = std::max(32, (seg + 31) / 32 * 32);
   pl.seg_len = seg;
@@ -1860,7 +1668,7 @@ static FwdPlan plan_bwd(int batch, int dim, int seqlen) {
   const int64_t lanes = (int64_t)batch * dim * kPB;
   int K = (int)((262144 + lanes - 1) / lanes);
   K = std::max(1, std::min(K, seqlen / 128));
-  if (const char* e = getenv("MTTS_SCAN_BWD_SEGS")) K = std::max(1, atoi(e));
+  if (override_of(MTTS_OVR_SCAN_BWD_SEGS) >= 1) K = override_of(MTTS_OVR_SCAN_BWD_SEGS);
   int seg = (seqlen + K - 1) / K;
   seg = std::max(kSub, (seg + kSub - 1) / kSub * kSub);
   pl.seg_len = seg;
@@ -1870,7 +1678,7 @@ static FwdPlan plan_bwd(int batch, int dim, int seqlen) {
 
 // 16-byte chunks of u / delta / z / out rows are addressable (wide kernel)
 static bool wide_io_ok(const MttsScanFwdArgs* a) {
-  if (getenv("MTTS_SCAN_NARROW")) return false;
+  if (override_of(MTTS_OVR_SCAN_PATH) == 3) return false;   // narrow kernels forced
   const int es = a->dtype_io == MTTS_BF16 ? 2 : 4;
   const int64_t epc = 16 / es;
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
@@ -1888,53 +1696,52 @@ static bool wide_io_ok(const MttsScanFwdArgs* a) {
 // 1024 waves), a lane owns ALL 16 states of one channel.  The P-lane
 // machinery of the kernels above (delta / delta*u exchange, the per-step
 // reduce-scatter of y and its lane selects, per-lane B/C slices) disappears:
-// B/C are wave-uniform (broadcast LDS reads) and the per-channel scalar work
-// (softplus, SiLU gate, D skip) runs once per channel-step in the lane that
-// uses it.  VALU per channel-step: 16 v_exp + 32 packed mul/fma + ~20 scalar.
+// B/C are wave-uniform and the per-channel scalar work (softplus, SiLU gate,
+// D skip) runs once per channel-step in the lane that uses it.  VALU per
+// channel-step: 16 v_exp + 32 packed mul/fma + ~16 scalar.
 // One wave per SIMD (the block's LDS makes a block of 4 waves own its CU);
 // the waves are independent: each runs its own LDS-DMA ring of u/delta/z
 // tiles NB-1 tiles ahead and its own B/C staging, with no workgroup barrier.
-// Outputs leave straight from registers (MTTS_C1_DIRECT_STORE, default): one
-// 4- (2-) byte store per lane and step, a wave writing 256 (128) B of one row
-// per instruction.  VMEM issue order per tile `it`: [B/C regs of it+1] [DMA
-// of it+NB-1] [checkpoint stores of tile it, when any] [TT y stores of tile
-// it]; waiting until at most NDMA + TT operations are in flight therefore
-// retires the B/C load and every older DMA, i.e. tile it+1 is complete (the
-// checkpoint stores only make the wait stricter).  With DIRECT_STORE 0 the
-// outputs replace u in the tile image and leave as 16-byte row chunks
-// ([stores of it-1] first, wait for NDMA).
+// Outputs leave straight from registers: one 4- (2-) byte store per lane and
+// step, a wave writing 256 (128) B of one row per instruction.  VMEM issue
+// order per tile `it`: [B/C regs of it+1] [DMA of it+NB-1] [checkpoint stores
+// of tile it, when any] [TT y stores of tile it]; waiting until at most
+// NDMA + TT operations are in flight therefore retires the B/C load and every
+// older DMA, i.e. tile it+1 is complete (the checkpoint stores only make the
+// wait stricter).
 //
-// SMALL (MTTS_C1_SMALL=1): 8-step tiles and a lighter register budget, so TWO
-// workgroups share a CU (<= 80 KiB of LDS and <= 256 registers per lane each):
-// two waves per SIMD, one hiding the other's dependency and memory stalls.
-template <typename Tio, typename Tbc, bool SP, bool HZ, bool SMALL>
-__global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const MttsScanFwdArgs a) {
+// Log2-domain state (round 4): the kernel carries dt' = softplus(x) / ln2 and
+// h' = h / ln2.  Then exp(dt A) = exp2(dt' A) (A unscaled), dt' u B = dt u B / ln2
+// keeps the recurrence h' = exp2(dt' A) h' + dt' u B exact in form, and
+// y = ln2 (C.h' + D log2(e) u): the ln2 rides in the SiLU gate's reciprocal
+// (rcp(fma(e, log2e, log2e)) = ln2 / (1 + e)).  softplus in log2 units is
+// max(log2(1 + 2^min(xl, 64)), xl) for xl = x log2(e) (torch's x > 20 -> x
+// threshold falls out of the max), with log1p's small-argument series below
+// e = 1e-3: 10 VALU per step instead of 14.
+// (B/C rows as wave-uniform scalar loads into SGPRs were tried: the kernel
+// already holds 96 SGPRs, and the 32-64 more spill through v_readlane.)
+
+template <typename Tio, typename Tbc, bool SP, bool HZ>
+__global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdArgs a) {
   constexpr int ES = (int)sizeof(Tio);
   constexpr int EPC = 16 / ES;            // elements per 16-byte chunk
   constexpr int CPR = 64 / EPC;           // chunks per 64-channel row
   constexpr int RPD = 64 / CPR;           // rows per DMA instruction (1 KiB): 4 fp32, 8 bf16
-  constexpr int DPT = ES == 4 ? (SMALL ? 2 : 4) : (SMALL ? 1 : 2);   // DMA instructions per array per tile
-  constexpr int TT = DPT * RPD;           // steps per tile: 16 (SMALL: 8)
-  // tile ring: DMA NB-1 tiles ahead (LDS per block: 155 / 112 KiB; SMALL 76 / 64 KiB)
-  constexpr int NB = ES == 4 ? 3 : (SMALL ? 5 : 4);
+  constexpr int DPT = ES == 4 ? 4 : 2;    // DMA instructions per array per tile
+  constexpr int TT = DPT * RPD;           // steps per tile: 16
+  constexpr int NB = ES == 4 ? 3 : 4;     // tile ring: DMA NB-1 tiles ahead (LDS per block: 155 / 112 KiB)
   constexpr int NAR = HZ ? 3 : 2;
   constexpr int IMG = TT * 64;
   constexpr int BCV = TT * 2 * kN / 64;   // B/C values staged per lane per tile
   constexpr int LPS = 2 * kN / BCV;       // lanes per B/C row
-  constexpr int BCB = BCV * (int)sizeof(Tbc);  // bytes per lane: 8, 16 or 32
+  constexpr int BCB = BCV * (int)sizeof(Tbc);  // bytes per lane: 16 or 32
   constexpr int NBCI = BCB > 16 ? 2 : 1;  // B/C load instructions per tile
   constexpr int NDMA = DPT * NAR;         // DMA instructions per tile
-#ifndef MTTS_C1_EA
-#define MTTS_C1_EA 1
-#endif
-#ifndef MTTS_C1_DIRECT_STORE
-#define MTTS_C1_DIRECT_STORE 1  // y stored per step from registers (0: through the tile image as 16-B row chunks)
-#endif
-  constexpr int EA = MTTS_C1_EA;          // exp(delta*A) formed EA steps ahead of its use
-  static_assert(kN % BCV == 0 && (BCB == 8 || BCB == 16 || BCB == 32), "B/C staging");
+  constexpr int EA = 1;                   // exp(dt*A) formed EA steps ahead of its use
+  static_assert(kN % BCV == 0 && (BCB == 16 || BCB == 32), "B/C staging");
   __shared__ __attribute__((aligned(16))) Tio sX[4][NB][NAR][IMG];
   // one B/C buffer per wave: staging for tile it+1 follows tile it's last read in program order
-  __shared__ __attribute__((aligned(16))) float sBC[4][1][TT * 2 * kN];
+  __shared__ __attribute__((aligned(16))) float sBC[4][TT * 2 * kN];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1957,8 +1764,8 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
   const Tio* __restrict__ gu = (const Tio*)a.u + (int64_t)b * a.u_bs + c0 + dcol;
   const Tio* __restrict__ gd = (const Tio*)a.delta + (int64_t)b * a.delta_bs + c0 + dcol;
   const Tio* __restrict__ gz = HZ ? (const Tio*)a.z + (int64_t)b * a.z_bs + c0 + dcol : gu;
-  Tio* __restrict__ go = (Tio*)a.out + (int64_t)b * a.out_bs + c0 + dcol;
-  Tio* __restrict__ goc = (Tio*)a.out + (int64_t)b * a.out_bs + c;  // direct-store build
+  Tio* __restrict__ goc = (Tio*)a.out + (int64_t)b * a.out_bs + c;
+  // staged B/C: lane -> (step row bs, column bcol of the staged [B | C] row)
   const int bs = lane / LPS, bcol = (lane % LPS) * BCV;
   const Tbc* __restrict__ gbc = bcol < kN ? (const Tbc*)a.Bm + (int64_t)b * a.B_bs + bcol
                                           : (const Tbc*)a.Cm + (int64_t)b * a.C_bs + (bcol - kN);
@@ -1968,33 +1775,34 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
 #pragma unroll
   for (int p = 0; p < kN / 2; ++p) {
     const int64_t ai = (int64_t)c * kN + 2 * p;
-    A2[p] = f2{ld_A(a, ai) * kLog2e, ld_A(a, ai + 1) * kLog2e};
+    A2[p] = f2{ld_A(a, ai), ld_A(a, ai + 1)};                      // log2 domain: exp2(dt' A)
     const int64_t o = ((int64_t)b * a.dim + c) * kN + 2 * p;
-    h[p] = a.h0 ? f2{a.h0[o], a.h0[o + 1]} : f2{0.f, 0.f};
+    h[p] = a.h0 ? f2{a.h0[o] * kLog2e, a.h0[o + 1] * kLog2e} : f2{0.f, 0.f};   // h' = h / ln2
   }
-  const float Dc = a.D ? a.D[c] : 0.f;
-  const float bias = a.delta_bias ? a.delta_bias[c] : 0.f;
+  const float Dc2 = a.D ? a.D[c] * kLog2e : 0.f;
+  const float bias2 = a.delta_bias ? a.delta_bias[c] * kLog2e : 0.f;
   const int nck = a.ckpt ? (L + kSub - 1) / kSub : 0;
   float* __restrict__ ck = nck ? a.ckpt + (int64_t)b * nck * a.dim * kN + (int64_t)c * kN : nullptr;
+  auto store_h = [&](float* dst) __attribute__((always_inline)) {   // h = ln2 h'
+#pragma unroll
+    for (int q = 0; q < kN / 4; ++q) {
+      const f2 lo = h[2 * q] * kLn2, hi = h[2 * q + 1] * kLn2;
+      *reinterpret_cast<f4*>(dst + 4 * q) = f4{lo[0], lo[1], hi[0], hi[1]};
+    }
+  };
 
   uint32_t stg[BCB / 4];
   auto load_bc = [&](int it) __attribute__((always_inline)) {
     const Tbc* p = gbc + (int64_t)min(it * TT + bs, L - 1) * bc_ls;
-    if constexpr (BCB == 8) {
-      uint32_t w[2];
-      ldg_asm<2>(w, p);
-      stg[0] = w[0]; stg[1] = w[1];
-    } else {
 #pragma unroll
-      for (int q = 0; q < NBCI; ++q) {
-        uint32_t w[4];
-        ldg_asm<4>(w, reinterpret_cast<const char*>(p) + 16 * q);
+    for (int q = 0; q < NBCI; ++q) {
+      uint32_t w[4];
+      ldg_asm<4>(w, reinterpret_cast<const char*>(p) + 16 * q);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) stg[4 * q + i] = w[i];
-      }
+      for (int i = 0; i < 4; ++i) stg[4 * q + i] = w[i];
     }
   };
-  auto stage_bc = [&](int bb) __attribute__((always_inline)) {
+  auto stage_bc = [&]() __attribute__((always_inline)) {
     float v[BCV];
     if constexpr (sizeof(Tbc) == 4) {
 #pragma unroll
@@ -2003,7 +1811,7 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
 #pragma unroll
       for (int q = 0; q < BCV / 2; ++q) unpack_bf2(stg[q], v[2 * q], v[2 * q + 1]);
     }
-    float* d = &sBC[wave][bb][bs * 2 * kN + bcol];
+    float* d = &sBC[wave][bs * 2 * kN + bcol];
 #pragma unroll
     for (int q = 0; q < BCV / 4; ++q)
       *reinterpret_cast<f4*>(d + 4 * q) = f4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
@@ -2011,9 +1819,6 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
   auto dma_tile = [&](int it, int buf) __attribute__((always_inline)) {
 #if defined(MTTS_C1_DIAG_NODMA)
     return;   // timing-only builds (tools/diag_build.sh): outputs are wrong; waits below drain to 0
-#endif
-#if defined(MTTS_C1_DIAG_FIXROW)
-    it = 0;   // every tile re-reads tile 0's rows (L2-resident): DMA issue cost without HBM traffic
 #endif
 #pragma unroll
     for (int k = 0; k < DPT; ++k) {
@@ -2023,38 +1828,45 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
       if constexpr (HZ) dma16(gz + (int64_t)t * a.z_ls, &sX[wave][buf][2][k * RPD * 64]);
     }
   };
-  auto store_tile = [&](int it, int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < DPT; ++k) {
-      const int t = it * TT + k * RPD + drow;
-      const uint4 v = *reinterpret_cast<const uint4*>(&sX[wave][buf][0][(k * RPD + drow) * 64 + dcol]);
-      if (t < L) *reinterpret_cast<uint4*>(go + (int64_t)t * a.out_ls) = v;
-    }
-  };
-  auto compute_tile = [&](auto tail, int it, int buf, int bb) __attribute__((always_inline)) {
+  auto compute_tile = [&](auto tail, int it, int buf) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail)::value;
     const int t0 = it * TT;
-    // step 0's B reads go out first (their latency hides under the scalar work);
-    // (2) below: B of step s+1 and C of step s read (broadcast) during step s
+    // B of step s+1 and C of step s are read (broadcast) during step s;
+    // step 0's B goes out first
     f4 bB[2][kN / 4], bC[2][kN / 4];
-    auto read_row = [&](int s, int half, f4 (&o)[kN / 4]) __attribute__((always_inline)) {
-      const f4* p = reinterpret_cast<const f4*>(&sBC[wave][bb][s * 2 * kN + half * kN]);
+    auto lds_row = [&](int s, int half, f4 (&o)[kN / 4]) __attribute__((always_inline)) {
+      const f4* p = reinterpret_cast<const f4*>(&sBC[wave][s * 2 * kN + half * kN]);
 #pragma unroll
       for (int q = 0; q < kN / 4; ++q) o[q] = p[q];
     };
-    read_row(0, 0, bB[0]);
+    auto fetch_B = [&](int s) __attribute__((always_inline)) { lds_row(s, 0, bB[s & 1]); };
+    auto fetch_C = [&](int s) __attribute__((always_inline)) { lds_row(s, 1, bC[s & 1]); };
+    auto Bv = [&](int s, int p) __attribute__((always_inline)) -> f2 {
+      const f4& q = bB[s & 1][p / 2];
+      return (p & 1) ? f2{q[2], q[3]} : f2{q[0], q[1]};
+    };
+    auto Cv = [&](int s, int p) __attribute__((always_inline)) -> f2 {
+      const f4& q = bC[s & 1][p / 2];
+      return (p & 1) ? f2{q[2], q[3]} : f2{q[0], q[1]};
+    };
+    fetch_B(0);
     // (1) the tile's per-channel scalar work up front: TT independent chains
     float dts[TT], dtus[TT], ugs[TT], gates[TT];
 #pragma unroll
     for (int s = 0; s < TT; ++s) {
       const int e = s * 64 + lane;
-      float dt = cvt_raw((raw_t<Tio>)sX[wave][buf][1][e]) + bias;
-      if constexpr (SP) dt = softplus_f(dt);
+      const float xl = fmaf(cvt_raw((raw_t<Tio>)sX[wave][buf][1][e]), kLog2e, bias2);
+      float dt = SP ? softplus_l2(xl) : xl;                          // dt / ln2
       ugs[s] = cvt_raw((raw_t<Tio>)sX[wave][buf][0][e]);
       const bool tv = !TAIL || t0 + s < L;
       dts[s] = tv ? dt : 0.f;                  // padded steps: identity map
       dtus[s] = tv ? dt * ugs[s] : 0.f;
-      gates[s] = HZ ? silu_f(cvt_raw((raw_t<Tio>)sX[wave][buf][2][e])) : 1.f;
+      if constexpr (HZ) {
+        const float zv = cvt_raw((raw_t<Tio>)sX[wave][buf][2][e]);
+        gates[s] = zv * fast_rcp(fmaf(__builtin_amdgcn_exp2f(-zv * kLog2e), kLog2e, kLog2e));   // ln2 silu(z)
+      } else {
+        gates[s] = kLn2;
+      }
     }
     // exp(delta*A) of step s+1 also forms during step s (independent of h):
     // the transcendental stream of one step overlaps the FMA chain of the other
@@ -2069,48 +1881,37 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
 #pragma unroll
     for (int k = 0; k < EA && k < TT; ++k) exps(k, ex[k]);
     // y of step s-1 (from h before step s's update) is formed in step s, so
-    // no step ends on the dependent y tail (sum, D skip, gate, LDS write)
-    auto yout = [&](int s, const f4 (&cq)[kN / 4]) __attribute__((always_inline)) {
+    // no step ends on the dependent y tail (sum, D skip, gate, store)
+    auto yout = [&](int s) __attribute__((always_inline)) {
       f2 ya = {0.f, 0.f}, yb = {0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < kN / 4; ++q) {
-        ya = __builtin_elementwise_fma(f2{cq[q][0], cq[q][1]}, h[2 * q], ya);
-        yb = __builtin_elementwise_fma(f2{cq[q][2], cq[q][3]}, h[2 * q + 1], yb);
+        ya = __builtin_elementwise_fma(Cv(s, 2 * q), h[2 * q], ya);
+        yb = __builtin_elementwise_fma(Cv(s, 2 * q + 1), h[2 * q + 1], yb);
       }
       const f2 y2 = ya + yb;
-      const float y = fmaf(Dc, ugs[s], y2[0] + y2[1]) * gates[s];
+      const float y = fmaf(Dc2, ugs[s], y2[0] + y2[1]) * gates[s];
 #if defined(MTTS_C1_DIAG_NOSTORE)
       asm volatile("" ::"v"(y));
-#elif MTTS_C1_DIRECT_STORE
-      if (!TAIL || t0 + s < L) stf(goc + (int64_t)(t0 + s) * a.out_ls, y);  // one 4-byte store per lane and step
 #else
-      stf(&sX[wave][buf][0][s * 64 + lane], y);  // the output replaces u in the tile image
+      if (!TAIL || t0 + s < L) stf(goc + (int64_t)(t0 + s) * a.out_ls, y);  // one 4-byte store per lane and step
 #endif
     };
 #pragma unroll
     for (int s = 0; s < TT; ++s) {
-      if (nck && s % kSub == 0 && ((t0 + s) & (kSub - 1)) == 0 && (!TAIL || t0 + s < L)) {
-#pragma unroll
-        for (int q = 0; q < kN / 4; ++q)
-          *reinterpret_cast<f4*>(ck + (int64_t)((t0 + s) / kSub) * a.dim * kN + 4 * q) =
-              f4{h[2 * q][0], h[2 * q][1], h[2 * q + 1][0], h[2 * q + 1][1]};
-      }
-      if (s + 1 < TT) read_row(s + 1, 0, bB[(s + 1) & 1]);
-      read_row(s, 1, bC[s & 1]);
+      if (nck && s % kSub == 0 && ((t0 + s) & (kSub - 1)) == 0 && (!TAIL || t0 + s < L))
+        store_h(ck + (int64_t)((t0 + s) / kSub) * a.dim * kN);
+      if (s + 1 < TT) fetch_B(s + 1);
+      fetch_C(s);
       __builtin_amdgcn_sched_barrier(0);
       if (s + EA < TT) exps(s + EA, ex[(s + EA) % (EA + 1)]);
-      if (s >= 1) yout(s - 1, bC[(s - 1) & 1]);
-      const float dtu = dtus[s];
+      if (s >= 1) yout(s - 1);
+      const f2 dtu2 = f2{dtus[s], dtus[s]};
 #pragma unroll
-      for (int q = 0; q < kN / 4; ++q) {
-        const f4 bq = bB[s & 1][q];
-        h[2 * q] = __builtin_elementwise_fma(ex[s % (EA + 1)][2 * q], h[2 * q], f2{dtu, dtu} * f2{bq[0], bq[1]});
-        h[2 * q + 1] =
-            __builtin_elementwise_fma(ex[s % (EA + 1)][2 * q + 1], h[2 * q + 1], f2{dtu, dtu} * f2{bq[2], bq[3]});
-      }
+      for (int p = 0; p < kN / 2; ++p) h[p] = __builtin_elementwise_fma(ex[s % (EA + 1)][p], h[p], dtu2 * Bv(s, p));
       __builtin_amdgcn_sched_barrier(0);
     }
-    yout(TT - 1, bC[(TT - 1) & 1]);
+    yout(TT - 1);
   };
 
   // prologue: B/C of tile 0 and the DMA of tiles 0..NB-2, all complete before tile 0
@@ -2119,17 +1920,16 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
   for (int k = 0; k < NB - 1; ++k)
     if (k < nt) dma_tile(k, k);
   wait_vm<0>(stg);
-  stage_bc(0);
+  stage_bc();
   for (int it = 0; it < nt; ++it) {
     const int buf = it % NB;
     const int prev = (it + NB - 1) % NB;
-    if (!MTTS_C1_DIRECT_STORE && it > 0) store_tile(it - 1, prev);  // its LDS read completes before the DMA below refills it
     const bool more = it + 1 < nt;
     const bool ahead = it + NB - 1 < nt;
     if (more) load_bc(it + 1);
     if (ahead) dma_tile(it + NB - 1, prev);
-    if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf, 0);
-    else compute_tile(TrueT{}, it, buf, 0);
+    if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf);
+    else compute_tile(TrueT{}, it, buf);
     if (more) {
 #if defined(MTTS_C1_DIAG_NODMA) || defined(MTTS_C1_DIAG_NOSTORE)
       // the hand-counted wait below assumes exactly NDMA DMAs and TT stores
@@ -2137,34 +1937,20 @@ __global__ __launch_bounds__(256, SMALL ? 2 : 1) void scan_fwd_c1_kernel(const M
       // (an asm load landing in a reallocated VGPR faults the GPU)
       wait_vm<0>(stg);
 #else
-      if (ahead) wait_vmn<NDMA + (MTTS_C1_DIRECT_STORE ? TT : 0)>(stg);  // stores of a full tile follow the DMA
+      if (ahead) wait_vmn<NDMA + TT>(stg);  // stores of a full tile follow the DMA
       else wait_vm<0>(stg);
 #endif
-      stage_bc(0);
+      stage_bc();
     }
   }
-  if (!MTTS_C1_DIRECT_STORE) store_tile(nt - 1, (nt - 1) % NB);
-  if (a.last_state) {
-#pragma unroll
-    for (int q = 0; q < kN / 4; ++q)
-      *reinterpret_cast<f4*>(a.last_state + ((int64_t)b * a.dim + c) * kN + 4 * q) =
-          f4{h[2 * q][0], h[2 * q][1], h[2 * q + 1][0], h[2 * q + 1][1]};
-  }
+  if (a.last_state) store_h(a.last_state + ((int64_t)b * a.dim + c) * kN);
 }
 
 // the one-lane-per-channel forward applies: whole 64-channel waves, 16-byte
 // B/C staging loads, and (unless forced for tests) B*D filling every SIMD
-// MTTS_C1_SMALL=1: the 8-step-tile, two-waves-per-SIMD form (read per launch).
-// Measured slower at the north-star shape (tools/scan_ab.py, same box,
-// interleaved: fp32 2.171 vs 2.132 ms, bf16 2.062 vs 1.961 ms): the halved
-// tiles double the per-tile overhead and the partner wave contends for the
-// same VALU, so the default stays the 16-step, one-wave-per-SIMD kernel.
-static bool c1_small() {
-  const char* e = getenv("MTTS_C1_SMALL");
-  return e && atoi(e) != 0;
-}
 static bool c1_ok(const MttsScanFwdArgs* a) {
-  if (getenv("MTTS_SCAN_NO_C1") || !wide_io_ok(a) || a->dim % 64) return false;
+  const int path = override_of(MTTS_OVR_SCAN_PATH);
+  if (path == 2 || !wide_io_ok(a) || a->dim % 64) return false;
   const int es = a->dtype_io == MTTS_BF16 ? 2 : 4, eb = a->dtype_bc == MTTS_BF16 ? 2 : 4;
   const int bcb = (32 / es) * 2 * kN / 64 * eb;    // B/C bytes per lane per tile
   const int64_t al = std::min(bcb, 16) / eb;       // element alignment of each load
@@ -2172,8 +1958,13 @@ static bool c1_ok(const MttsScanFwdArgs* a) {
     return ((uintptr_t)p % (al * eb)) == 0 && bs % al == 0 && ls % al == 0;
   };
   if (!ok(a->Bm, a->B_bs, a->B_ls) || !ok(a->Cm, a->C_bs, a->C_ls)) return false;
-  if (getenv("MTTS_SCAN_C1")) return true;
+  if (path == 1) return true;
   return (int64_t)a->batch * a->dim >= 65536;
+}
+template <typename Tio, typename Tbc, bool SP, bool HZ>
+static void launch_c1(const MttsScanFwdArgs* a, hipStream_t st) {
+  hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, HZ>), dim3((a->dim / 64 + 3) / 4, a->batch), dim3(256), 0, st,
+                     *a);
 }
 
 template <int P, typename Tio, typename Tbc, bool SP>
@@ -2181,38 +1972,15 @@ static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream
   const int nbx = (a->dim + kBlock / P - 1) / (kBlock / P);
   float* seg = (float*)a->workspace;
   if (c1_ok(a)) {
-    const dim3 grid((a->dim / 64 + 3) / 4, a->batch);
-    const bool sm = c1_small();
-    if (a->z) {
-      if (sm) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true, true>), grid, dim3(256), 0, st, *a);
-      else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, true, false>), grid, dim3(256), 0, st, *a);
-    } else {
-      if (sm) hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false, true>), grid, dim3(256), 0, st, *a);
-      else hipLaunchKernelGGL((scan_fwd_c1_kernel<Tio, Tbc, SP, false, false>), grid, dim3(256), 0, st, *a);
-    }
-    return;
-  }
-  if (wide_io_ok(a) && !getenv("MTTS_SCAN_FWD_V1")) {
-    if (getenv("MTTS_SCAN_XDPP")) {
-      if (pl.K > 1)
-        hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kState, SP, false>), dim3(nbx, a->batch, pl.K - 1),
-                           dim3(kBlock), 0, st, *a, pl.seg_len, seg);
-      hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kFull, SP, false>), dim3(nbx, a->batch, pl.K),
-                         dim3(kBlock), 0, st, *a, pl.seg_len, seg);
-      return;
-    }
-    if (pl.K > 1)
-      hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kState, SP, true>), dim3(nbx, a->batch, pl.K - 1),
-                         dim3(kBlock), 0, st, *a, pl.seg_len, seg);
-    hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kFull, SP, true>), dim3(nbx, a->batch, pl.K), dim3(kBlock), 0,
-                       st, *a, pl.seg_len, seg);
+    if (a->z) launch_c1<Tio, Tbc, SP, true>(a, st);
+    else launch_c1<Tio, Tbc, SP, false>(a, st);
     return;
   }
   if (wide_io_ok(a)) {
     if (pl.K > 1)
-      hipLaunchKernelGGL((scan_fwd_wide_kernel<P, Tio, Tbc, kState, SP>), dim3(nbx, a->batch, pl.K - 1),
+      hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kState, SP>), dim3(nbx, a->batch, pl.K - 1),
                          dim3(kBlock), 0, st, *a, pl.seg_len, seg);
-    hipLaunchKernelGGL((scan_fwd_wide_kernel<P, Tio, Tbc, kFull, SP>), dim3(nbx, a->batch, pl.K), dim3(kBlock), 0,
+    hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kFull, SP>), dim3(nbx, a->batch, pl.K), dim3(kBlock), 0,
                        st, *a, pl.seg_len, seg);
     return;
   }
@@ -2349,12 +2117,16 @@ extern "C" int mtts_selective_scan_bwd(const MttsScanBwdArgs* a, void* stream) {
     else launch_bwd<bf16_t, bf16_t>(a, pl, slab, par, segw, st);
   }
   MTTS_LAUNCH_CHECK("selective_scan_bwd");
-  const int64_t tot = (int64_t)a->f.batch * L * 2 * kN;
-  hipLaunchKernelGGL(scan_bwd_reduce_bc, dim3((tot + 255) / 256), dim3(256), 0, st, slab, a->f.batch, nblk, L, a->dB,
-                     a->dB_bs, a->dB_ls, a->dC, a->dC_bs, a->dC_ls);
-  MTTS_LAUNCH_CHECK("selective_scan_bwd_reduce_bc");
-  hipLaunchKernelGGL(scan_bwd_reduce_par, dim3((a->f.dim * (kN + 2) + 255) / 256), dim3(256), 0, st, par,
-                     a->f.batch * pl.K, a->f.dim, a->dA, a->dD, a->ddelta_bias, a->f.a_is_log ? a->f.A : nullptr);
-  MTTS_LAUNCH_CHECK("selective_scan_bwd_reduce_par");
+  BwdReduceArgs r{};
+  r.slab = slab; r.par = par;
+  r.batch = a->f.batch; r.nblk = nblk; r.L = L; r.dim = a->f.dim; r.npar = a->f.batch * pl.K;
+  const int64_t nbc4 = (int64_t)a->f.batch * L * (2 * kN / 4);
+  r.nbc = (int)((nbc4 + 255) / 256);
+  r.dB = a->dB; r.dB_bs = a->dB_bs; r.dB_ls = a->dB_ls;
+  r.dC = a->dC; r.dC_bs = a->dC_bs; r.dC_ls = a->dC_ls;
+  r.dA = a->dA; r.dD = a->dD; r.dbias = a->ddelta_bias; r.a_log = a->f.a_is_log ? a->f.A : nullptr;
+  const int npb = (a->f.dim * (kN + 2) + 255) / 256;
+  hipLaunchKernelGGL(scan_bwd_reduce, dim3(r.nbc + npb), dim3(256), 0, st, r);
+  MTTS_LAUNCH_CHECK("selective_scan_bwd_reduce");
   return MTTS_OK;
 }

@@ -440,6 +440,11 @@ extern "C" int mtts_gemm_skinny(const MttsSkinnyArgs* a, void* stream) {
   const int ces = a->c_dtype == MTTS_F32 ? 4 : 2;
   MTTS_CHECK((uintptr_t)a->c % (4 * ces) == 0 && a->ldc % 4 == 0,
              "gemm_skinny: C must be %d-byte aligned with ldc a multiple of 4", 4 * ces);
+  // SMALL_K with bf16 C moves 8 consecutive columns (16 bytes) per lane
+  MTTS_CHECK(a->mode != MTTS_SKINNY_SMALL_K || ces == 4 ||
+                 (a->n % 8 == 0 && a->ldc % 8 == 0 && (uintptr_t)a->c % 16 == 0),
+             "gemm_skinny: SMALL_K with bf16 C needs n %% 8 == 0, ldc %% 8 == 0 and a 16-byte aligned C "
+             "(n=%d ldc=%d)", a->n, a->ldc);
   SkinnyP p;
   p.a = (const bf16_t*)a->a; p.b = (const bf16_t*)a->b; p.c = a->c;
   p.lda = a->lda; p.ldb = a->ldb; p.ldc = a->ldc;
@@ -448,11 +453,7 @@ extern "C" int mtts_gemm_skinny(const MttsSkinnyArgs* a, void* stream) {
   p.beta = a->beta;
   hipStream_t st = (hipStream_t)stream;
   if (a->mode == MTTS_SKINNY_N) {
-    const char* e = getenv("MTTS_SKINNY_MB");
-    const int mb = e ? atoi(e) : 4;   // 64 rows per workgroup (tools/skinny_ab.py: 1 / 2 / 4 rows-blocks)
-    if (mb == 4) launch_skinny_n<4>(p, st);
-    else if (mb == 1) launch_skinny_n<1>(p, st);
-    else launch_skinny_n<2>(p, st);
+    launch_skinny_n<4>(p, st);   // 64 rows per workgroup (tools/skinny_ab.py: 4 row-blocks beat 1 / 2)
   } else {
     const dim3 grid((a->n + 255) / 256, (a->m + 63) / 64);
     switch (a->k / 32) {

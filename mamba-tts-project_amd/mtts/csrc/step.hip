@@ -106,144 +106,6 @@ __global__ void state_update_kernel(const MttsStateUpdateArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------
-// Decode: x_proj fused into the state update (one launch instead of two).
-// x_dbl = u . W_x^T (B <= 32 rows, R + 2N <= 128 columns, K = d_inner) is a
-// reduction over ALL channels, so every workgroup forms the whole (B x n)
-// product itself (768 v_mfma_f32_16x16x32_bf16 at the C4 shape, its 4 waves
-// splitting K, operands from L2: u 128 KiB + W_x 384 KiB), rounds it to bf16
-// as the unfused x_proj output is, keeps it in LDS, then runs the state
-// update (dt_proj dot, exp, h, y; four lanes per (batch, channel), as
-// state_update_kernel) for its CPW channels x all batch rows.
-constexpr int kXsCPW = 32;     // channels per workgroup
-constexpr int kXsMaxN = 128;   // R + 2N
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(256) void xproj_state_kernel(const MttsStateUpdateArgs a, const bf16_t* __restrict__ wx,
-                                                          int nx) {
-  __shared__ __attribute__((aligned(16))) f32x4_t red[3][2 * (kXsMaxN / 16)][64];
-  __shared__ float xd[32][kXsMaxN + 4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int B = a.batch, R = a.dt_rank, N = 16;
-  const int li = lane & 15, kq = (lane >> 4) * 8;
-  const int ncb = (nx + 15) / 16;   // column blocks (<= 8)
-  const bf16_t* ub = (const bf16_t*)a.x;
-  // ---- phase 1: x_dbl (B x nx) = u (B x dim) . wx (nx x dim)^T, K split over the 4 waves
-  const bf16_t* up[2];
-  const bf16_t* wp[kXsMaxN / 16];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) up[r] = ub + (int64_t)min(r * 16 + li, B - 1) * a.x_bs + kq + wave * 32;
-#pragma unroll
-  for (int c = 0; c < kXsMaxN / 16; ++c) wp[c] = wx + (int64_t)min(c * 16 + li, nx - 1) * a.dim + kq + wave * 32;
-  f32x4_t acc[2][kXsMaxN / 16];
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int c = 0; c < kXsMaxN / 16; ++c) acc[r][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int ni = a.dim / 128;   // k-steps of 32 per wave (dim % 128 == 0)
-  uint4 fu[2][2], fw[2][kXsMaxN / 16];
-  auto load = [&](int i, int st) __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) fu[st][r] = *(const uint4*)(up[r] + i * 128);
-#pragma unroll
-    for (int c = 0; c < kXsMaxN / 16; ++c)
-      if (c < ncb) fw[st][c] = *(const uint4*)(wp[c] + i * 128);
-  };
-  load(0, 0);
-  for (int i = 0; i < ni; i += 2) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (i + h < ni) {
-        if (i + h + 1 < ni) load(i + h + 1, h ^ 1);
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-          for (int c = 0; c < kXsMaxN / 16; ++c)
-            if (c < ncb)
-              acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fw[h][c]),
-                                                                  __builtin_bit_cast(bf16x8_t, fu[h][r]), acc[r][c], 0,
-                                                                  0, 0);
-      }
-    }
-  }
-  if (wave > 0) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int c = 0; c < kXsMaxN / 16; ++c)
-        if (c < ncb) red[wave - 1][r * (kXsMaxN / 16) + c][lane] = acc[r][c];
-  }
-  __syncthreads();
-  if (wave == 0) {   // fixed-order sum, bf16 rounding (the unfused x_proj writes bf16), into the LDS table
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int c = 0; c < kXsMaxN / 16; ++c)
-        if (c < ncb) {
-          f32x4_t v = acc[r][c];
-#pragma unroll
-          for (int w = 0; w < 3; ++w) v += red[w][r * (kXsMaxN / 16) + c][lane];
-          const int row = r * 16 + li;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int col = c * 16 + (lane >> 4) * 4 + e;
-            if (row < 32 && col < kXsMaxN) xd[row][col] = bf2f(f2bf(v[e]));
-          }
-        }
-  }
-  __syncthreads();
-  // ---- phase 2: state update of (b, c), c in this workgroup's kXsCPW channels
-  const int j = threadIdx.x & 3;
-  const int c0 = blockIdx.x * kXsCPW;
-  const int npairs = B * kXsCPW;
-  for (int p = threadIdx.x >> 2; p < npairs; p += 64) {
-    const int b = p / kXsCPW, c = c0 + p % kXsCPW;
-    if (c >= a.dim) continue;
-    const int64_t pc = (int64_t)b * a.dim + c;
-    float4* sp = reinterpret_cast<float4*>(a.state + pc * 16) + j;
-    const float4 s = *sp;
-    const float4 A = reinterpret_cast<const float4*>(a.A + (int64_t)c * 16)[j];
-    const float x = bf2f(ub[(int64_t)b * a.x_bs + c]);
-    // fused dt_proj: x_dbl[b, :R] . dt_w[c, :], a quarter of R per lane (R % 32 == 0: host)
-    const bf16_t* wr = (const bf16_t*)a.dt_w + (int64_t)c * R;
-    const int q4 = R >> 2;
-    float s0 = 0.f, s1 = 0.f;
-    for (int r = j * q4; r < (j + 1) * q4; r += 8) {
-      typedef short s16x8 __attribute__((ext_vector_type(8)));
-      const s16x8 wv = *reinterpret_cast<const s16x8*>(wr + r);
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        s0 = fmaf(xd[b][r + e], bf2f((bf16_t)wv[e]), s0);
-        s1 = fmaf(xd[b][r + e + 1], bf2f((bf16_t)wv[e + 1]), s1);
-      }
-    }
-    float dt = s0 + s1;
-    dt += dpp<kQuadXor1>(dt);
-    dt += dpp<kQuadXor2>(dt);
-    dt += a.dt_bias ? a.dt_bias[c] : 0.f;
-    if (a.dt_softplus) dt = softplus_f(dt);
-    const float dtx = dt * x;
-    float h[4] = {s.x, s.y, s.z, s.w};
-    const float Av[4] = {A.x, A.y, A.z, A.w};
-    float y = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float e = __builtin_amdgcn_exp2f(dt * Av[i] * kLog2e);
-      h[i] = fmaf(e, h[i], dtx * xd[b][R + 4 * j + i]);
-      y = fmaf(xd[b][R + N + 4 * j + i], h[i], y);
-    }
-    *sp = make_float4(h[0], h[1], h[2], h[3]);
-    y += dpp<kQuadXor1>(y);
-    y += dpp<kQuadXor2>(y);
-    if (j != 0) continue;
-    if (a.D) y = fmaf(a.D[c], x, y);
-    if (a.z) y *= silu_f(bf2f(((const bf16_t*)a.z)[(int64_t)b * a.z_bs + c]));
-    if (a.out) ((bf16_t*)a.out)[(int64_t)b * a.out_bs + c] = f2bf(y);
-    if (a.out_packed) ((bf16_t*)a.out_packed)[xpk_index(b, c)] = f2bf(y);
-  }
-}
 
 }  // namespace mtts
 
@@ -291,21 +153,3 @@ extern "C" int mtts_selective_state_update(const MttsStateUpdateArgs* a, void* s
   return MTTS_OK;
 }
 
-extern "C" int mtts_xproj_state_update(const MttsStateUpdateArgs* a, const void* wx, int n_xdbl, void* stream) {
-  MTTS_CHECK(a && a->state && a->x && a->A && wx && a->dt_w, "xproj_state_update: null tensor");
-  MTTS_CHECK(a->batch > 0 && a->batch <= 32 && a->dim > 0 && a->dim % 128 == 0,
-             "xproj_state_update: needs 1 <= batch <= 32 and dim %% 128 == 0 (batch=%d dim=%d)", a->batch, a->dim);
-  MTTS_CHECK(a->dstate == 16, "xproj_state_update: dstate must be 16");
-  MTTS_CHECK(a->dtype_io == MTTS_BF16, "xproj_state_update: bf16 activations only");
-  MTTS_CHECK(a->dt_rank > 0 && a->dt_rank % 32 == 0 && n_xdbl == a->dt_rank + 32 && n_xdbl <= kXsMaxN,
-             "xproj_state_update: needs dt_rank %% 32 == 0 and n_xdbl = dt_rank + 2*16 <= %d", kXsMaxN);
-  MTTS_CHECK(((uintptr_t)a->x | (uintptr_t)wx | (uintptr_t)a->dt_w) % 16 == 0 && a->x_bs % 8 == 0,
-             "xproj_state_update: x / W_x / dt_w must be 16-byte aligned, x row stride a multiple of 8");
-  MTTS_CHECK((uintptr_t)a->state % 16 == 0 && (uintptr_t)a->A % 16 == 0, "xproj_state_update: state/A alignment");
-  MTTS_CHECK(a->out || a->out_packed, "xproj_state_update: no output");
-  MTTS_CHECK(!a->out_packed || a->dim % 32 == 0, "xproj_state_update: packed output needs dim %% 32 == 0");
-  const dim3 grid((a->dim + kXsCPW - 1) / kXsCPW);
-  hipLaunchKernelGGL(xproj_state_kernel, grid, dim3(256), 0, (hipStream_t)stream, *a, (const bf16_t*)wx, n_xdbl);
-  MTTS_LAUNCH_CHECK("xproj_state_update");
-  return MTTS_OK;
-}

@@ -26,7 +26,6 @@ Call `reset()` after modifying weights in place between decode steps.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -66,15 +65,31 @@ def _proj_rows(x, w, b=None, act=None):
 
 
 class DecodeEngine:
+    # routing switches for in-process A/B timing (tools/decode_ab.py); the
+    # defaults are the measured-fastest path (DESIGN.md §4 decode)
+    OPTIONS = {"rows": True,       # HIP row-GEMMs (csrc/rows.hip / gemv.hip) instead of hipBLASLt
+               "fused": True,      # fused-epilogue step (LN prologues, residual / conv epilogues)
+               "fuse_conv": True,  # conv update in in_proj's epilogue
+               "packed": True,     # weights re-laid in MFMA fragment order (gemv16)
+               "xpacked": True}    # activation images packed too
+
     def __init__(self, model, use_graph=True, use_rows=True):
         self.m = model
         self.use_graph = use_graph
-        self.use_rows = use_rows and os.environ.get("MTTS_DECODE_ROWS", "1") != "0"
+        self.use_rows = use_rows and self.OPTIONS["rows"]
         self.reset()
 
     def reset(self):
+        # a flag left by the previous session must not surface in the next one:
+        # wait for its copy, then clear host and device flags (check_errors()
+        # before reset() is how a caller observes it)
+        if getattr(self, "_err_ev", None) is not None:
+            self._err_ev.synchronize()
+            self._err_host.zero_()
+            _err_flag(self._err_dev).zero_()
         self._err_host = None
         self._err_ev = None
+        self._err_dev = None
         self.xpk = False
         self.ctx_key = None
         self.ctx_refs = None
@@ -126,7 +141,7 @@ class DecodeEngine:
         the shapes csrc/rows.hip takes (checked once per context)."""
         m = self.m
         if (not self.use_rows or cd != torch.bfloat16 or B > ops.GEMM_ROWS_MAX
-                or os.environ.get("MTTS_DECODE_FUSED", "1") == "0"):
+                or not self.OPTIONS["fused"]):
             return False
         d = m.token_embed.weight.shape[1]
         if not ops.gemm_rows_ln_ok(d):
@@ -190,7 +205,7 @@ class DecodeEngine:
         if self.xpk:
             return self._step_xpk(x, states, ln)
 
-        fuse_conv = os.environ.get("MTTS_DECODE_FUSE_CONV", "1") != "0"
+        fuse_conv = self.OPTIONS["fuse_conv"]
         for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
             conv_state, ssm_state = states[i]
             mm = l.mamba
@@ -216,7 +231,7 @@ class DecodeEngine:
         """Every projection packed and every operand shape the packed
         activation images take (K, N % 32; short key side): the step of
         _step_xpk applies."""
-        if os.environ.get("MTTS_DECODE_XPACKED", "1") == "0":
+        if not self.OPTIONS["xpacked"]:
             return False
         c = self.ctx
         names = self._PACKED
@@ -249,7 +264,6 @@ class DecodeEngine:
         like its weights; the LayerNorm(+FiLM) prologues run on the packed
         rows.  9 launches per layer, as _step_rows."""
         m, c = self.m, self.ctx
-        fuse_xs = os.environ.get("MTTS_DECODE_XS", "0") != "0"   # measured slower (tools/decode_ab.py xs: 1.10 vs 0.77 ms): off
         xp = None   # packed image of the residual stream (none before layer 0)
         for i, (l, p) in enumerate(zip(m.layers, c["layers"])):
             conv_state, ssm_state = states[i]
@@ -258,13 +272,11 @@ class DecodeEngine:
             xz, u, up = ops.gemm_rows(x if xp is None else xp, p["Win_p"],
                                       conv=(conv_state, p["conv_w"], p["conv_b"]), ln=ln(l.norm_mamba),
                                       u_packed=True)
-            if fuse_xs and ops.xproj_state_ok(u, p["Wx"], p["Wdt"]):   # x_proj inside the state update: one launch
-                y = ops.xproj_state_update(ssm_state, u, p["Wx"], p["A"], p["D"], xz[:, di:], p["dt_bias"], True,
-                                           dt_w=p["Wdt"], packed_out=True)
-            else:
-                x_dbl = ops.gemm_rows(up, p["Wx_p"])
-                y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
-                                     xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"], packed_out=True)
+            # (x_proj fused into the state update measured slower, 1.10 vs 0.77 ms
+            # per step: every workgroup pulls 512 KiB through dependent L2 trips)
+            x_dbl = ops.gemm_rows(up, p["Wx_p"])
+            y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
+                                 xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"], packed_out=True)
             x, xp = ops.gemm_rows(y, p["Wout_p"], res=x, packed_out="also")
             q = ops.gemm_rows(xp, p["Wq_p"], p["bq"], ln=ln(l.norm_cross))
             o = attention_decode_packed(q, p["khm"], p["vhm"], l.cross_attn.num_heads, c["kpm"])
@@ -308,21 +320,37 @@ class DecodeEngine:
         return mm_(h, c["Wh"], c["bh"])[:, None]
 
     # -- out-of-range token ids --------------------------------------------------
-    def _check_token_flag(self, dev):
+    def _check_token_flag(self, dev, blocking=False):
         """The fused step embeds through mtts_embed_sum, which zero-fills and
         flags a row whose token id is outside token_embed (nn.Embedding raises
         there, mamba_decoder.py:217).  The flag of an earlier step is read from
-        a pinned copy once its event has completed (no host sync), so a bad id
-        raises IndexError at the next decode_step call at the latest."""
-        if self._err_ev is not None and self._err_ev.query() and int(self._err_host[0]) != 0:
+        a pinned copy; without `blocking` only once its event has completed (no
+        host sync), so the IndexError is best-effort and deferred: it comes at
+        a later decode_step once the GPU has caught up, or at check_errors(),
+        which waits for the copy and is the guarantee."""
+        if self._err_ev is None:
+            return
+        if blocking:
+            self._err_ev.synchronize()
+        elif not self._err_ev.query():
+            return
+        if int(self._err_host[0]) != 0:
             self._err_host.zero_()
             _err_flag(dev).zero_()
             raise IndexError("decode_step: last_token id out of range of token_embed (index out of range in self)")
+
+    def check_errors(self):
+        """Blocking: raise IndexError if any step since the last check embedded
+        an out-of-range token id (call before reset() / at the end of a
+        generation to observe every error)."""
+        if self._err_dev is not None:
+            self._check_token_flag(self._err_dev, blocking=True)
 
     def _post_token_flag(self, dev):
         if self._err_host is None:
             self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._err_ev = torch.cuda.Event()
+            self._err_dev = dev
         self._err_host.copy_(_err_flag(dev), non_blocking=True)
         self._err_ev.record()
 
@@ -341,7 +369,7 @@ class DecodeEngine:
             self.ctx_refs = conds                  # strong references (see _same_ctx)
             self.ctx_versions = tuple(None if t is None else t._version for t in conds)
             self.fused = self._fused_ok(cd, last_token.shape[0])
-            if self.fused and os.environ.get("MTTS_DECODE_PACKED", "1") != "0":
+            if self.fused and self.OPTIONS["packed"]:
                 self._pack_ctx()
             self.xpk = self.fused and self._xpk_ok()
             self.graph = None

@@ -84,10 +84,13 @@ def mm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor = None, gelu_aux:
 def tn_splits(m: int, n: int, k: int) -> int:
     """Split-K factor for the weight gradient: fill >= ~256 workgroups while
     each split keeps >= 1024 of the reduction (C2: in_proj 4, out_proj / FFN
-    8, q / o projections 16; tools/bench_mgemm.py)."""
+    8, q / o projections 16; tools/bench_mgemm.py); with fewer than 64 output
+    tiles a split may go down to 256 (C2's text K/V projection, 1024 tokens x
+    32 tiles: 4 splits instead of 32 workgroups on 256 CUs)."""
     tiles = -(-m // TILE) * -(-n // TILE)
+    min_k = 1024 if tiles >= 64 else 256
     s = 1
-    while tiles * s < 256 and k % (64 * s * 2) == 0 and k // (s * 2) >= 1024:
+    while tiles * s < 256 and k % (64 * s * 2) == 0 and k // (s * 2) >= min_k:
         s *= 2
     return s
 
@@ -116,7 +119,8 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, beta: floa
 # ------------------------------------------------------------------ skinny GEMMs (csrc/skinny.hip)
 SKINNY_N, SKINNY_SMALL_K = 0, 1
 SKINNY = True   # routing switch (in-process A/B: tools/skinny_ab.py)
-SKINNY_TN = False  # x_proj / dt_proj weight gradients on the TN kernel (35.5 vs 33.7 us bmm split: off)
+SKINNY_TN_KERNEL = True  # x_proj / dt_proj weight gradients on the SKINNY_TN kernel (mamba.py; skinny_tn_ok)
+WGRAD_SKINNY_ON_TN = False  # linear.wgrad: skinny weight gradients on the big TN kernel (35.5 vs 33.7 us: off)
 SKINNY_XPROJ = False   # x_proj forward on SKINNY_N (25 vs 21 us hipBLASLt: off)
 
 
@@ -127,7 +131,8 @@ def _skinny_operand(t):
 
 def skinny_ok(a: torch.Tensor, b: torch.Tensor, out_dtype=torch.bfloat16, out: torch.Tensor = None) -> bool:
     """a (m, k) . b (n, k)^T on csrc/skinny.hip: bf16 k-contiguous operands,
-    k % 32 == 0, n % 4 == 0, and either n <= 128 or k <= 128."""
+    k % 32 == 0, n % 4 == 0, and either n <= 128 or k <= 128 (SMALL_K with a
+    bf16 C: n % 8 == 0 and 16-byte C rows)."""
     if not (SKINNY and _skinny_operand(a) and _skinny_operand(b) and a.shape[1] == b.shape[1]):
         return False
     m, k = a.shape
@@ -135,9 +140,14 @@ def skinny_ok(a: torch.Tensor, b: torch.Tensor, out_dtype=torch.bfloat16, out: t
     if m == 0 or k % 32 or n % 4 or not (n <= 128 or k <= 128):
         return False
     if out is not None:
+        out_dtype = out.dtype
         es = 4 if out.dtype == torch.float32 else 2
         if (out.dtype not in (torch.float32, torch.bfloat16) or out.stride(1) != 1 or out.stride(0) % 4
                 or out.data_ptr() % (4 * es) or tuple(out.shape) != (m, n)):
+            return False
+    if n > 128 and out_dtype == torch.bfloat16:
+        # SMALL_K's bf16 stores move 8 columns (16 bytes) per lane (mtts_gemm_skinny)
+        if n % 8 or (out is not None and (out.stride(0) % 8 or out.data_ptr() % 16)):
             return False
     return out_dtype in (torch.float32, torch.bfloat16)
 
@@ -167,7 +177,7 @@ SKINNY_TN_MODE = 2
 def skinny_tn_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
     """a (k, m) wide (m % 128 == 0), b (k, n) narrow (n <= 128, n % 8 == 0),
     both token-major bf16 with 16-byte rows: the SKINNY_TN weight gradient."""
-    return (SKINNY and _skinny_operand(a) and _skinny_operand(b) and a.shape[0] == b.shape[0] and a.shape[0] > 0
+    return (SKINNY and SKINNY_TN_KERNEL and _skinny_operand(a) and _skinny_operand(b) and a.shape[0] == b.shape[0] and a.shape[0] > 0
             and a.shape[1] % 128 == 0 and b.shape[1] <= 128 and b.shape[1] % 8 == 0)
 
 

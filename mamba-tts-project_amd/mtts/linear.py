@@ -187,7 +187,7 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4, out: torch.Tensor 
     if dy.dtype == torch.float32:
         return torch.mm(dy.t(), x, out=out) if out is not None else dy.t() @ x
     big = dy.shape[1] >= HIP_WGRAD_MIN and x.shape[1] >= HIP_WGRAD_MIN
-    skinny = G.SKINNY_TN and min(dy.shape[1], x.shape[1]) >= 64 and max(dy.shape[1], x.shape[1]) >= HIP_WGRAD_MIN
+    skinny = G.WGRAD_SKINNY_ON_TN and min(dy.shape[1], x.shape[1]) >= 64 and max(dy.shape[1], x.shape[1]) >= HIP_WGRAD_MIN
     if ((big or skinny) and G.tn_ok(dy, x)
             and (out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0))):
         return G.mm_tn(dy, x, out=out)

@@ -299,42 +299,6 @@ def state_update(state, x, dt, A, Bm, Cm, D=None, z=None, dt_bias=None, softplus
     return out if yp is None else yp
 
 
-def xproj_state_ok(u, wx, dt_w):
-    """The fused x_proj + state update (mtts_xproj_state_update) takes these
-    decode shapes: bf16, batch <= 32, d_inner % 128 == 0, dt_rank % 32 == 0,
-    16 states, 16-byte aligned row-major operands."""
-    return (u.dtype == torch.bfloat16 and wx.dtype == torch.bfloat16 and dt_w is not None and dt_w.dtype == u.dtype
-            and u.dim() == 2 and u.shape[0] <= 32 and u.shape[1] % 128 == 0 and u.stride(1) == 1 and u.stride(0) % 8 == 0
-            and wx.is_contiguous() and dt_w.is_contiguous() and dt_w.shape[1] % 32 == 0
-            and wx.shape == (dt_w.shape[1] + 32, u.shape[1]) and dt_w.shape[0] == u.shape[1]
-            and all(t.data_ptr() % 16 == 0 for t in (u, wx, dt_w)))
-
-
-def xproj_state_update(state, u, wx, A, D=None, z=None, dt_bias=None, softplus=True, dt_w=None, packed_out=False):
-    """Decode step's x_proj fused into the state update: x_dbl = u wx^T
-    (bf16-rounded) -> dt = x_dbl[:, :R] dt_w^T, B / C = x_dbl[:, R:] ->
-    state update (state (B, D, 16) fp32 IN PLACE).  Returns y as state_update
-    does (a PackedAct with packed_out)."""
-    _check_cuda(state, u, wx, A, dt_w)
-    Bsz, Dm = u.shape
-    yp = PackedAct.empty(Bsz, Dm, u.device) if packed_out else None
-    out = None if packed_out else torch.empty(Bsz, Dm, device=u.device, dtype=u.dtype)
-    a = L.StateUpdateArgs()
-    a.batch, a.dim, a.dstate = Bsz, Dm, state.shape[-1]
-    a.dtype_io, a.dtype_bc, a.dt_softplus = L.dtype_code(u), L.dtype_code(u), int(softplus)
-    a.x_bs = u.stride(0)
-    a.out_bs = 0 if out is None else out.stride(0)
-    if z is not None:
-        a.z_bs = z.stride(0)
-    a.state, a.x, a.A = state.data_ptr(), u.data_ptr(), A.data_ptr()
-    a.D, a.z, a.dt_bias, a.out = L.ptr(D), L.ptr(z), L.ptr(dt_bias), L.ptr(out)
-    a.dt_rank, a.dt_w = dt_w.shape[1], dt_w.data_ptr()
-    if yp is not None:
-        a.out_packed = yp.data.data_ptr()
-    L.call_raw("mtts_xproj_state_update", C.byref(a), wx.data_ptr(), wx.shape[0])
-    return out if yp is None else yp
-
-
 def causal_conv1d_update(x, conv_state, weight, bias=None, activation=None):
     """[upstream] signature: x (B, D), conv_state (B, D, K) fp32 (in place)."""
     return conv_update(x, conv_state, _f32c(weight.reshape(x.shape[1], -1)), _f32c(bias),

@@ -86,20 +86,16 @@ def test_forward_matches_reference(case, dtype):
     close(lse, ref_lse, 1e-5 if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("qt", ["2", "1"])
 @pytest.mark.parametrize("pattern", ["ramp", "steps", "late_spike"])
 @pytest.mark.parametrize("case", [(2, 256, 1100, 4, 64), (1, 128, 700, 2, 128), (2, 256, 128, 4, 64),
                                   (1, 256, 100, 2, 128), (2, 300, 700, 4, 64), (1, 520, 333, 2, 32)])
-def test_forward_deferred_max_rescales(case, pattern, qt, monkeypatch):
+def test_forward_deferred_max_rescales(case, pattern):
     """The bf16 forward kernels defer the running-max update until a row's
     max grows by more than 2^8 (attn.hip softmax_step).  Scores that grow
     along the key axis -- smoothly, in jumps at 32/64-key tile seams, or as
     one late spike -- force rescales on some rows of a wave and deferrals
-    on others; the result must still match the float64 reference.  qt: two
-    32-query tiles per wave (long keys, hd <= 64, >= 256 queries) or one
-    (MTTS_ATTN_FWD_QT=1)."""
+    on others; the result must still match the float64 reference."""
     from mtts import attn_kernels as A
-    monkeypatch.setenv("MTTS_ATTN_FWD_QT", qt)
     B, T, S, H, hd = case
     q, kv, kpm = make(B, T, S, H, hd, torch.float32, seed=3)
     d = H * hd
@@ -184,15 +180,15 @@ def _ref_grads(q, kv, H, kpm, do):
     return q.grad, kv.grad
 
 
-@pytest.mark.parametrize("chunks", [None, "1", "3"])
+@pytest.mark.parametrize("chunks", [None, 1, 3])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", CASES[:6] + [(1, 5, 300, 2, 64), (3, 1, 12, 4, 16)])
-def test_backward_matches_reference(case, dtype, chunks, monkeypatch):
-    if chunks is not None:
-        monkeypatch.setenv("MTTS_ATTN_CHUNKS", chunks)
+def test_backward_matches_reference(case, dtype, chunks):
+    from mtts import _lib as L
     B, T, S, H, hd = case
     q, kv, kpm = make(B, T, S, H, hd, dtype, seed=3)
-    o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
+    with L.override(attn_chunks=chunks):
+        o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
     rq, rkv = _ref_grads(q, kv, H, kpm, do)
     tol = 5e-5 if dtype == torch.float32 else 3e-2
     close(dq, rq, tol)
@@ -223,27 +219,25 @@ def test_north_star_shape_bf16():
     close(dkv[:2], rkv, 3e-2)
 
 
-@pytest.mark.parametrize("path", ["split", "split_dq_v1", "split_kv_v1", "fused"])
+@pytest.mark.parametrize("path", ["split", "split_generic", "fused"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", [(1, 100, 1100, 2, 128), (2, 64, 777, 4, 64), (2, 33, 129, 2, 32),
                                   (1, 300, 260, 2, 128), (1, 300, 700, 2, 64), (2, 160, 300, 8, 64)])
-def test_backward_long_key_side(case, dtype, path, monkeypatch):
+def test_backward_long_key_side(case, dtype, path):
     """Key side longer than one key group (the train.py shape: 5k reference
     keys): the split backward (dQ launch -- wave-per-query-slice kernel for
-    bf16 hd 64/128, or the key-split mode-2 kernel (MTTS_ATTN_DQ_V1) -- then
-    the per-key-group dK/dV launch: register-resident K / V kernel for bf16
-    hd 64, or mode 1 (MTTS_ATTN_KV_V1); (1, 300, 700, 2, 64) runs it over
-    query chunks into partials) and the fused chunked one
-    (MTTS_ATTN_BWD_FUSED) all match."""
-    if path == "fused":
-        monkeypatch.setenv("MTTS_ATTN_BWD_FUSED", "1")
-    if path == "split_dq_v1":
-        monkeypatch.setenv("MTTS_ATTN_DQ_V1", "1")
-    if path == "split_kv_v1":
-        monkeypatch.setenv("MTTS_ATTN_KV_V1", "1")
+    bf16 hd 64/128, or the generic key-split mode-2 kernel -- then the
+    per-key-group dK/dV launch: register-resident K / V kernel for bf16 hd 64,
+    or the generic mode 1; (1, 300, 700, 2, 64) runs it over query chunks
+    into partials) and the fused chunked one all match (paths forced with
+    mtts_set_override: attn_bwd, attn_generic)."""
+    from mtts import _lib as L
     B, T, S, H, hd = case
     q, kv, kpm = make(B, T, S, H, hd, dtype, seed=5)
-    o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
+    force = {"split": dict(attn_bwd=L.ATTN_BWD_SPLIT), "split_generic": dict(attn_bwd=L.ATTN_BWD_SPLIT, attn_generic=1),
+             "fused": dict(attn_bwd=L.ATTN_BWD_FUSED)}[path]
+    with L.override(**force):
+        o, dq, dkv, do = _grads(q, kv, H, kpm, fused=True)
     rq, rkv = _ref_grads(q, kv, H, kpm, do)
     tol = 5e-5 if dtype == torch.float32 else 3e-2
     close(dq, rq, tol)
@@ -265,10 +259,11 @@ def test_backward_c5_shape_bf16(hd):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_single_query_fully_masked_and_generic_agree(dtype, monkeypatch):
+def test_single_query_fully_masked_and_generic_agree(dtype):
     """q_len == 1 (single-query kernel): a fully masked batch row is NaN with
     lse = -inf like torch, other rows match the float64 reference and the
-    generic MFMA kernel (MTTS_ATTN_DECODE_OFF) on the same inputs."""
+    generic MFMA kernel (override attn_generic) on the same inputs."""
+    from mtts import _lib as L
     from mtts import attn_kernels as A
     B, S, H, hd = 4, 77, 8, 128
     q, kv, kpm = make(B, 1, S, H, hd, dtype, seed=3, full_mask_batch=2)
@@ -280,8 +275,8 @@ def test_single_query_fully_masked_and_generic_agree(dtype, monkeypatch):
     tol = 2e-5 if dtype == torch.float32 else 2e-2
     close(out[keep], ref, tol)
     close(lse[keep], ref_lse, 1e-5)
-    monkeypatch.setenv("MTTS_ATTN_DECODE_OFF", "1")
-    out2, _ = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+    with L.override(attn_generic=1):
+        out2, _ = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
     close(out[keep], out2[keep].double(), tol)
 
 

@@ -1,0 +1,141 @@
+"""C5 data parallelism: the train.py step composition (train_harness.TrainStep:
+text encoder -> duration predictor + loss -> style pipeline -> voice-prompt
+embedding -> decoder -> codec CE; reference train.py:168-241) with a
+GradAllReduce over EVERY trainable parameter of the four modules and the two
+FusedClipAdams (clip over the decoder only, Adam over all:
+train.py:152-159, 232-235).
+
+Two ranks (spawned processes) share cuda:0 through the gloo backend (RCCL needs
+one GPU per rank; mtts/dp.py's bucket / hook / averaging path is
+backend-independent), each stepping on its half of the batch.  Reference: one
+process running the same TrainStep without a GradAllReduce on the MEAN of the
+two shards' total losses.  Checks after the first step: every gradient of the
+text encoder, duration predictor and decoder within 1e-5 of its max (fp32; the
+only difference is the order of the cross-shard sum), the style pipeline's
+parameters without gradient on the reference (dead branch) and zero on the
+ranks; after 2 steps every parameter within Adam's rounding-flip bound of the
+reference (see test_gpu_dp.py).  Dropout off (two ranks cannot share one
+dropout stream)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+WORLD, SHARD = 2, 2
+SMALL = dict(d_model=64, d_style=16, dec_layers=2, dec_heads=4, d_ff=128, text_layers=2, text_heads=2, text_d_k=32,
+             text_d_inner=128, dur_filter=64, style_heads=4, max_len=256, dropout=0.0)
+LR = 1e-3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup(grad_allreduce_factory=None):
+    import train_harness as th
+    torch.manual_seed(0)
+    models = th.build_models("cuda", **SMALL)
+    dp = None
+    if grad_allreduce_factory is not None:
+        params = [p for m in models for p in m.parameters() if p.requires_grad]
+        dp = grad_allreduce_factory(params)
+    step = th.TrainStep(models, lr=LR, grad_allreduce=dp)
+    batch = th.synthetic_batch(WORLD * SHARD, "cuda", T_text=12, T_codec=24, T_ref=16, d_style=SMALL["d_style"],
+                               seed=5)
+    return models, step, dp, batch
+
+
+def _shard(batch, r):
+    return {k: v[r * SHARD:(r + 1) * SHARD] for k, v in batch.items()}
+
+
+def _named(models):
+    """Trainable parameters (the text encoder's sinusoid table is a frozen
+    parameter, FastSpeech2's requires_grad=False position_enc)."""
+    return {f"{mn}.{k}": p for mn, m in zip(("te", "dur", "sty", "dec"), models) for k, p in m.named_parameters()
+            if p.requires_grad}
+
+
+def _worker(rank, port, q):
+    import sys
+    import traceback
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mamba-tts-project_amd")]
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        from mtts.dp import GradAllReduce
+        models, step, dp, batch = _setup(lambda ps: GradAllReduce(ps, bucket_mb=0.05, first_bucket_mb=0.01))
+        mine = _shard(batch, rank)
+        grads = None
+        for it in range(2):
+            total = step.losses(mine)[0]
+            step.backward(total)
+            if grads is None:
+                grads = {n: p.grad.detach().cpu().numpy().copy() for n, p in _named(models).items()}
+            step.optimizer_step()
+            print(f"[c5 dp rank {rank}] step {it} done", flush=True)
+        torch.cuda.synchronize()
+        q.put((rank, {n: p.detach().cpu().numpy().copy() for n, p in _named(models).items()}, grads, len(dp.buckets)))
+        dist.destroy_process_group()
+    except Exception:   # report instead of leaving the parent waiting on the queue
+        q.put((rank, None, traceback.format_exc(), 0))
+        raise
+
+
+def test_c5_train_step_dp_world2_matches_single_process_mean_loss():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=150) for _ in range(WORLD)]
+    errors = [r[2] for r in res if r[1] is None]
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert not errors, "worker failed:\n" + "\n".join(errors)
+    for p in procs:
+        assert p.exitcode == 0
+
+    models, step, _, batch = _setup()
+    named = _named(models)
+    ref_grads = None
+    for _ in range(2):
+        total = sum(step.losses(_shard(batch, r))[0] for r in range(WORLD)) / WORLD
+        step.backward(total)
+        if ref_grads is None:
+            ref_grads = {n: None if p.grad is None else p.grad.detach().cpu().clone() for n, p in named.items()}
+        step.optimizer_step()
+    torch.cuda.synchronize()
+
+    for rank, got, grads, nb in res:
+        assert nb > 2, "small buckets must split the flat buffer"
+        for n, p in named.items():
+            g_ref = ref_grads[n]
+            g = torch.from_numpy(grads[n])
+            if n.startswith("sty."):
+                # dead branch in train.py: no gradient on the reference; the flat
+                # buffer hands the optimizer zeros, which Adam turns into no update
+                assert g_ref is None and (g == 0).all(), f"rank {rank} {n}"
+            else:
+                assert g_ref is not None, n
+                g_err = (g - g_ref).abs().max().item()
+                assert g_err <= 1e-5 * max(g_ref.abs().max().item(), 1e-6), f"rank {rank} grad {n}: {g_err:.3e}"
+            err = (torch.from_numpy(got[n]) - p.detach().cpu()).abs()
+            # Adam normalises an update to ~lr: an element whose gradient is at
+            # rounding level may flip sign on one side (<= 2 lr per step)
+            assert err.max().item() <= 4 * LR, f"rank {rank} {n}: {err.max().item():.3e}"
+            assert (err > 1e-5).float().mean().item() <= 2e-3, f"rank {rank} {n}: too many differing elements"

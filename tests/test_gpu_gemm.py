@@ -25,6 +25,16 @@ def rel(x, ref):
     return ((x.float() - ref.float()).abs().max() / ref.float().abs().max().clamp_min(1e-30)).item()
 
 
+def gelu_matches(act, pre):
+    """The epilogue's GELU of the bf16 pre-activation vs F.gelu of the same
+    bf16 values: within one bf16 ulp element-wise (the epilogue evaluates
+    erfc through one polynomial + exp2 with <= 2.8e-6 relative error in fp32,
+    csrc/gemm.hip gelu_f, so a value next to a rounding boundary may round the
+    other way), tiny tail values (|gelu| < 1e-6) within 1e-6 absolute."""
+    ref = F.gelu(pre.float())
+    return bool(((act.float() - ref).abs() <= ref.abs() * 2.0 ** -8 + 1e-6).all())
+
+
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 128), (1000, 264, 192), (300, 1032, 1024),
                                    (16384, 1024, 1024), (1024, 2048, 1024), (37, 8, 64), (4096, 96, 2048)])
 def test_nt_plain(m, n, k):
@@ -61,7 +71,7 @@ def test_nt_gelu_epilogue_matches_torch_exactly():
     ref_pre = torch.addmm(bias, a, b.t())
     assert rel(pre, ref_pre) < 1e-2
     # the activation is F.gelu of the bf16 pre-activation the kernel wrote
-    assert torch.equal(act, F.gelu(pre))
+    assert gelu_matches(act, pre)
 
 
 def test_nt_dgelu_epilogue():
@@ -98,6 +108,8 @@ def test_default_splits_fill_the_chip():
     assert G.tn_splits(4096, 1024, 16384) * 16 * 4 >= 256
     assert G.tn_splits(1024, 1024, 16384) == 16
     assert G.tn_splits(256, 256, 64) == 1
+    assert G.tn_splits(2048, 1024, 1024) == 4     # C2 text K/V: 32 tiles, 1024 tokens
+    assert G.tn_splits(4096, 1024, 16384) == 4 and G.tn_splits(1024, 2048, 16384) == 8
 
 
 def test_refuses_unsupported_shapes():
@@ -135,18 +147,14 @@ def test_ffn_fused_matches_per_op_path():
         assert rel(a, b) < 2e-2, nm
 
 
-@pytest.fixture(params=["2", "1", "0"])
+@pytest.fixture(params=["pingpong", "narrow"])
 def gemm_mode(request):
-    """MTTS_GEMM_PP: 2 = ping-pong persistent (default), 1 = ping-pong with one
-    tile per workgroup, 0 = the round-2 single-group kernel."""
-    import os
-    old = os.environ.get("MTTS_GEMM_PP")
-    os.environ["MTTS_GEMM_PP"] = request.param
-    yield request.param
-    if old is None:
-        os.environ.pop("MTTS_GEMM_PP", None)
-    else:
-        os.environ["MTTS_GEMM_PP"] = old
+    """The ping-pong kernel (default) or the single-group kernel with 8-byte
+    epilogue stores (the fallback for 8-byte-aligned outputs; forced with the
+    gemm_narrow override)."""
+    from mtts import _lib as L
+    with L.override(gemm_narrow=1 if request.param == "narrow" else None):
+        yield request.param
 
 
 @pytest.mark.parametrize("m,n,k", [(16384, 4096, 1024), (16484, 4104, 1024), (4096, 2048, 128), (8192, 1024, 2048)])
@@ -162,7 +170,7 @@ def test_nt_every_kernel_many_tiles(gemm_mode, m, n, k):
     pre = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
     act = G.mm_nt(a, b, bias=bias, gelu_aux=pre)
     assert rel(pre, ref + bias) < 1e-2
-    assert torch.equal(act, F.gelu(pre))
+    assert gelu_matches(act, pre)
     bias16 = rnd(n)
     assert rel(G.mm_nt(a, b, bias=bias16), ref + bias16.float()) < 1e-2
     aux = rnd(m, n, scale=3.0)
@@ -238,6 +246,35 @@ def test_skinny_strided_views_and_accumulate():
     assert rel(du, ref) < 1e-2
 
 
+@pytest.mark.parametrize("n", [132, 260, 264])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_skinny_small_k_ragged_columns(n, beta):
+    """SMALL_K's bf16 stores move 8 columns per lane: n % 8 == 4 with a bf16
+    C is refused (skinny_ok and the C-ABI), never written past the row end;
+    fp32 C (4-column stores) takes n % 4 == 0, with and without accumulate."""
+    torch.manual_seed(n + int(beta))
+    m, k = 200, 64
+    a, b = rnd(m, k), rnd(n, k)
+    if n % 8:
+        assert not G.skinny_ok(a, b, out_dtype=torch.bfloat16)
+        with pytest.raises(RuntimeError, match="SMALL_K with bf16 C"):
+            G.mm_skinny(a, b, out_dtype=torch.bfloat16)
+    else:
+        assert G.skinny_ok(a, b, out_dtype=torch.bfloat16)
+        # a 16-row guard band past C: nothing outside the (m, n) block changes
+        buf = torch.full((m + 16, n), 3.0, device=dev, dtype=torch.bfloat16)
+        c = buf[:m]
+        c0 = c.float().clone()
+        G.mm_skinny(a, b, out=c, beta=beta)
+        assert rel(c, a.float() @ b.float().t() + beta * c0) < 1e-2
+        assert (buf[m:] == 3.0).all()
+    c32 = torch.full((m, n), 0.5, device=dev)
+    ref = a.float() @ b.float().t() + beta * c32
+    assert G.skinny_ok(a, b, out_dtype=torch.float32, out=c32)
+    G.mm_skinny(a, b, out=c32, beta=beta)
+    assert rel(c32, ref) < 1e-5
+
+
 def test_skinny_rejects_bad_shapes():
     a, b = rnd(64, 48), rnd(32, 48)
     assert not G.skinny_ok(a, b)                     # k % 32
@@ -276,3 +313,62 @@ def test_skinny_tn_weight_gradient(k, m, n, trans):
         ref = ref.t()
     assert out.shape == ref.shape
     assert rel(out, ref) < 1e-5
+
+
+# ------------------------------------------------------------------ C2 routing, every hand-written mode
+C2_M = 16384
+
+
+@pytest.mark.parametrize("ragged", [False, True])
+def test_c2_projection_route_every_hand_written_kernel(ragged):
+    """Every GEMM a C2 layer routes to the hand-written kernels (linear.proj /
+    FFN epilogues / linear.wgrad at the default tn_splits), at C2's token count
+    (and ragged: 56 rows fewer, an output width off the 256 tile), bf16
+    operands, against fp32 products of the same operands: bf16 outputs 1e-2 of
+    max, fp32 weight gradients (split-K, fixed-order slab sum) 1e-5."""
+    torch.manual_seed(17 + int(ragged))
+    M = C2_M - (56 if ragged else 0)
+    dn = 8 if ragged else 0
+    nt_cases = {   # name: (n, k, epilogue)
+        "in_proj fwd": (4096 + dn, 1024, None), "in_proj dgrad": (1024 + dn, 4096, None),
+        "out_proj fwd": (1024 + dn, 2048, None), "out_proj dgrad": (2048 + dn, 1024, None),
+        "q / o fwd + bias": (1024 + dn, 1024, "bias"), "FFN1 + bias + GELU": (2048 + dn, 1024, "gelu"),
+        "FFN2 fwd + bias": (1024 + dn, 2048, "bias"), "FFN2 dgrad + GELU'": (2048 + dn, 1024, "dgelu"),
+    }
+    for name, (n, k, epi) in nt_cases.items():
+        x, w = rnd(M, k), rnd(n, k)
+        assert LIN._nt_route(x, w), name
+        ref = x.float() @ w.float().t()
+        if epi is None:
+            got = LIN.proj(x, w)
+            assert rel(got, ref) < 1e-2, name
+        elif epi == "bias":
+            b = rnd(n, dtype=torch.float32)
+            assert rel(LIN.proj(x, w, b), ref + b) < 1e-2, name
+        elif epi == "gelu":
+            b = rnd(n, dtype=torch.float32)
+            pre = torch.empty(M, n, device=dev, dtype=torch.bfloat16)
+            act = G.mm_nt(x, w, bias=b, gelu_aux=pre)
+            assert rel(pre, ref + b) < 1e-2, name
+            assert gelu_matches(act, pre), name
+        else:
+            aux = rnd(M, n, scale=3.0)
+            got = G.mm_nt(x, w, dgelu_aux=aux)
+            assert rel(got, torch.ops.aten.gelu_backward(ref.to(torch.bfloat16), aux)) < 1e-2, name
+    tn_cases = {"in_proj": (4096 + dn, 1024), "out_proj": (1024 + dn, 2048), "q / o": (1024 + dn, 1024),
+                "FFN1": (2048 + dn, 1024), "FFN2": (1024 + dn, 2048)}
+    for name, (m, n) in tn_cases.items():
+        # the token axis is the reduction (k % (64 * splits)): C2's full count,
+        # ragged only in the output dims
+        dy, x = rnd(C2_M, m), rnd(C2_M, n)
+        splits = G.tn_splits(m, n, C2_M)
+        assert G.tn_ok(dy, x) and LIN.HIP_WGRAD_MIN <= min(m, n), name
+        assert splits > 1, f"{name}: C2 weight gradients run split-K"
+        got = LIN.wgrad(dy, x)
+        assert rel(got, dy.float().t() @ x.float()) < 1e-5, f"{name} (splits {splits})"
+        # the default split count also into a row slice with accumulate (beta = 1)
+        full = torch.randn(m + 16, n, device=dev)
+        before = full.clone()
+        G.mm_tn(dy, x, out=full[8:8 + m], beta=1.0)
+        assert rel(full[8:8 + m], before[8:8 + m] + dy.float().t() @ x.float()) < 1e-5, f"{name} beta"
+        assert torch.equal(full[:8], before[:8]) and torch.equal(full[8 + m:], before[8 + m:]), name

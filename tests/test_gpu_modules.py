@@ -244,8 +244,9 @@ def test_decode_engine_out_of_range_token_raises():
     (mamba_decoder.py:217).  The fused engine embeds through mtts_embed_sum,
     which zero-fills the row (no uninitialised memory reaches the logits or
     the states) and flags it; the engine reads the flag without a host sync
-    and raises IndexError at the next decode_step call at the latest, then
-    clears it (the following steps run normally)."""
+    and raises IndexError at a later decode_step (best-effort, deferred) or at
+    the blocking check_errors(), then clears it (the following steps run
+    normally); reset() drops a pending flag so a new session starts clean."""
     import mamba_decoder
     torch.manual_seed(1)
     m = mamba_decoder.MambaTTSDecoder(10, d_model=1024, n_layers=2, n_heads=8, d_ff=2048, d_style=256).to(DEV).eval()
@@ -268,3 +269,16 @@ def test_decode_engine_out_of_range_token_raises():
         torch.cuda.synchronize()
         lg, st = m.decode_step(good, text, z, st, 3)
         assert torch.isfinite(lg).all()
+        # check_errors() is the blocking guarantee; reset() clears a pending flag
+        eng = m._engine
+        eng.check_errors()
+        m.decode_step(bad, text, z, st, 4)
+        with pytest.raises(IndexError, match="out of range"):
+            eng.check_errors()
+        eng.check_errors()
+        m.decode_step(bad, text, z, st, 5)
+        eng.reset()
+        lg, st = m.decode_step(good, text, z, [None, None], 0)
+        torch.cuda.synchronize()
+        m.decode_step(good, text, z, st, 1)
+        eng.check_errors()

@@ -2,7 +2,6 @@
 independent Mamba v1, float64) and the CPU oracle.  Tolerance: the north
 star's 1e-3 relative (fp32), measured as max|err| <= 1e-3 * max|ref| per
 tensor; bf16 I/O runs use a looser, stated bound."""
-import os
 
 import numpy as np
 import pytest
@@ -34,41 +33,24 @@ def g32(a):
     return torch.from_numpy(np.asarray(a)).to(DEV, torch.float32)
 
 
-@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2", "4v1", "2v1:s2", "4d", "2d:s2", "4c1"])
+@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2", "4c1"])
 def scan_p(request):
     """P (lanes per channel) and, with ':sK', a forced split of L into K
     segments for both the forward and the backward (two-pass path); 'n'
     forces the narrow (per-lane element) forward kernel instead of the
-    16-byte-chunk one; 'v1' the register-staged wide forward kernel instead of
-    the LDS-DMA one; 'd' the LDS-DMA kernel with DPP broadcasts instead of
-    the LDS (delta, delta*u) exchange; 'c1' the one-lane-per-channel forward
-    (scan_fwd_c1_kernel) forced below its B*D threshold wherever D % 64 == 0."""
-    keys = ("MTTS_SCAN_P", "MTTS_SCAN_SEGS", "MTTS_SCAN_BWD_SEGS", "MTTS_SCAN_NARROW", "MTTS_SCAN_FWD_V1",
-            "MTTS_SCAN_XDPP", "MTTS_SCAN_C1")
-    old = {k: os.environ.get(k) for k in keys}
+    16-byte-chunk LDS-DMA one; 'c1' the one-lane-per-channel forward
+    (scan_fwd_c1_kernel) below its B*D threshold wherever D % 64 == 0.
+    Forced through the library's kernel-path overrides (mtts_set_override)."""
+    from mtts import _lib as L
     p, _, segs = request.param.partition(":s")
+    path = None
     if p.endswith("c1"):
-        p = p[:-2]
-        os.environ["MTTS_SCAN_C1"] = "1"
-    if p.endswith("v1"):
-        p = p[:-2]
-        os.environ["MTTS_SCAN_FWD_V1"] = "1"
-    if p.endswith("d"):
-        p = p[:-1]
-        os.environ["MTTS_SCAN_XDPP"] = "1"
+        p, path = p[:-2], L.SCAN_C1
     if p.endswith("n"):
-        p = p[:-1]
-        os.environ["MTTS_SCAN_NARROW"] = "1"
-    os.environ["MTTS_SCAN_P"] = p
-    if segs:
-        os.environ["MTTS_SCAN_SEGS"] = segs
-        os.environ["MTTS_SCAN_BWD_SEGS"] = segs
-    yield request.param
-    for k, v in old.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
+        p, path = p[:-1], L.SCAN_NARROW
+    with L.override(scan_p=int(p), scan_path=path, scan_segs=int(segs) if segs else None,
+                    scan_bwd_segs=int(segs) if segs else None):
+        yield request.param
 
 
 @pytest.mark.parametrize("name", ["scan_full.npz", "scan_plain.npz", "scan_short.npz"])
@@ -149,20 +131,11 @@ def _scan_inputs(B, L, D, dtype, bc_dtype, seed, strided_bc=False):
     return u, dl, A, Bm, Cm, Dp, z, bias, h0
 
 
-def _with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update({k: v for k, v in env.items() if v is not None})
-    for k, v in env.items():
-        if v is None:
-            os.environ.pop(k, None)
-    try:
+def _with_path(path, fn):
+    """Run fn with the scan forward path forced (None: automatic)."""
+    from mtts import _lib as L
+    with L.override(scan_path=path):
         return fn()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 @pytest.mark.parametrize("B,L,D", [(1, 1, 64), (2, 37, 128), (3, 200, 192), (2, 1003, 64), (1, 16, 320), (2, 203, 256),
@@ -180,8 +153,8 @@ def test_scan_c1_kernel_vs_oracle(B, L, D, io, bc, with_z, strided):
     z = z if with_z else None
     run = lambda: ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, h0=h0, want_last=True,  # noqa: E731
                                want_ckpt=True)
-    out, last, ck = _with_env({"MTTS_SCAN_C1": "1", "MTTS_SCAN_NO_C1": None}, run)
-    out_w, last_w, ck_w = _with_env({"MTTS_SCAN_C1": None, "MTTS_SCAN_NO_C1": "1"}, run)
+    out, last, ck = _with_path(1, run)       # c1 forced
+    out_w, last_w, ck_w = _with_path(2, run)   # the P-lane LDS-DMA kernel
     ref, rlast = R.selective_scan_ref(*(t.double().cpu() for t in (u.transpose(1, 2), dl.transpose(1, 2), A,
                                                                   Bm.transpose(1, 2), Cm.transpose(1, 2), Dp)),
                                       None if z is None else z.double().cpu().transpose(1, 2),
@@ -203,8 +176,8 @@ def test_scan_c1_north_star_width():
     u, dl, A, Bm, Cm, Dp, z, bias, _ = _scan_inputs(B, L, D, torch.float32, torch.float32, 7)
     dl = dl * 0.2
     run = lambda: ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, want_last=True)  # noqa: E731
-    out, last, _ = _with_env({"MTTS_SCAN_C1": None, "MTTS_SCAN_NO_C1": None}, run)
-    out_w, last_w, _ = _with_env({"MTTS_SCAN_NO_C1": "1"}, run)
+    out, last, _ = _with_path(None, run)
+    out_w, last_w, _ = _with_path(2, run)
     close(out, out_w, rtol=1e-5, name="c1 vs w2 out")
     close(last, last_w, rtol=1e-5, name="c1 vs w2 last")
     for b, c in ((0, 0), (31, 1984)):
@@ -307,8 +280,8 @@ def test_conv1d_tiled_vs_oracle_with_state(shape, dtype):
     LDS sum of the time tiles' dw/db) on the in_proj layout (x = xz[..., :D],
     row stride 2D), ragged L, a prefilled conv_state entering the forward AND
     the backward (pre-activations and dw include the history), vs the float64
-    oracle; the untiled kernels (MTTS_CONV_UNTILED) give the same values."""
-    import os
+    oracle; the untiled kernels (override conv_untiled) give the same values."""
+    from mtts import _lib
     from mtts import ops
     torch.manual_seed(2)
     B, L, D = shape
@@ -331,13 +304,10 @@ def test_conv1d_tiled_vs_oracle_with_state(shape, dtype):
     assert dxz[..., D:].abs().max().item() == 0.0, "dx wrote outside its half of d(xz)"
     close(dw, wr.grad, rtol=tol, name="dw")
     close(db, br.grad, rtol=tol, name="db")
-    os.environ["MTTS_CONV_UNTILED"] = "1"
-    try:
+    with _lib.override(conv_untiled=1):
         out2, _ = ops.conv_fwd(x, w, b, True, state_in=st, want_state=True)
         dxz2 = torch.zeros_like(xz)
         _, dw2, db2 = ops.conv_bwd(x, w, b, go, True, dx=dxz2[..., :D], state_in=st)
-    finally:
-        del os.environ["MTTS_CONV_UNTILED"]
     assert torch.equal(out, out2), "tiled and untiled forward differ"
     assert torch.equal(dxz, dxz2), "tiled and untiled dx differ"
     close(dw2, dw, rtol=1e-5, name="dw tiled vs untiled")
@@ -852,31 +822,3 @@ def test_scan_a_is_log_matches_explicit_A(shape, dtype):
     close(r2[5], r1[5] * A, rtol=tol, name="dA_log")
 
 
-@pytest.mark.parametrize("B,Dm,R", [(32, 2048, 64), (7, 256, 32), (1, 128, 64)])
-def test_xproj_state_update_matches_unfused(B, Dm, R):
-    """Decode: x_proj fused into the state update (mtts_xproj_state_update)
-    equals x_dbl = bf16(u W_x^T) followed by the dt_proj-fused state update:
-    y (row-major and packed image) and the in-place state."""
-    from mtts import ops
-    torch.manual_seed(B + Dm + R)
-    bf = torch.bfloat16
-    u = torch.randn(B, Dm, device=DEV).to(bf)
-    wx = (torch.randn(R + 32, Dm, device=DEV) / Dm ** 0.5).to(bf)
-    wdt = (torch.randn(Dm, R, device=DEV) / R ** 0.5).to(bf)
-    A = -torch.exp(torch.randn(Dm, 16, device=DEV) * 0.5)
-    Dp = torch.randn(Dm, device=DEV)
-    z = torch.randn(B, Dm, device=DEV).to(bf)
-    bias = torch.randn(Dm, device=DEV) * 0.1
-    st0 = torch.randn(B, Dm, 16, device=DEV)
-    assert ops.xproj_state_ok(u, wx, wdt)
-    s1, s2 = st0.clone(), st0.clone()
-    x_dbl = (u.float() @ wx.float().t()).to(bf)
-    y1 = ops.state_update(s1, u, x_dbl[:, :R], A, x_dbl[:, R:R + 16], x_dbl[:, R + 16:], Dp, z, bias, True, dt_w=wdt)
-    y2 = ops.xproj_state_update(s2, u, wx, A, Dp, z, bias, True, dt_w=wdt)
-    close(y2.float(), y1.float(), rtol=2e-2, name="y")
-    close(s2, s1, rtol=2e-2, name="state")
-    if Dm % 32 == 0:
-        s3 = st0.clone()
-        yp = ops.xproj_state_update(s3, u, wx, A, Dp, z, bias, True, dt_w=wdt, packed_out=True)
-        close(yp.unpack().float(), y2.float(), rtol=0, name="packed y")
-        assert torch.equal(s3, s2)

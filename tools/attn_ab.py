@@ -1,10 +1,12 @@
 """Attention fwd/bwd timing at the C2 (T_kv=128) and C5 (T_kv=5248) shapes,
-with env variants (MTTS_ATTN_CHUNKS ...).  python tools/attn_ab.py"""
+with the generic kernels and query-chunk counts forced through the library's
+path overrides (mtts_set_override).  python tools/attn_ab.py"""
 import os
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mamba-tts-project_amd")]
 import torch  # noqa: E402
+from mtts import _lib as L  # noqa: E402
 from mtts import attn_kernels as A  # noqa: E402
 
 
@@ -37,26 +39,12 @@ for name in os.environ.get("SHAPES", "C2,C5,C5m").split(","):
     fl = 4 * B * T * S * d
     tf = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
     print(f"{name} fwd {tf * 1e3:.1f} us {fl / tf / 1e9:.0f} TF/s", flush=True)
-    if name != "C2":
-        os.environ["MTTS_ATTN_FWD_DB"] = "0"
+    with L.override(attn_generic=1):
         tf0 = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
         o0, l0 = A.attention_fwd(q, k, v, H, kpm, want_lse=True)
-        os.environ.pop("MTTS_ATTN_FWD_DB")
-        print(f"{name} fwd single-buffered {tf0 * 1e3:.1f} us {fl / tf0 / 1e9:.0f} TF/s; max|diff| out "
-              f"{(o0.float() - out.float()).abs().max().item():.2e} lse {(l0 - lse).abs().max().item():.2e}", flush=True)
-    if name == "C2":
-        os.environ["MTTS_ATTN_FWD_SHORT"] = "0"
-        tf0 = timed(lambda: A.attention_fwd(q, k, v, H, kpm, want_lse=True))
-        os.environ.pop("MTTS_ATTN_FWD_SHORT")
-        o0, l0 = A.attention_fwd(q, k, v, H, kpm, want_lse=True)
-        os.environ["MTTS_ATTN_FWD_SHORT"] = "0"
-        o1, l1 = A.attention_fwd(q, k, v, H, kpm, want_lse=True)
-        os.environ.pop("MTTS_ATTN_FWD_SHORT")
-        print(f"{name} fwd generic kernel {tf0 * 1e3:.1f} us; short vs generic max|diff| out "
-              f"{(o0.float() - o1.float()).abs().max().item():.2e} lse {(l0 - l1).abs().max().item():.2e}", flush=True)
-    for ch in ([None, "8", "16", "32"] if name == "C2" else [None]):
-        if ch:
-            os.environ["MTTS_ATTN_CHUNKS"] = ch
-        tb = timed(lambda: A.attention_bwd(q, k, v, H, kpm, out, lse, do))
-        os.environ.pop("MTTS_ATTN_CHUNKS", None)
+    print(f"{name} fwd generic kernel {tf0 * 1e3:.1f} us {fl / tf0 / 1e9:.0f} TF/s; max|diff| out "
+          f"{(o0.float() - out.float()).abs().max().item():.2e} lse {(l0 - lse).abs().max().item():.2e}", flush=True)
+    for ch in ([None, 8, 16, 32] if name == "C2" else [None]):
+        with L.override(attn_chunks=ch):
+            tb = timed(lambda: A.attention_bwd(q, k, v, H, kpm, out, lse, do))
         print(f"{name} bwd chunks={ch} {tb * 1e3:.1f} us {2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)

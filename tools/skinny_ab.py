@@ -1,6 +1,6 @@
 """Skinny GEMMs (csrc/skinny.hip) vs torch/hipBLASLt at the C2 Mamba shapes
 (per-op event timings), then the in-process C2 training step with the skinny
-routing on / off (gemm.SKINNY, gemm.SKINNY_TN), interleaved rounds."""
+routing on / off (gemm.SKINNY, gemm.SKINNY_TN_KERNEL), interleaved rounds."""
 import os
 import sys
 import time
@@ -52,11 +52,10 @@ def op_bench():
               f"d(dt) {t(ops['d(dt)       (16384x64, K=2048)'][0]):6.1f} us", flush=True)
     os.environ.pop("MTTS_SKINNY_MB")
     for name, (dy_, x_) in {"dW_dt (2048x64)": (dd, x_dbl[:, :R]), "dW_x (96x2048)": (gx, u)}.items():
-        G.SKINNY_TN = True
+        G.WGRAD_SKINNY_ON_TN = True
         a = t(lambda: LIN.wgrad(dy_, x_))
-        G.SKINNY_TN = False
+        G.WGRAD_SKINNY_ON_TN = False
         b = t(lambda: LIN.wgrad(dy_, x_))
-        G.SKINNY_TN = True
         print(f"{name}: TN {a:6.1f} us   bmm split {b:6.1f} us", flush=True)
     for name, (a_, b_, tr) in {"dW_dt skinny-TN": (dd, x_dbl[:, :R], False), "dW_x^T skinny-TN": (u, gx, True)}.items():
         print(f"{name}: {t(lambda: G.mm_skinny_tn(a_, b_, trans_c=tr)):6.1f} us", flush=True)
