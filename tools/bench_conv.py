@@ -6,7 +6,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mamba-tts-project_amd")]
 import torch  # noqa: E402
-from mtts import ops  # noqa: E402
+from mtts import _lib, ops  # noqa: E402
 
 B, L, D = 8, 2048, 2048
 xz = torch.randn(B, L, 2 * D, device="cuda").to(torch.bfloat16)
@@ -33,11 +33,8 @@ def t(fn, it=20):
 n = B * L * D * 2
 for rnd in range(2):
     for mode in ("tiled", "untiled"):
-        if mode == "untiled":
-            os.environ["MTTS_CONV_UNTILED"] = "1"
-        else:
-            os.environ.pop("MTTS_CONV_UNTILED", None)
-        tf = t(lambda: ops.conv_fwd(x, w, bias, True))
-        tb = t(lambda: ops.conv_bwd(x, w, bias, du, True, dx=dxz[..., :D]))
+        with _lib.override(conv_untiled=int(mode == "untiled")):
+            tf = t(lambda: ops.conv_fwd(x, w, bias, True))
+            tb = t(lambda: ops.conv_bwd(x, w, bias, du, True, dx=dxz[..., :D]))
         print(f"{mode:8s} conv fwd {tf:.1f} us ({2 * n / tf / 1e3:.0f} GB/s)   bwd {tb:.1f} us "
               f"({3 * n / tb / 1e3:.0f} GB/s)", flush=True)

@@ -11,6 +11,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from mtts import ops  # noqa: E402
+from mtts.decode import DecodeEngine  # noqa: E402
 
 
 def t_us(fn, iters=50, reps=20):
@@ -53,7 +54,6 @@ def shapes():
 
 def step(modes=(True, False)):
     import mamba_decoder
-    from mtts.decode import DecodeEngine
     c = dict(bench.C2)
     dev = "cuda"
     torch.manual_seed(0)
@@ -87,36 +87,18 @@ if __name__ == "__main__":
         shapes()
     if "step" in what:
         step()
-    if "tune" in what:
-        for k, v in [("MTTS_DECODE_FUSE_CONV", "0"), ("MTTS_DECODE_FUSE_CONV", "1"), ("MTTS_ROWS_KS", "4"),
-                     ("MTTS_ROWS_KS", "8"), ("MTTS_ROWS_KS", "16")]:
-            os.environ[k] = v
-            print(k, v, end=" ", flush=True)
-            step((True,))
-            os.environ.pop(k)
     if "rowsonly" in what:
         step((True,))
-    if "packed" in what:   # packed-weight projections (csrc/gemv.hip) vs row-major, interleaved
-        for _ in range(2):
-            for pk in ("1", "0"):
-                os.environ["MTTS_DECODE_PACKED"] = pk
-                print("packed", pk, end=" ", flush=True)
-                step((True,))
-        os.environ.pop("MTTS_DECODE_PACKED")
-    if "xpacked" in what:   # packed activation images (csrc/gemv.hip) vs row-major operands, interleaved
-        for _ in range(2):
-            for pk in ("1", "0"):
-                os.environ["MTTS_DECODE_XPACKED"] = pk
-                print("xpacked", pk, end=" ", flush=True)
-                step((True,))
-        os.environ.pop("MTTS_DECODE_XPACKED")
-    if "xs" in what:   # x_proj fused into the state update (mtts_xproj_state_update) vs two launches, interleaved
-        for _ in range(2):
-            for v in ("1", "0"):
-                os.environ["MTTS_DECODE_XS"] = v
-                print("xs", v, end=" ", flush=True)
-                step((True,))
-        os.environ.pop("MTTS_DECODE_XS")
+    # DecodeEngine.OPTIONS A/B, interleaved: python tools/decode_ab.py opt:packed
+    for w in what:
+        if w.startswith("opt:"):
+            key = w[4:]
+            for _ in range(2):
+                for v in (True, False):
+                    DecodeEngine.OPTIONS[key] = v
+                    print(key, v, end=" ", flush=True)
+                    step((True,))
+            DecodeEngine.OPTIONS[key] = True
     if "splitk" in what:   # rows kernels with / without the cross-workgroup K split, interleaved
         for _ in range(2):
             for sk in (True, False):
@@ -124,11 +106,3 @@ if __name__ == "__main__":
                 print("splitk", sk, end=" ", flush=True)
                 step((True,))
         ops.ROWS_SPLITK = True
-    if "modes" in what:
-        for env in ({}, {"MTTS_ROWS_KS": "2"}, {"MTTS_ROWS_KS": "4"}, {"MTTS_ROWS_KS": "8"},
-                    {"MTTS_DECODE_FUSED": "0"}, {}):
-            os.environ.update(env)
-            print(env, end=" ", flush=True)
-            step((True, False))
-            for k in env:
-                os.environ.pop(k)

@@ -46,11 +46,6 @@ def op_bench():
     }
     for name, (a, b) in ops.items():
         print(f"{name}: skinny {t(a):6.1f} us   torch {t(b):6.1f} us", flush=True)
-    for mb in ("1", "2", "4"):
-        os.environ["MTTS_SKINNY_MB"] = mb
-        print(f"  MB={mb}: x_proj fwd {t(ops['x_proj fwd  (16384x96, K=2048)'][0]):6.1f} us   "
-              f"d(dt) {t(ops['d(dt)       (16384x64, K=2048)'][0]):6.1f} us", flush=True)
-    os.environ.pop("MTTS_SKINNY_MB")
     for name, (dy_, x_) in {"dW_dt (2048x64)": (dd, x_dbl[:, :R]), "dW_x (96x2048)": (gx, u)}.items():
         G.WGRAD_SKINNY_ON_TN = True
         a = t(lambda: LIN.wgrad(dy_, x_))
