@@ -55,7 +55,7 @@ const char* mtts_last_error(void);
  * unknown key. */
 enum {
   MTTS_OVR_AUTO = -1,
-  MTTS_OVR_SCAN_PATH = 0,     /* forward: 1 one-lane-per-channel (c1), 2 LDS-DMA P-lane (w2), 3 narrow, 4 c1 wave pairs (c1p) */
+  MTTS_OVR_SCAN_PATH = 0,     /* forward: 1 one-lane-per-channel (c1), 2 LDS-DMA P-lane (w2), 3 narrow */
   MTTS_OVR_SCAN_P = 1,        /* lanes per channel of the P-lane kernels: 2 or 4 */
   MTTS_OVR_SCAN_SEGS = 2,     /* forward L segments (>= 1) */
   MTTS_OVR_SCAN_BWD_SEGS = 3, /* backward L segments (>= 1) */

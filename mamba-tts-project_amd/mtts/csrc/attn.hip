@@ -49,6 +49,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
+// raw buffer resource over `bytes` bytes from p: loads at or past the range read 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
 constexpr int kKB = 64;  // forward: keys per LDS block
 
 __device__ __forceinline__ f32x16 mfma_bf16(s16x8 a, s16x8 b, f32x16 c) {
@@ -333,7 +338,7 @@ __device__ __forceinline__ int kimg(int row, int ch) { return row * HD + 8 * (ch
 // QT = query tiles of 32 per wave: with 2 (hd <= 64) every K / V fragment
 // read from LDS feeds two MFMAs, halving the LDS bytes per MFMA.
 template <int HD, int QT>
-__global__ __launch_bounds__(256) void attn_fwd_db_kernel(MttsAttnFwdArgs a) {
+__global__ __launch_bounds__(256, 4) void attn_fwd_db_kernel(MttsAttnFwdArgs a) {
   // hd 64 / 128: K and V in the unpadded swizzled kimg image (row reads of K,
   // transposed reads of V, both conflict-free; 32 KiB per workgroup at hd 64
   // instead of 43, so 4 workgroups fit a CU); other head dims padded pitches
@@ -371,32 +376,43 @@ __global__ __launch_bounds__(256) void attn_fwd_db_kernel(MttsAttnFwdArgs a) {
   // Loads are issued unconditionally and consumed only in put(): a select or
   // branch on the loaded data in fetch() would make the compiler wait for
   // them before the block's MFMAs, which is exactly what this kernel avoids.
+  // K / V rows as buffer loads (round 4): the lane's row / column byte offset
+  // is fixed, the block's key origin rides in the scalar offset, and rows at
+  // or past kv_len fall outside the buffer's range and read as zeros -- no
+  // per-block 64-bit address arithmetic, clamps or selects (host: every
+  // range below 2 GiB)
   f32x4 pk[NPF], pv[NPF];
   uint32_t praw = 0;
   int pk0 = 0;
-  const uint8_t* mbase = mb ? mb : (const uint8_t*)kbase;
+  const __amdgpu_buffer_rsrc_t rk = brsrc(kbase, (uint32_t)(((int64_t)(a.kv_len - 1) * a.k_ls + HD) * 2));
+  const __amdgpu_buffer_rsrc_t rv = brsrc(vbase, (uint32_t)(((int64_t)(a.kv_len - 1) * a.k_ls + HD) * 2));
+  const __amdgpu_buffer_rsrc_t rm = brsrc(mb ? mb : (const uint8_t*)kbase, mb ? (uint32_t)a.kv_len : 0u);
+  uint32_t ok_[NPF];   // K and V share the row stride (host)
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int idx = tid + 256 * i;
+    const int row = idx / (HD / CH), cc = (idx % (HD / CH)) * CH;
+    ok_[i] = (uint32_t)((row * a.k_ls + cc) * 2);
+  }
   auto fetch = [&](int k0) __attribute__((always_inline)) {
     pk0 = k0;
+    const int sk = (int)(k0 * a.k_ls * 2);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      const int idx = tid + 256 * i;
-      const int row = idx / (HD / CH), cc = (idx % (HD / CH)) * CH;
-      const int kc = min(k0 + row, a.kv_len - 1);
-      pk[i] = *(const f32x4*)(kbase + kc * a.k_ls + cc);
-      pv[i] = *(const f32x4*)(vbase + kc * a.v_ls + cc);
+      pk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, ok_[i], sk, 0));
+      pv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, ok_[i], sk, 0));
     }
-    praw = mbase[mb ? min(k0 + lane, a.kv_len - 1) : 0];
+    praw = __builtin_amdgcn_raw_buffer_load_b8(rm, (uint32_t)lane, k0, 0);
   };
   auto put = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx / (HD / CH), cc = (idx % (HD / CH)) * CH;
-      const bool in = pk0 + row < a.kv_len;
       const int ko = SWZ ? kimg<HD>(row, cc / CH) : row * KP + cc;
       const int vo = SWZ ? kimg<HD>(row, cc / CH) : row * VP + cc;
-      *(f32x4*)(sK[buf] + ko) = in ? pk[i] : f32x4{};
-      *(f32x4*)(sV[buf] + vo) = in ? pv[i] : f32x4{};
+      *(f32x4*)(sK[buf] + ko) = pk[i];
+      *(f32x4*)(sV[buf] + vo) = pv[i];
     }
     const bool ok = pk0 + lane < a.kv_len && !(mb && praw);
     const uint64_t bal = __ballot(ok);
@@ -1027,30 +1043,37 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
     for (int dt = 0; dt < ND; ++dt) oT[u][dt] = kimg<HD>(4 * h + qq + 8 * u, 4 * dt + 2 * g + (pp >> 1)) + 4 * (pp & 1);
 
   // block staging: loads issued unconditionally, consumed only in put()
+  // buffer loads as attn_fwd_db_kernel: rows past kv_len read zeros (host:
+  // K and V share the row stride, 31-bit spans)
   f32x4 pk[NPF], pv[NPF];
   uint32_t praw = 0;
   int pk0 = 0;
-  const uint8_t* mbase = mb ? mb : (const uint8_t*)kbase;
+  const __amdgpu_buffer_rsrc_t rk = brsrc(kbase, (uint32_t)(((int64_t)(f.kv_len - 1) * f.k_ls + HD) * 2));
+  const __amdgpu_buffer_rsrc_t rv = brsrc(vbase, (uint32_t)(((int64_t)(f.kv_len - 1) * f.k_ls + HD) * 2));
+  const __amdgpu_buffer_rsrc_t rm = brsrc(mb ? mb : (const uint8_t*)kbase, mb ? (uint32_t)f.kv_len : 0u);
+  uint32_t ok_[NPF];
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int idx = tid + 256 * i;
+    ok_[i] = (uint32_t)(((idx / (HD / 8)) * f.k_ls + (idx % (HD / 8)) * 8) * 2);
+  }
   auto fetch = [&](int k0) __attribute__((always_inline)) {
     pk0 = k0;
+    const int sk = (int)(k0 * f.k_ls * 2);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      const int idx = tid + 256 * i;
-      const int row = idx / (HD / 8), cc = (idx % (HD / 8)) * 8;
-      const int kc = min(k0 + row, f.kv_len - 1);
-      pk[i] = *(const f32x4*)(kbase + (int64_t)kc * f.k_ls + cc);
-      pv[i] = *(const f32x4*)(vbase + (int64_t)kc * f.v_ls + cc);
+      pk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, ok_[i], sk, 0));
+      pv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, ok_[i], sk, 0));
     }
-    praw = mbase[mb ? min(k0 + lane, f.kv_len - 1) : 0];
+    praw = __builtin_amdgcn_raw_buffer_load_b8(rm, (uint32_t)lane, k0, 0);
   };
   auto put = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx / (HD / 8), ch = idx % (HD / 8);
-      const bool in = pk0 + row < f.kv_len;
-      *(f32x4*)(sK[buf] + kimg<HD>(row, ch)) = in ? pk[i] : f32x4{};
-      *(f32x4*)(sV[buf] + kimg<HD>(row, ch)) = in ? pv[i] : f32x4{};
+      *(f32x4*)(sK[buf] + kimg<HD>(row, ch)) = pk[i];
+      *(f32x4*)(sV[buf] + kimg<HD>(row, ch)) = pv[i];
     }
     const bool ok = pk0 + lane < f.kv_len && !(mb && praw);
     const uint64_t bal = __ballot(ok);
@@ -1351,7 +1374,9 @@ void launch_fwd(const MttsAttnFwdArgs* a, hipStream_t st) {
   const int nw = a->q_len >= 128 ? 4 : (a->q_len + 31) / 32;
   dim3 grid((a->q_len + 32 * nw - 1) / (32 * nw), a->heads, a->batch);
   if constexpr (sizeof(T) == 2 && HD >= 32) {
-    if (nw == 4 && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1) {
+    // K / V rows by buffer loads: one row stride, 31-bit byte spans
+    const bool span_ok = a->k_ls == a->v_ls && (int64_t)(a->kv_len + 64) * a->k_ls * 2 < (1ll << 31);
+    if (nw == 4 && span_ok && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1) {
       // (two 32-query tiles per wave sharing every K / V fragment read, QT = 2,
       // measured equal to QT = 1 at the C5 shape: 717 vs 680-720 us)
       attn_fwd_db_kernel<HD, 1><<<grid, 256, 0, st>>>(*a);

@@ -528,6 +528,25 @@ __device__ __forceinline__ void dma16(const void* g, void* lds) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(l) : "memory", "m0");
 #endif
 }
+// The same LDS-DMA as a buffer load (round 4): base / range in an SGPR
+// descriptor, a lane-constant byte offset in voff and the tile's row origin
+// in the scalar offset, so a DMA costs no per-lane address arithmetic; rows at
+// or past the range read 0.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 rsrc4(const void* p, uint32_t bytes) {   // p, bytes wave-uniform
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  return i32x4{__builtin_amdgcn_readfirstlane((int)(uint32_t)a), __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff)),
+               __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* lds) {   // wave-uniform LDS byte address
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds);
+}
+__device__ __forceinline__ void dma16b(const i32x4& rs, uint32_t voff, int soff, uint32_t lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen nt lds"
+               ::"v"(voff), "s"(lds), "s"(rs), "s"(soff) : "memory", "m0");
+#endif
+}
 // W-dword global load into registers, invisible to the compiler's wait
 // insertion (so a later LDS-DMA can stay in flight past its consumer);
 // consume only after wait_vm<N>(regs) with the loads counted.
@@ -1760,11 +1779,22 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
   const int L = a.seqlen;
   const int nt = (L + TT - 1) / TT;
 
+  // u / delta / z / out addressed through buffer descriptors over the wave's
+  // 64-channel column of the batch row (host: byte spans below 2 GiB): a
+  // lane-constant offset + the row origin in a scalar register
   const int drow = lane / CPR, dcol = (lane % CPR) * EPC;
-  const Tio* __restrict__ gu = (const Tio*)a.u + (int64_t)b * a.u_bs + c0 + dcol;
-  const Tio* __restrict__ gd = (const Tio*)a.delta + (int64_t)b * a.delta_bs + c0 + dcol;
-  const Tio* __restrict__ gz = HZ ? (const Tio*)a.z + (int64_t)b * a.z_bs + c0 + dcol : gu;
-  Tio* __restrict__ goc = (Tio*)a.out + (int64_t)b * a.out_bs + c;
+  auto span = [&](int64_t ls) { return (uint32_t)(((int64_t)(L - 1) * ls + 64) * ES); };
+  const i32x4 ru = rsrc4((const Tio*)a.u + (int64_t)b * a.u_bs + c0, span(a.u_ls));
+  const i32x4 rd = rsrc4((const Tio*)a.delta + (int64_t)b * a.delta_bs + c0, span(a.delta_ls));
+  const i32x4 rz = HZ ? rsrc4((const Tio*)a.z + (int64_t)b * a.z_bs + c0, span(a.z_ls)) : ru;
+  const uint32_t vu = (uint32_t)((drow * a.u_ls + dcol) * ES), vd = (uint32_t)((drow * a.delta_ls + dcol) * ES);
+  const uint32_t vz = HZ ? (uint32_t)((drow * a.z_ls + dcol) * ES) : vu;
+  const uint32_t sx0 = lds_u32(&sX[wave][0][0][0]);   // this wave's tile ring
+  const uint64_t op = (uint64_t)(uintptr_t)((Tio*)a.out + (int64_t)b * a.out_bs + c0);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(   // wave-uniform: no waterfall
+      (void*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(op >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)op)),
+      0, __builtin_amdgcn_readfirstlane((int)span(a.out_ls)), 0x00020000);
   // staged B/C: lane -> (step row bs, column bcol of the staged [B | C] row)
   const int bs = lane / LPS, bcol = (lane % LPS) * BCV;
   const Tbc* __restrict__ gbc = bcol < kN ? (const Tbc*)a.Bm + (int64_t)b * a.B_bs + bcol
@@ -1820,12 +1850,14 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
 #if defined(MTTS_C1_DIAG_NODMA)
     return;   // timing-only builds (tools/diag_build.sh): outputs are wrong; waits below drain to 0
 #endif
+    const uint32_t lb = sx0 + (uint32_t)(buf * NAR * IMG * ES);
 #pragma unroll
     for (int k = 0; k < DPT; ++k) {
-      const int t = min(it * TT + k * RPD + drow, L - 1);  // rows past L: any valid row (never stored)
-      dma16(gu + (int64_t)t * a.u_ls, &sX[wave][buf][0][k * RPD * 64]);
-      dma16(gd + (int64_t)t * a.delta_ls, &sX[wave][buf][1][k * RPD * 64]);
-      if constexpr (HZ) dma16(gz + (int64_t)t * a.z_ls, &sX[wave][buf][2][k * RPD * 64]);
+      const int t = it * TT + k * RPD;   // rows past L read zeros (never stored)
+      const uint32_t lk = lb + (uint32_t)(k * RPD * 64 * ES);
+      dma16b(ru, vu, (int)(t * a.u_ls * ES), lk);
+      dma16b(rd, vd, (int)(t * a.delta_ls * ES), lk + IMG * ES);
+      if constexpr (HZ) dma16b(rz, vz, (int)(t * a.z_ls * ES), lk + 2 * IMG * ES);
     }
   };
   auto compute_tile = [&](auto tail, int it, int buf) __attribute__((always_inline)) {
@@ -1894,7 +1926,11 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
 #if defined(MTTS_C1_DIAG_NOSTORE)
       asm volatile("" ::"v"(y));
 #else
-      if (!TAIL || t0 + s < L) stf(goc + (int64_t)(t0 + s) * a.out_ls, y);  // one 4-byte store per lane and step
+      // one 4- (2-) byte store per lane and step; rows past L fall outside the range
+      if constexpr (ES == 4)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(y), ro, (uint32_t)(lane * 4), (t0 + s) * (int)a.out_ls * 4, 0);
+      else
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(y), ro, (uint32_t)(lane * 2), (t0 + s) * (int)a.out_ls * 2, 0);
 #endif
     };
 #pragma unroll
@@ -1958,7 +1994,10 @@ static bool c1_ok(const MttsScanFwdArgs* a) {
     return ((uintptr_t)p % (al * eb)) == 0 && bs % al == 0 && ls % al == 0;
   };
   if (!ok(a->Bm, a->B_bs, a->B_ls) || !ok(a->Cm, a->C_bs, a->C_ls)) return false;
-  if (path == 1 || path == 4) return true;
+  // buffer-addressed rows: a batch row's byte span (and the last tile's row origin) below 2 GiB
+  auto fits = [&](int64_t ls) { return (int64_t)(a->seqlen + 32) * ls * es < (1ll << 31); };
+  if (!fits(a->u_ls) || !fits(a->delta_ls) || !fits(a->out_ls) || (a->z && !fits(a->z_ls))) return false;
+  if (path == 1) return true;
   return (int64_t)a->batch * a->dim >= 65536;
 }
 template <typename Tio, typename Tbc, bool SP, bool HZ>
@@ -1967,289 +2006,10 @@ static void launch_c1(const MttsScanFwdArgs* a, hipStream_t st) {
                      *a);
 }
 
-// ------------------------------------------------------------- forward, a wave PAIR per channel group (round 4)
-// scan_fwd_c1_kernel has exactly one wave per SIMD at the north-star shape
-// (B*D/64 = 1024 waves), and a lone wave issues a VALU instruction every ~4
-// cycles where two interleaved waves issue one every ~2 (MI355X_MICROARCH.md
-// "vector-instruction ISSUE cost"; tools/ubench/valu_costs.hip).  Here the 64
-// channels of a group are shared by two waves on one SIMD: wave hf owns
-// states 8hf..8hf+7 of every channel (8 exps and 16 packed mul/fma per
-// channel-step), both form the per-channel dt' and dt'u from the same LDS
-// tiles (wave 0 DMAs u, wave 1 delta), wave 1 hands its partial C.h' of every
-// step to wave 0 through LDS, and wave 0 adds D log2(e) u, applies the SiLU
-// gate (z loaded per lane straight into registers a tile ahead) and stores y.
-// Block = 4 pairs, 512 threads, two waves per SIMD; ONE barrier per 16-step
-// tile publishes the next tile's DMA (each wave drained its own) and the
-// partials.  VMEM order per tile, wave 0: [y stores of tile it-1] [z of it+1]
-// [checkpoint of it] [B/C of it+1] [DMA of it+NB-1]; wave 1: [checkpoint]
-// [B/C] [DMA]: waiting for vmcnt(DPT) retires everything but the newest DMA.
-// Log2-domain state and softplus as scan_fwd_c1_kernel.
-template <typename Tio, typename Tbc, bool SP, bool HZ>
-__global__ __launch_bounds__(512, 1) void scan_fwd_c1p_kernel(const MttsScanFwdArgs a) {
-  constexpr int ES = (int)sizeof(Tio);
-  constexpr int EPC = 16 / ES;            // elements per 16-byte chunk
-  constexpr int CPR = 64 / EPC;           // chunks per 64-channel row
-  constexpr int RPD = 64 / CPR;           // rows per DMA instruction: 4 fp32, 8 bf16
-  constexpr int TT = 16;                  // steps per tile (= kSub: one checkpoint per tile)
-  constexpr int DPT = TT / RPD;           // DMA instructions per tile and wave
-  constexpr int NB = ES == 4 ? 3 : 4;     // tile ring (LDS per block: 136 / 104 KiB)
-  constexpr int IMG = TT * 64;
-  constexpr int NH = kN / 2;              // states per wave
-  constexpr int NP = NH / 2;              // f2 pairs per wave
-  constexpr int BCV = TT * 2 * NH / 64;   // B/C values staged per lane and tile: 4
-  constexpr int BCW = BCV * (int)sizeof(Tbc) / 4;   // dwords per lane: 4 fp32, 2 bf16
-  static_assert(TT == kSub && BCV == 4, "tile geometry");
-  __shared__ __attribute__((aligned(16))) Tio sX[4][NB][2][IMG];      // [pair][buf][u | delta]
-  __shared__ __attribute__((aligned(16))) float sBC[8][TT * 2 * NH];  // per wave: [step][B 8 | C 8]
-  __shared__ __attribute__((aligned(16))) float sY[4][2][IMG];        // [pair][tile parity]: wave 1's C.h'
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int pr = wave & 3;                // waves pr and pr + 4 share SIMD pr
-  const int hf = wave >> 2;
-  int bx = blockIdx.x, b = blockIdx.y;
-  if ((gridDim.y & 7) == 0) {             // a batch row's blocks on one XCD (as scan_fwd_c1_kernel)
-    const int id = blockIdx.x + gridDim.x * blockIdx.y, j = id >> 3;
-    b = (id & 7) * (gridDim.y >> 3) + j / gridDim.x;
-    bx = j % gridDim.x;
-  }
-  const int c0 = (bx * 4 + pr) * 64;      // dim % 256 == 0 (host): every wave has a group
-  const int c = c0 + lane;
-  const int L = a.seqlen;
-  const int nt = (L + TT - 1) / TT;
-
-  const int drow = lane / CPR, dcol = (lane % CPR) * EPC;
-  const Tio* __restrict__ gx = hf == 0 ? (const Tio*)a.u + (int64_t)b * a.u_bs + c0 + dcol
-                                       : (const Tio*)a.delta + (int64_t)b * a.delta_bs + c0 + dcol;
-  const int64_t x_ls = hf == 0 ? a.u_ls : a.delta_ls;
-  // staged B/C: lane -> step bs, 4 values of B (q < 2) or C (q >= 2) of this wave's states
-  const int bs = lane >> 2, q4 = lane & 3;
-  const int soff = hf * NH + (q4 & 1) * 4;
-  const Tbc* __restrict__ gbc = q4 < 2 ? (const Tbc*)a.Bm + (int64_t)b * a.B_bs + soff
-                                       : (const Tbc*)a.Cm + (int64_t)b * a.C_bs + soff;
-  const int64_t bc_ls = q4 < 2 ? a.B_ls : a.C_ls;
-  const int bcol = (q4 < 2 ? 0 : NH) + (q4 & 1) * 4;
-
-  f2 A2[NP], h[NP];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int64_t ai = (int64_t)c * kN + hf * NH + 2 * p;
-    A2[p] = f2{ld_A(a, ai), ld_A(a, ai + 1)};
-    const int64_t o = ((int64_t)b * a.dim + c) * kN + hf * NH + 2 * p;
-    h[p] = a.h0 ? f2{a.h0[o] * kLog2e, a.h0[o + 1] * kLog2e} : f2{0.f, 0.f};
-  }
-  const float Dc2 = a.D ? a.D[c] * kLog2e : 0.f;
-  const float bias2 = a.delta_bias ? a.delta_bias[c] * kLog2e : 0.f;
-  const int nck = a.ckpt ? (L + kSub - 1) / kSub : 0;
-  float* __restrict__ ck = nck ? a.ckpt + (int64_t)b * nck * a.dim * kN + (int64_t)c * kN + hf * NH : nullptr;
-  auto store_h = [&](float* dst) __attribute__((always_inline)) {
-#pragma unroll
-    for (int q = 0; q < NP / 2; ++q) {
-      const f2 lo = h[2 * q] * kLn2, hi = h[2 * q + 1] * kLn2;
-      *reinterpret_cast<f4*>(dst + 4 * q) = f4{lo[0], lo[1], hi[0], hi[1]};
-    }
-  };
-
-  uint32_t stg[BCW];
-  auto load_bc = [&](int it) __attribute__((always_inline)) {
-    const Tbc* p = gbc + (int64_t)min(it * TT + bs, L - 1) * bc_ls;
-    ldg_asm<BCW>(stg, p);
-  };
-  auto stage_bc = [&]() __attribute__((always_inline)) {
-    float v[4];
-    if constexpr (sizeof(Tbc) == 4) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = __uint_as_float(stg[q]);
-    } else {
-      unpack_bf2(stg[0], v[0], v[1]);
-      unpack_bf2(stg[1], v[2], v[3]);
-    }
-    *reinterpret_cast<f4*>(&sBC[wave][bs * 2 * NH + bcol]) = f4{v[0], v[1], v[2], v[3]};
-  };
-  auto dma_tile = [&](int it, int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < DPT; ++k) {
-      const int t = min(it * TT + k * RPD + drow, L - 1);   // rows past L: any valid row (never used)
-      dma16(gx + (int64_t)t * x_ls, &sX[pr][buf][hf][k * RPD * 64]);
-    }
-  };
-  auto barrier = []() __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes done
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  // one body per wave role (wave-uniform branch, both paths reach the same barriers)
-  auto run = [&](auto role) __attribute__((always_inline)) {
-    constexpr int HF = decltype(role)::value;
-    constexpr bool ZL = HF == 0 && HZ;    // wave 0 loads z
-    uint32_t zn[TT][1];                   // wave 0: raw z of the next tile (in flight) / this tile
-    float pys[TT], gts[TT];               // wave 0: C.h' + D log2(e) u and SiLU gate of a tile's steps
-    const Tio* __restrict__ gz = ZL ? (const Tio*)a.z + (int64_t)b * a.z_bs + c : nullptr;
-    Tio* __restrict__ goc = (Tio*)a.out + (int64_t)b * a.out_bs + c;
-    auto load_z = [&](int it) __attribute__((always_inline)) {
-      if constexpr (ZL) {
-#pragma unroll
-        for (int s = 0; s < TT; ++s) ldg_asm<1, ES == 2>(zn[s], gz + (int64_t)min(it * TT + s, L - 1) * a.z_ls);
-      }
-    };
-    auto redefine = [&]() __attribute__((always_inline)) {   // nothing that reads them moves above a wait
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-      for (int q = 0; q < BCW; ++q) asm volatile("" : "+v"(stg[q]));
-      if constexpr (ZL) {
-#pragma unroll
-        for (int s = 0; s < TT; ++s) asm volatile("" : "+v"(zn[s][0]));
-      }
-#endif
-    };
-    auto finish_y = [&](int it) __attribute__((always_inline)) {   // wave 0, after the barrier closing tile it
-      if constexpr (HF == 0) {
-        const int t0 = it * TT;
-        const float* yb = &sY[pr][it & 1][lane];
-#pragma unroll
-        for (int s = 0; s < TT; ++s)
-          if (t0 + s < L) stf(goc + (int64_t)(t0 + s) * a.out_ls, (pys[s] + yb[s * 64]) * gts[s]);
-      }
-    };
-    auto gates = [&]() __attribute__((always_inline)) {   // wave 0: ln2 silu(z) of the tile z holds
-      if constexpr (HF == 0) {
-#pragma unroll
-        for (int s = 0; s < TT; ++s) {
-          if constexpr (HZ) {
-            const float zv = ES == 4 ? __uint_as_float(zn[s][0]) : __uint_as_float(zn[s][0] << 16);
-            gts[s] = zv * fast_rcp(fmaf(__builtin_amdgcn_exp2f(-zv * kLog2e), kLog2e, kLog2e));
-          } else {
-            gts[s] = kLn2;
-          }
-        }
-      }
-    };
-    auto compute_tile = [&](auto tail, int it, int buf) __attribute__((always_inline)) {
-      constexpr bool TAIL = decltype(tail)::value;
-      const int t0 = it * TT;
-      f4 bB[2][NH / 4], bC[2][NH / 4];
-      auto lds_row = [&](int s, int half, f4 (&o)[NH / 4]) __attribute__((always_inline)) {
-        const f4* p = reinterpret_cast<const f4*>(&sBC[wave][s * 2 * NH + half * NH]);
-#pragma unroll
-        for (int q = 0; q < NH / 4; ++q) o[q] = p[q];
-      };
-      auto Bv = [&](int s, int p) __attribute__((always_inline)) -> f2 {
-        const f4& q = bB[s & 1][p / 2];
-        return (p & 1) ? f2{q[2], q[3]} : f2{q[0], q[1]};
-      };
-      auto Cv = [&](int s, int p) __attribute__((always_inline)) -> f2 {
-        const f4& q = bC[s & 1][p / 2];
-        return (p & 1) ? f2{q[2], q[3]} : f2{q[0], q[1]};
-      };
-      lds_row(0, 0, bB[0]);
-      float dts[TT], dtus[TT];
-#pragma unroll
-      for (int s = 0; s < TT; ++s) {
-        const int e = s * 64 + lane;
-        const float xl = fmaf(cvt_raw((raw_t<Tio>)sX[pr][buf][1][e]), kLog2e, bias2);
-        const float dt = SP ? softplus_l2(xl) : xl;
-        const float uv = cvt_raw((raw_t<Tio>)sX[pr][buf][0][e]);
-        const bool tv = !TAIL || t0 + s < L;
-        dts[s] = tv ? dt : 0.f;
-        dtus[s] = tv ? dt * uv : 0.f;
-        if constexpr (HF == 0) pys[s] = Dc2 * uv;   // y partial starts at D log2(e) u
-      }
-      f2 ex[2][NP];
-      auto exps = [&](int s, f2 (&o)[NP]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          const f2 x = f2{dts[s], dts[s]} * A2[p];
-          o[p] = f2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
-        }
-      };
-      exps(0, ex[0]);
-      float* ysl = &sY[pr][it & 1][lane];
-      auto yout = [&](int s) __attribute__((always_inline)) {
-        f2 ya = {0.f, 0.f}, yb = {0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < NP / 2; ++q) {
-          ya = __builtin_elementwise_fma(Cv(s, 2 * q), h[2 * q], ya);
-          yb = __builtin_elementwise_fma(Cv(s, 2 * q + 1), h[2 * q + 1], yb);
-        }
-        const f2 y2 = ya + yb;
-        if constexpr (HF == 0) pys[s] += y2[0] + y2[1];
-        else ysl[s * 64] = y2[0] + y2[1];
-      };
-#pragma unroll
-      for (int s = 0; s < TT; ++s) {
-        if (s + 1 < TT) lds_row(s + 1, 0, bB[(s + 1) & 1]);
-        lds_row(s, 1, bC[s & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (s + 1 < TT) exps(s + 1, ex[(s + 1) & 1]);
-        if (s >= 1) yout(s - 1);
-        const f2 dtu2 = f2{dtus[s], dtus[s]};
-#pragma unroll
-        for (int p = 0; p < NP; ++p) h[p] = __builtin_elementwise_fma(ex[s & 1][p], h[p], dtu2 * Bv(s, p));
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      yout(TT - 1);
-    };
-
-    // prologue: B/C of tile 0, the DMA of tiles 0..NB-2 and z of tile 0, all complete before tile 0
-    load_bc(0);
-#pragma unroll
-    for (int k = 0; k < NB - 1; ++k)
-      if (k < nt) dma_tile(k, k);
-    load_z(0);
-    wait_vm<0>(stg);
-    redefine();
-    stage_bc();
-    barrier();
-    for (int it = 0; it < nt; ++it) {
-      const int buf = it % NB;
-      const int prev = (it + NB - 1) % NB;
-      const bool more = it + 1 < nt;
-      const bool ahead = it + NB - 1 < nt;
-      if (it > 0) finish_y(it - 1);
-      gates();                          // z of tile it (landed by the last wait), before its reload
-      if (more) load_z(it + 1);
-      if (nck && it * TT < L) store_h(ck + (int64_t)it * a.dim * kN);
-      if (more) load_bc(it + 1);
-      if (ahead) dma_tile(it + NB - 1, prev);
-      if ((it + 1) * TT <= L) compute_tile(FalseT{}, it, buf);
-      else compute_tile(TrueT{}, it, buf);
-      if (more) {
-        if (ahead) wait_vmn<DPT>(stg);
-        else wait_vm<0>(stg);
-        redefine();
-        stage_bc();
-      }
-      barrier();
-    }
-    finish_y(nt - 1);
-  };
-  if (hf == 0) run(std::integral_constant<int, 0>{});
-  else run(std::integral_constant<int, 1>{});
-  if (a.last_state) store_h(a.last_state + ((int64_t)b * a.dim + c) * kN + hf * NH);
-}
-
-// the paired kernel applies where the one-lane-per-channel kernel does and
-// the block's 4 groups of 64 channels are all present
-static bool c1p_ok(const MttsScanFwdArgs* a) {
-  const int path = override_of(MTTS_OVR_SCAN_PATH);
-  if (path != 4 || a->dim % 256) return false;   // opt-in while it is measured (round 4)
-  return c1_ok(a);
-}
-template <typename Tio, typename Tbc, bool SP, bool HZ>
-static void launch_c1p(const MttsScanFwdArgs* a, hipStream_t st) {
-  hipLaunchKernelGGL((scan_fwd_c1p_kernel<Tio, Tbc, SP, HZ>), dim3(a->dim / 256, a->batch), dim3(512), 0, st, *a);
-}
-
 template <int P, typename Tio, typename Tbc, bool SP>
 static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream_t st) {
   const int nbx = (a->dim + kBlock / P - 1) / (kBlock / P);
   float* seg = (float*)a->workspace;
-  if (c1p_ok(a)) {
-    if (a->z) launch_c1p<Tio, Tbc, SP, true>(a, st);
-    else launch_c1p<Tio, Tbc, SP, false>(a, st);
-    return;
-  }
   if (c1_ok(a)) {
     if (a->z) launch_c1<Tio, Tbc, SP, true>(a, st);
     else launch_c1<Tio, Tbc, SP, false>(a, st);

@@ -33,20 +33,17 @@ def g32(a):
     return torch.from_numpy(np.asarray(a)).to(DEV, torch.float32)
 
 
-@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2", "4c1", "4c1p"])
+@pytest.fixture(params=["2", "4", "4:s3", "4n", "2n:s2", "4c1"])
 def scan_p(request):
     """P (lanes per channel) and, with ':sK', a forced split of L into K
     segments for both the forward and the backward (two-pass path); 'n'
     forces the narrow (per-lane element) forward kernel instead of the
     16-byte-chunk LDS-DMA one; 'c1' the one-lane-per-channel forward
-    (scan_fwd_c1_kernel) below its B*D threshold wherever D % 64 == 0, 'c1p'
-    its wave-pair form wherever D % 256 == 0 (else c1).
+    (scan_fwd_c1_kernel) below its B*D threshold wherever D % 64 == 0.
     Forced through the library's kernel-path overrides (mtts_set_override)."""
     from mtts import _lib as L
     p, _, segs = request.param.partition(":s")
     path = None
-    if p.endswith("c1p"):
-        p, path = p[:-3], L.SCAN_C1P
     if p.endswith("c1"):
         p, path = p[:-2], L.SCAN_C1
     if p.endswith("n"):
@@ -145,22 +142,19 @@ def _with_path(path, fn):
                                    (1, 50, 512), (1, 1, 256), (3, 1003, 512), (1, 17, 768)])
 @pytest.mark.parametrize("io,bc", [("f32", "f32"), ("f32", "bf16"), ("bf16", "bf16"), ("bf16", "f32")])
 @pytest.mark.parametrize("with_z,strided", [(True, False), (False, True)])
-@pytest.mark.parametrize("kernel", ["c1", "c1p"])
-def test_scan_c1_kernel_vs_oracle(B, L, D, io, bc, with_z, strided, kernel):
-    """scan_fwd_c1_kernel / scan_fwd_c1p_kernel (the wave-pair form, D % 256
-    == 0) forced, against the float64 oracle on the same (already rounded)
-    inputs: outputs, last state and the backward's checkpoints (h every 16
-    steps, compared with the P=4 LDS-DMA kernel's); h0, ragged L (tail tiles),
-    D % 256 != 0 (idle waves, c1), strided B/C."""
+def test_scan_c1_kernel_vs_oracle(B, L, D, io, bc, with_z, strided):
+    """scan_fwd_c1_kernel (forced) against the float64 oracle on the same
+    (already rounded) inputs: outputs, last state and the backward's
+    checkpoints (h every 16 steps, compared with the P=4 LDS-DMA kernel's);
+    h0, ragged L (tail tiles), D % 256 != 0 (idle waves), strided B/C."""
     from mtts import _lib, ops
-    if kernel == "c1p" and D % 256:
-        pytest.skip("the wave-pair kernel takes whole 256-channel blocks")
+    kernel = "c1"
     dt = {"f32": torch.float32, "bf16": torch.bfloat16}
     u, dl, A, Bm, Cm, Dp, z, bias, h0 = _scan_inputs(B, L, D, dt[io], dt[bc], B * L + D, strided)
     z = z if with_z else None
     run = lambda: ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, h0=h0, want_last=True,  # noqa: E731
                                want_ckpt=True)
-    out, last, ck = _with_path(_lib.SCAN_C1 if kernel == "c1" else _lib.SCAN_C1P, run)
+    out, last, ck = _with_path(_lib.SCAN_C1, run)
     out_w, last_w, ck_w = _with_path(2, run)   # the P-lane LDS-DMA kernel
     ref, rlast = R.selective_scan_ref(*(t.double().cpu() for t in (u.transpose(1, 2), dl.transpose(1, 2), A,
                                                                   Bm.transpose(1, 2), Cm.transpose(1, 2), Dp)),
@@ -185,11 +179,8 @@ def test_scan_c1_north_star_width():
     run = lambda: ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, want_last=True)  # noqa: E731
     out, last, _ = _with_path(None, run)
     out_w, last_w, _ = _with_path(2, run)
-    out_p, last_p, _ = _with_path(4, run)      # wave-pair kernel
     close(out, out_w, rtol=1e-5, name="c1 vs w2 out")
     close(last, last_w, rtol=1e-5, name="c1 vs w2 last")
-    close(out_p, out_w, rtol=1e-5, name="c1p vs w2 out")
-    close(last_p, last_w, rtol=1e-5, name="c1p vs w2 last")
     for b, c in ((0, 0), (31, 1984)):
         sl = lambda t: t[b:b + 1, :, c:c + 64].double().cpu().transpose(1, 2)  # noqa: E731
         ref = R.selective_scan_ref(sl(u), sl(dl), A[c:c + 64].double().cpu(),

@@ -1,6 +1,6 @@
 """Run selective_scan_fwd at the north-star shape a few times (for rocprofv3).
 python tools/scan_once.py [fp32|bf16]; SCAN_PATH=<n> forces a forward kernel
-(mtts_set_override MTTS_OVR_SCAN_PATH: 1 c1, 2 w2, 4 c1p)."""
+(mtts_set_override MTTS_OVR_SCAN_PATH: 1 c1, 2 w2)."""
 import contextlib
 import os
 import sys
