@@ -1222,31 +1222,42 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(BwdParams p) {
     for (int dt = 0; dt < ND; ++dt) oT[u][dt] = kimg<HD>(4 * h + qq + 8 * u, 4 * dt + 2 * g + (pp >> 1)) + 4 * (pp & 1);
 
   // ---- slice staging: loads issued unconditionally (clamped), consumed in put()
+  // slices as buffer loads (round 4): lane-constant row / column offsets,
+  // the slice origin in the scalar offset, rows at or past qend read zeros
   f32x4 pq[NPF], pg[NPF];
   float pl = 0.f, pd = 0.f;
   int ps0 = qbeg;
+  const __amdgpu_buffer_rsrc_t rq = brsrc(qb, (uint32_t)(((int64_t)(qend - 1) * f.q_ls + HD) * 2));
+  const __amdgpu_buffer_rsrc_t rg = brsrc(gb, (uint32_t)(((int64_t)(qend - 1) * a.do_ls + HD) * 2));
+  const __amdgpu_buffer_rsrc_t rl = brsrc(lbuf, (uint32_t)qend * 4);
+  const __amdgpu_buffer_rsrc_t rd = brsrc(dbuf, (uint32_t)qend * 4);
+  uint32_t oq_[NPF], og_[NPF];
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int idx = tid + 256 * i;
+    const int row = idx / (HD / 8), cc = (idx % (HD / 8)) * 8;
+    oq_[i] = (uint32_t)((row * f.q_ls + cc) * 2);
+    og_[i] = (uint32_t)((row * a.do_ls + cc) * 2);
+  }
   auto fetch = [&](int q0) __attribute__((always_inline)) {
     ps0 = q0;
+    const int sq = (int)(q0 * f.q_ls * 2), sg = (int)(q0 * a.do_ls * 2);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      const int idx = tid + 256 * i;
-      const int row = idx / (HD / 8), cc = (idx % (HD / 8)) * 8;
-      const int qc_ = min(q0 + row, qend - 1);
-      pq[i] = *(const f32x4*)(qb + (int64_t)qc_ * f.q_ls + cc);
-      pg[i] = *(const f32x4*)(gb + (int64_t)qc_ * a.do_ls + cc);
+      pq[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, oq_[i], sq, 0));
+      pg[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, og_[i], sg, 0));
     }
-    const int ql = min(q0 + (tid & (QS - 1)), qend - 1);
-    pl = lbuf[ql];
-    pd = dbuf[ql];
+    const uint32_t ol = (uint32_t)(tid & (QS - 1)) * 4;
+    pl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, ol, q0 * 4, 0));
+    pd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, ol, q0 * 4, 0));
   };
   auto put = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx / (HD / 8), ch = idx % (HD / 8);
-      const bool in = ps0 + row < qend;
-      *(f32x4*)(sQ[buf] + kimg<HD>(row, ch)) = in ? pq[i] : f32x4{};
-      *(f32x4*)(sG[buf] + kimg<HD>(row, ch)) = in ? pg[i] : f32x4{};
+      *(f32x4*)(sQ[buf] + kimg<HD>(row, ch)) = pq[i];
+      *(f32x4*)(sG[buf] + kimg<HD>(row, ch)) = pg[i];
     }
     if (tid < QS) {
       const bool in = ps0 + tid < qend;
@@ -1652,10 +1663,14 @@ template <typename T, int HD>
 void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
   constexpr int NT = BwdCfg<T, HD>::NW * 64;
   const MttsAttnFwdArgs& f = p.a.f;
+  // the dQ / dK-dV kernels address K / V / Q / dO rows through buffer
+  // descriptors: one K / V row stride, 31-bit byte spans
+  const bool span_ok = f.k_ls == f.v_ls && (int64_t)(f.kv_len + 64) * f.k_ls * 2 < (1ll << 31) &&
+                       (int64_t)(f.q_len + 64) * std::max(f.q_ls, p.a.do_ls) * 2 < (1ll << 31);
   if (split) {
     constexpr int KG = BwdCfg<T, HD>::KG;
     if constexpr (std::is_same<T, bf16_t>::value && (HD == 64 || HD == 128)) {
-      if (mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1)
+      if (span_ok && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1)
         attn_bwd_dq_kernel<HD><<<dim3((f.q_len + 127) / 128, f.heads, f.batch), 256, 0, st>>>(p);
       else
         attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
@@ -1663,7 +1678,7 @@ void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
       attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
     }
     if constexpr (std::is_same<T, bf16_t>::value && HD == 64) {
-      if (mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1) {
+      if (span_ok && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1) {
         attn_bwd_kv_kernel<HD><<<dim3((f.kv_len + 127) / 128 * p.nchunk, f.heads, f.batch), 256, 0, st>>>(p);
         return;
       }
