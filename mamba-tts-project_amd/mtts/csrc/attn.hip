@@ -103,8 +103,8 @@ __device__ __forceinline__ float lane_group_sum(float v) {
   if constexpr (NL >= 4) v += mtts::dpp<mtts::kQuadXor2>(v);
   if constexpr (NL >= 8) v += mtts::xor4(v, lane);
   if constexpr (NL >= 16) v += mtts::xor8(v);
-  if constexpr (NL >= 32) v += mtts::xor16(v, lane);
-  if constexpr (NL >= 64) v += mtts::xor32(v, lane);
+  if constexpr (NL >= 32) v = mtts::sum_xor16(v);
+  if constexpr (NL >= 64) v = mtts::sum_xor32(v);
   return v;
 }
 
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(MttsAttnFwdArgs a) {
         S[i] = ok ? S[i] * c : -INFINITY;
         tmax = fmaxf(tmax, S[i]);
       }
-      tmax = fmaxf(tmax, mtts::xor32(tmax, lane));
+      tmax = mtts::max_xor32(tmax);
       const float mn = fmaxf(m, tmax);
       const float ms = mn == -INFINITY ? 0.f : mn;
       const float alpha = exp2_raw(m - ms);
@@ -298,7 +298,7 @@ __device__ __forceinline__ void softmax_step(f32x16& S, uint32_t mask_word, int 
   float tmax = S[0];
 #pragma unroll
   for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, S[i]);
-  tmax = fmaxf(tmax, mtts::xor32(tmax, lane)) * c;
+  tmax = mtts::max_xor32(tmax) * c;
   if (!__all(tmax <= m + kDeferMax)) {
     const float mn = fmaxf(m, tmax);
     const float alpha = exp2_raw(m - (mn == -INFINITY ? 0.f : mn));
@@ -1514,8 +1514,8 @@ __device__ __forceinline__ float groups_max(float v, int lane) {
   if constexpr (G <= 2) v = fmaxf(v, mtts::dpp<mtts::kQuadXor2>(v));
   if constexpr (G <= 4) v = fmaxf(v, mtts::xor4(v, lane));
   if constexpr (G <= 8) v = fmaxf(v, mtts::xor8(v));
-  v = fmaxf(v, mtts::xor16(v, lane));
-  return fmaxf(v, mtts::xor32(v, lane));
+  v = mtts::max_xor16(v);
+  return mtts::max_xor32(v);
 }
 
 template <typename T, int HD, int U>

@@ -134,6 +134,16 @@ __device__ __forceinline__ float sum_xor32(float v) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// max(v, v[lane ^ 16]) / max(v, v[lane ^ 32]) without selects (both swap
+// outputs are {own, partner})
+__device__ __forceinline__ float max_xor16(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor32(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 // lane ^ 4 within each 16-lane row
 __device__ __forceinline__ float xor4(float v, int lane) {
   float a = dpp<kRowRor4>(v);   // from lane-4

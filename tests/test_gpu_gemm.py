@@ -159,9 +159,8 @@ def gemm_mode(request):
 
 @pytest.mark.parametrize("m,n,k", [(16384, 4096, 1024), (16484, 4104, 1024), (4096, 2048, 128), (8192, 1024, 2048)])
 def test_nt_every_kernel_many_tiles(gemm_mode, m, n, k):
-    """More work items than CUs (the persistent kernel runs several tiles per
-    workgroup, its K-tile stream crossing tile boundaries), ragged edges in
-    both dimensions, K of 2 K-tiles; plain, bias + GELU and GELU-backward."""
+    """More work items than CUs (several rounds of workgroups), ragged edges
+    in both dimensions, K of 2 K-tiles; plain, bias + GELU and GELU-backward."""
     torch.manual_seed(m + n + k)
     a, b = rnd(m, k), rnd(n, k)
     ref = a.float() @ b.float().t()

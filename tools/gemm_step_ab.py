@@ -42,6 +42,16 @@ def timeit(n=10):
     return (time.perf_counter() - t0) / n * 1e3
 
 
+if len(sys.argv) > 3 and sys.argv[1] == "ovr":   # gemm_step_ab.py ovr <override key> <value>: value vs automatic
+    from mtts import _lib
+    key, val = sys.argv[2], int(sys.argv[3])
+    res = {f"{key}={val}": [], "auto": []}
+    for _ in range(3):
+        for kind in res:
+            with _lib.override(**{key: val if kind != "auto" else None}):
+                res[kind].append(timeit())
+    print({k: [round(x, 2) for x in v] for k, v in res.items()}, flush=True)
+    sys.exit(0)
 if len(sys.argv) > 1:          # profile one mode: gemm_step_ab.py hip|blaslt [steps]
     G.ENABLED = sys.argv[1] == "hip"
     print(sys.argv[1], round(timeit(int(sys.argv[2]) if len(sys.argv) > 2 else 5), 2), flush=True)
