@@ -217,11 +217,11 @@ def scan_roofline(dtype, B=32, L=8192, D=2048, iters=20, rounds=5, barrier=False
 
 def pmc_traffic(dtype_key):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3
-    PMC passes (profiles/r03_scan_pmc_summary.json, made by tools/gpu/evidence_r03.sh
-    + tools/pmc_summary.py r03 gpurun_out/ev3/pmc):
+    PMC passes (profiles/r04_scan_pmc_summary.json, made by tools/gpu/evidence_r04.sh
+    + tools/pmc_summary.py r04 gpurun_out/ev4/pmc):
     2 x FETCH_SIZE (gfx950 counts half of wide coalesced streaming reads,
     MI355X_MICROARCH.md HBM section) + WRITE_SIZE, both KB x 1024."""
-    path = os.path.join(ROOT, "profiles", "r03_scan_pmc_summary.json")
+    path = os.path.join(ROOT, "profiles", "r04_scan_pmc_summary.json")
     try:
         with open(path) as f:
             return json.load(f)[dtype_key]["traffic_bytes"]
@@ -580,7 +580,7 @@ def main():
                                      "reference's precision, f32 math)",
                            "bound": "hbm", "achieved": fbw / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                            "frac": fbw / HBM_PEAK, "traffic": pmc_traffic("fp32"), "ms": fms, "algorithmic_bytes": fb,
-                           "traffic_source": "profiles/r03_scan_pmc_summary.json (2*FETCH_SIZE+WRITE_SIZE)"}
+                           "traffic_source": "profiles/r04_scan_pmc_summary.json (2*FETCH_SIZE+WRITE_SIZE)"}
         if roof[1] is not None:
             (sms, sb, sbw) = roof[1]
             log(f"[bench] scan bf16 north-star {sms:.3f} ms {sbw / 1e9:.0f} GB/s")

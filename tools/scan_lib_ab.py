@@ -47,6 +47,8 @@ def timed(fn, iters=20, rounds=5):
 out = {"pkg": os.path.relpath(PKG, ROOT)}
 from mtts import _lib  # noqa: E402
 paths = {"": None}
+if hasattr(_lib, "SCAN_C1P"):   # this tree: also the wave-pair forward
+    paths["_c1p"] = _lib.SCAN_C1P
 for name, dt in (("ns_fp32", torch.float32), ("ns_bf16", torch.bfloat16)):
     a = args(32, 8192, 2048, dt, dt)
     o = torch.empty_like(a[0])
