@@ -1049,6 +1049,11 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
   constexpr int PIT = wide_pitch_dw(kPB, ROWB / 4, (64 / kPB) * ES / 4) * 4 / ES;
   constexpr int NCH = 3 * TT * CPR / kBlock;
   __shared__ __attribute__((aligned(16))) Tio sX[WIDE ? 2 : 1][3][WIDE ? TT * PIT : 1];
+  // per-wave [dt | dy][channel][step] of the tile (pitch 36 floats: distinct
+  // bank groups for the 16 channels' 16-byte reads): one ds_read_b128 per
+  // group instead of eight DPP broadcasts (as scan_bwd_kernel)
+  constexpr int kBrP = TT + 4;
+  __shared__ __attribute__((aligned(16))) float sBr[kWaves][2][16 * kBrP];
   const int cl = threadIdx.x / kPB;
   const MttsScanFwdArgs& f = a.f;
   const int j = threadIdx.x % kPB;
@@ -1157,8 +1162,10 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
       if constexpr (WIDE) load_w(t0 - TT);
       else load(t0 - TT, nx, ng, nz);
     }
-    static_for<G>([&](auto gc) {
-      constexpr int g = G - 1 - decltype(gc)::value;
+    // the tile's per-step dt and dy (this lane's steps) into the wave's table
+    float* const br = &sBr[threadIdx.x >> 6][0][((threadIdx.x & 63) >> 2) * kBrP];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
       const bool tv = t0 + g * kPB + j < t_end;
       R rx, rg, rz;
       if constexpr (WIDE) {
@@ -1177,11 +1184,16 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
       float dy = tv ? cvt_raw(rg) : 0.f;
       if (has_z) dy *= silu_f(cvt_raw(rz));
       S += dt;
+      br[g * kPB + j] = dt;
+      br[16 * kBrP + g * kPB + j] = dy;
+    }
+    static_for<G>([&](auto gc) {
+      constexpr int g = G - 1 - decltype(gc)::value;
+      const f4 d4 = *reinterpret_cast<const f4*>(br + g * kPB);
+      const f4 y4 = *reinterpret_cast<const f4*>(br + 16 * kBrP + g * kPB);
 #pragma unroll
       for (int s = kPB - 1; s >= 0; --s) {
-        float dts = s == 0 ? bcast4<0>(dt) : s == 1 ? bcast4<1>(dt) : s == 2 ? bcast4<2>(dt) : bcast4<3>(dt);
-        float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
-        asm volatile("" : "+v"(dts), "+v"(dys));
+        const float dts = d4[s], dys = y4[s];
         const f4 Cq = *reinterpret_cast<const f4*>(&sC[buf][(g * kPB + s) * kN + j * kNSB]);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -1237,6 +1249,12 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   const int ck_end = min(nck, (kseg + 1) * seg_len / kSub);
 
   __shared__ __attribute__((aligned(16))) float red[kWaves][kSub * 2 * kN];  // per-wave dB/dC of one chunk
+  // per-wave [dt | dt*u][channel][step] of the chunk (row pitch 20 floats:
+  // the 16 channels' 16-byte reads hit distinct bank groups): a lane reads
+  // its channel's 4 steps of a group with one ds_read_b128 instead of four
+  // DPP broadcasts (round 4: DPP costs ~2.5 plain VALU ops)
+  constexpr int kBrP = 20;
+  __shared__ __attribute__((aligned(16))) float sBr[kWaves][2][16 * kBrP];
   __shared__ __attribute__((aligned(16))) float sBC[kSub * 2 * kN];          // B|C of the chunk, fp32
   // WIDE staging: [buffer][u, delta, z, dout][kSub rows of the block's channels]
   constexpr int ES = (int)sizeof(Tio);
@@ -1406,6 +1424,18 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       if constexpr (SP) d = softplus_f(d);
       dt[g] = (full || t_start + g * kPB + j < L) ? d : 0.f;
     }
+    // the chunk's dt and dt*u into this wave's broadcast table (the previous
+    // chunk's reads of it precede these writes in the wave's program order)
+    float* const br = &sBr[wave][0][(lane >> 2) * kBrP];
+#pragma unroll
+    for (int g = 0; g < kGB; ++g) {
+      br[g * kPB + j] = dt[g];
+      br[16 * kBrP + g * kPB + j] = dt[g] * uu[g];
+    }
+    auto bcast_dt = [&](int g, f4& d4, f4& u4) __attribute__((always_inline)) {
+      d4 = *reinterpret_cast<const f4*>(br + g * kPB);
+      u4 = *reinterpret_cast<const f4*>(br + 16 * kBrP + g * kPB);
+    };
     if constexpr (!WIDE) __syncthreads();
 
     // ---- replay the chunk forward: h history in registers (state pairs, packed f32)
@@ -1415,12 +1445,11 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       f2 h2[2] = {hs2[0], hs2[1]};
 #pragma unroll
       for (int g = 0; g < kGB; ++g) {
-        const float dtu = dt[g] * uu[g];
+        f4 d4, u4;
+        bcast_dt(g, d4, u4);
 #pragma unroll
         for (int s = 0; s < kPB; ++s) {
-          float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
-          float dtus = s == 0 ? bcast4<0>(dtu) : s == 1 ? bcast4<1>(dtu) : s == 2 ? bcast4<2>(dtu) : bcast4<3>(dtu);
-          asm volatile("" : "+v"(dts), "+v"(dtus));
+          const float dts = d4[s], dtus = u4[s];
           const f4 Bq = *reinterpret_cast<const f4*>(&sBC[(g * kPB + s) * 2 * kN + j * kNSB]);
 #pragma unroll
           for (int p = 0; p < 2; ++p) {
@@ -1452,15 +1481,15 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
         dzv = go[g] * y * sg * (1.f + zz[g] * (1.f - sg));
       }
       dD_acc = fmaf(dy, uu[g], dD_acc);
-      const float dtu_g = dt[g] * uu[g];
+      f4 d4, u4;
+      bcast_dt(g, d4, u4);
 
       float ddt_p[kPB], du_p[kPB];
 #pragma unroll
       for (int s = kPB - 1; s >= 0; --s) {
         float dys = s == 0 ? bcast4<0>(dy) : s == 1 ? bcast4<1>(dy) : s == 2 ? bcast4<2>(dy) : bcast4<3>(dy);
-        float dts = s == 0 ? bcast4<0>(dt[g]) : s == 1 ? bcast4<1>(dt[g]) : s == 2 ? bcast4<2>(dt[g]) : bcast4<3>(dt[g]);
-        float dtus = s == 0 ? bcast4<0>(dtu_g) : s == 1 ? bcast4<1>(dtu_g) : s == 2 ? bcast4<2>(dtu_g) : bcast4<3>(dtu_g);
-        asm volatile("" : "+v"(dys), "+v"(dts), "+v"(dtus));
+        asm volatile("" : "+v"(dys));
+        const float dts = d4[s], dtus = u4[s];
         const f2 dys2 = {dys, dys}, dts2 = {dts, dts}, dtus2 = {dtus, dtus};
         const int tl = g * kPB + s;
         const f4 Bq = *reinterpret_cast<const f4*>(&sBC[tl * 2 * kN + j * kNSB]);
