@@ -144,11 +144,13 @@ __device__ __forceinline__ float max_xor32(float v) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
-// lane ^ 4 within each 16-lane row
+constexpr int kQuadRev = 0x1B;         // [3,2,1,0]: lane ^ 3
+constexpr int kRowHalfMirror = 0x141;  // lane i <- lane 7 - i within 8: lane ^ 7
+// lane ^ 4 = (lane ^ 3) ^ 7: two DPP movs, no select (the second one fuses
+// into a following add / max as its DPP source)
 __device__ __forceinline__ float xor4(float v, int lane) {
-  float a = dpp<kRowRor4>(v);   // from lane-4
-  float b = dpp<kRowRor12>(v);  // from lane+4
-  return (lane & 4) ? a : b;
+  (void)lane;
+  return dpp<kRowHalfMirror>(dpp<kQuadRev>(v));
 }
 __device__ __forceinline__ float xor8(float v) { return dpp<kRowRor8>(v); }
 
