@@ -1440,6 +1440,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
 
     // ---- replay the chunk forward: h history in registers (state pairs, packed f32)
     f2 hh[kSub][2];
+    f2 ee[kSub];   // exp(dt A) of state pair 0 (pair 1 is recomputed in the reverse pass)
     const f2 hs2[2] = {f2{hs[0], hs[1]}, f2{hs[2], hs[3]}};
     {
       f2 h2[2] = {hs2[0], hs2[1]};
@@ -1458,6 +1459,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
             const f2 bv = p ? f2{Bq[2], Bq[3]} : f2{Bq[0], Bq[1]};
             h2[p] = __builtin_elementwise_fma(e, h2[p], f2{dtus, dtus} * bv);
             hh[g * kPB + s][p] = h2[p];
+            if (p == 0) ee[g * kPB + s] = e;
           }
         }
       }
@@ -1501,8 +1503,13 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
           const f2 cv = p ? f2{Cq[2], Cq[3]} : f2{Cq[0], Cq[1]};
           const f2 dh = __builtin_elementwise_fma(dys2, cv, carry2[p]);
           const f2 hp = tl > 0 ? hh[tl > 0 ? tl - 1 : 0][p] : hs2[p];
-          const f2 x = dts2 * A2v[p];
-          const f2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+          f2 e;
+          if (p == 0) {
+            e = ee[tl];
+          } else {
+            const f2 x = dts2 * A2v[p];
+            e = f2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+          }
           const f2 t1 = dh * e * hp;
           ddtA = __builtin_elementwise_fma(Anv[p], t1, ddtA);
           dus = __builtin_elementwise_fma(dh, bv, dus);
