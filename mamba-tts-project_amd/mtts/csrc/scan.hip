@@ -1266,6 +1266,11 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
   constexpr int NOUT = (3 * kSub * CPR + kBlock - 1) / kBlock;
   __shared__ __attribute__((aligned(16))) Tio sIn[WIDE ? 2 : 1][4][WIDE ? kSub * PIT : 1];
   const int cl = threadIdx.x / kPB;                // local channel
+  // exp(dt A) of state pair 1 from the replay, per wave and step (32 KiB per
+  // block; with fp32 WIDE staging it would cost the second block per CU, so
+  // that form recomputes it)
+  constexpr bool kEL = !WIDE || sizeof(Tio) == 2;
+  __shared__ __attribute__((aligned(16))) f2 sE[kEL ? kWaves : 1][kEL ? kSub : 1][64];
 
   // per-batch bases (uniform) + 32-bit per-lane offsets (lane j owns steps 4g+j)
   const Tio* __restrict__ u0 = (const Tio*)f.u + (int64_t)b * f.u_bs;
@@ -1460,6 +1465,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
             h2[p] = __builtin_elementwise_fma(e, h2[p], f2{dtus, dtus} * bv);
             hh[g * kPB + s][p] = h2[p];
             if (p == 0) ee[g * kPB + s] = e;
+            else if constexpr (kEL) sE[wave][g * kPB + s][lane] = e;
           }
         }
       }
@@ -1506,6 +1512,8 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
           f2 e;
           if (p == 0) {
             e = ee[tl];
+          } else if constexpr (kEL) {
+            e = sE[wave][tl][lane];
           } else {
             const f2 x = dts2 * A2v[p];
             e = f2{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
