@@ -1724,12 +1724,14 @@ static FwdPlan plan_fwd(int batch, int dim, int seqlen) {
   return pl;
 }
 
-// backward: P = 4 lanes per channel, 2 waves/SIMD resident (238 VGPRs)
+// backward: P = 4 lanes per channel, 2 waves/SIMD resident (<= 256 VGPRs);
+// 6 x 64k lanes: C2 runs K = 6 segments (0.496 vs 0.502 ms at K = 4,
+// tools/scan_lib_ab.py SWEEP, profiles/r04_scan_ab_bwd_ldsrs.jsonl)
 static FwdPlan plan_bwd(int batch, int dim, int seqlen) {
   FwdPlan pl;
   pl.P = kPB;
   const int64_t lanes = (int64_t)batch * dim * kPB;
-  int K = (int)((262144 + lanes - 1) / lanes);
+  int K = (int)((393216 + lanes - 1) / lanes);
   K = std::max(1, std::min(K, seqlen / 128));
   if (override_of(MTTS_OVR_SCAN_BWD_SEGS) >= 1) K = override_of(MTTS_OVR_SCAN_BWD_SEGS);
   int seg = (seqlen + K - 1) / K;

@@ -65,4 +65,12 @@ out["c2_fwd"] = timed(lambda: ops.scan_fwd(*a, True, want_ckpt=True))
 _, _, ck = ops.scan_fwd(*a, True, want_ckpt=True)
 dout = torch.randn_like(a[0])
 out["c2_bwd"] = timed(lambda: ops.scan_bwd(*a, True, None, ck, dout))
+# SWEEP="scan_bwd_segs=2,3,4;scan_segs=1,2": C2 fwd / bwd under each override value
+for item in filter(None, os.environ.get("SWEEP", "").split(";")):
+    key, vals = item.split("=")
+    for v in vals.split(","):
+        with _lib.override(**{key: int(v)}):
+            out[f"c2_fwd_{key}{v}"] = timed(lambda: ops.scan_fwd(*a, True, want_ckpt=True))
+            _, _, ck = ops.scan_fwd(*a, True, want_ckpt=True)
+            out[f"c2_bwd_{key}{v}"] = timed(lambda: ops.scan_bwd(*a, True, None, ck, dout))
 print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in out.items()}), flush=True)
