@@ -24,7 +24,9 @@ def timed(fn, it=20):
     return e[0].elapsed_time(e[1]) / it
 
 
-SHAPES = {"C2": (8, 2048, 128, 128), "C5": (4, 5120, 5248, 128), "C5m": (8, 5120, 5248, 64)}
+SHAPES = {"C2": (8, 2048, 128, 128), "C5": (4, 5120, 5248, 128), "C5m": (8, 5120, 5248, 64),
+          # query-count probes of the workgroup-round tail at C5m (2048 / 2560 / 3072 workgroups)
+          "C5m4k": (8, 4096, 5248, 64), "C5m6k": (8, 6144, 5248, 64)}
 for name in os.environ.get("SHAPES", "C2,C5,C5m").split(","):
     B, T, S, hd = SHAPES[name]
     H = 8
