@@ -285,6 +285,23 @@ constexpr float kDeferMax = 8.f;
 // more than kDeferMax, so in the steady state the O accumulators are not
 // touched by VALU (P <= 2^8 before its bf16 rounding; lse = m + log l holds
 // for any m).
+// max of 16 MFMA scores as 8 v_max3_f32 (inline asm: fmaxf on values the
+// compiler cannot prove canonical gets a v_max x, x quieting pass per operand)
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float max16_xor32(const f32x16& S) {
+  float t = max3_raw(S[0], S[1], S[2]);
+#pragma unroll
+  for (int i = 3; i < 16; i += 2) t = max3_raw(t, S[i], S[i + 1 < 16 ? i + 1 : i]);
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+  float m2;
+  asm("v_max_f32 %0, %1, %2" : "=v"(m2) : "v"(__uint_as_float(r[0])), "v"(__uint_as_float(r[1])));
+  return m2;
+}
+
 template <int ND>
 __device__ __forceinline__ void softmax_step(f32x16& S, uint32_t mask_word, int h, int lane, float c, float& m,
                                              float& l, f32x16 (&O)[ND]) {
@@ -295,10 +312,7 @@ __device__ __forceinline__ void softmax_step(f32x16& S, uint32_t mask_word, int 
     for (int i = 0; i < 16; ++i)
       if (!((w >> ((i & 3) + 8 * (i >> 2))) & 1u)) S[i] = -INFINITY;
   }
-  float tmax = S[0];
-#pragma unroll
-  for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, S[i]);
-  tmax = mtts::max_xor32(tmax) * c;
+  const float tmax = max16_xor32(S) * c;
   if (!__all(tmax <= m + kDeferMax)) {
     const float mn = fmaxf(m, tmax);
     const float alpha = exp2_raw(m - (mn == -INFINITY ? 0.f : mn));
