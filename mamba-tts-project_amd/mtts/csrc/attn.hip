@@ -1185,7 +1185,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
 //   P = exp2(c S) (masked keys 0), dS = P dP
 //   dV += P^T dO, dK += dS^T Q   (the accumulators' registers as A operands)
 template <int HD>
-__global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(BwdParams p) {
+__global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
   static_assert(HD == 64, "kv kernel: hd 64 (its K / V / dK / dV registers)");
   constexpr int KG = 128, NQ = HD / 16, ND = HD / 32;
   constexpr int QS = 32;                   // queries per staged slice
@@ -1237,10 +1237,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(BwdParams p) {
 
   // ---- slice staging: loads issued unconditionally (clamped), consumed in put()
   // slices as buffer loads (round 4): lane-constant row / column offsets,
-  // the slice origin in the scalar offset, rows at or past qend read zeros
-  f32x4 pq[NPF], pg[NPF];
-  float pl = 0.f, pd = 0.f;
-  int ps0 = qbeg;
+  // the slice origin in the scalar offset, rows at or past qend read zeros.
+  // Two register sets: slice j+2 is loaded while slice j computes and slice
+  // j+1 (loaded an iteration earlier) goes to LDS at its end -- two slices
+  // of L2 latency cover instead of one (the kernel's stall was memory wait,
+  // profiles/r04_attn_c5_pmc.txt)
+  f32x4 pq[2][NPF], pg[2][NPF];
+  float pl[2] = {0.f, 0.f}, pd[2] = {0.f, 0.f};
+  int ps0[2] = {qbeg, qbeg};
   const __amdgpu_buffer_rsrc_t rq = brsrc(qb, (uint32_t)(((int64_t)(qend - 1) * f.q_ls + HD) * 2));
   const __amdgpu_buffer_rsrc_t rg = brsrc(gb, (uint32_t)(((int64_t)(qend - 1) * a.do_ls + HD) * 2));
   const __amdgpu_buffer_rsrc_t rl = brsrc(lbuf, (uint32_t)qend * 4);
@@ -1253,30 +1257,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(BwdParams p) {
     oq_[i] = (uint32_t)((row * f.q_ls + cc) * 2);
     og_[i] = (uint32_t)((row * a.do_ls + cc) * 2);
   }
-  auto fetch = [&](int q0) __attribute__((always_inline)) {
-    ps0 = q0;
+  auto fetch = [&](auto set_c, int q0) __attribute__((always_inline)) {
+    constexpr int st = decltype(set_c)::value;
+    ps0[st] = q0;
     const int sq = (int)(q0 * f.q_ls * 2), sg = (int)(q0 * a.do_ls * 2);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      pq[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, oq_[i], sq, 0));
-      pg[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, og_[i], sg, 0));
+      pq[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, oq_[i], sq, 0));
+      pg[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, og_[i], sg, 0));
     }
     const uint32_t ol = (uint32_t)(tid & (QS - 1)) * 4;
-    pl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, ol, q0 * 4, 0));
-    pd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, ol, q0 * 4, 0));
+    pl[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, ol, q0 * 4, 0));
+    pd[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, ol, q0 * 4, 0));
   };
-  auto put = [&](int buf) __attribute__((always_inline)) {
+  auto put = [&](auto set_c, int buf) __attribute__((always_inline)) {
+    constexpr int st = decltype(set_c)::value;
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx / (HD / 8), ch = idx % (HD / 8);
-      *(f32x4*)(sQ[buf] + kimg<HD>(row, ch)) = pq[i];
-      *(f32x4*)(sG[buf] + kimg<HD>(row, ch)) = pg[i];
+      *(f32x4*)(sQ[buf] + kimg<HD>(row, ch)) = pq[st][i];
+      *(f32x4*)(sG[buf] + kimg<HD>(row, ch)) = pg[st][i];
     }
     if (tid < QS) {
-      const bool in = ps0 + tid < qend;
-      sL[buf][tid] = in ? -pl * inv_scale : 0.f;   // P = exp2(c (S + L))
-      sD[buf][tid] = in ? pd : 0.f;
+      const bool in = ps0[st] + tid < qend;
+      sL[buf][tid] = in ? -pl[st] * inv_scale : 0.f;   // P = exp2(c (S + L))
+      sD[buf][tid] = in ? pd[st] : 0.f;
     }
   };
 
@@ -1284,21 +1290,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(BwdParams p) {
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) dK[dt] = dV[dt] = f32x16{};
   const int nsl = qend > qbeg ? (qend - qbeg + QS - 1) / QS : 0;
+  const int qlast = qbeg + QS * (nsl - 1);
+  using S0_ = std::integral_constant<int, 0>;
+  using S1_ = std::integral_constant<int, 1>;
   if (nsl > 0) {
-    fetch(qbeg);
-    put(0);
+    fetch(S0_{}, qbeg);
+    put(S0_{}, 0);
+    fetch(S1_{}, min(qbeg + QS, qlast));
   }
   __syncthreads();
-  for (int j = 0; j < nsl; ++j) {
-    const int buf = j & 1, q0 = qbeg + QS * j;
-    fetch(min(q0 + QS, qbeg + QS * (nsl - 1)));   // in flight under this slice's math
-    const bf16_t* qs = sQ[buf];
-    const bf16_t* gs = sG[buf];
+  // slice j (LDS buffer j & 1); register set j & 1 is free (its slice went to
+  // LDS at the end of iteration j-1) and takes slice j+2, set (j+1) & 1
+  // holds slice j+1
+  auto slice = [&](auto par_c, int j) __attribute__((always_inline)) {
+    constexpr int par = decltype(par_c)::value;
+    const int q0 = qbeg + QS * j;
+    fetch(std::integral_constant<int, par>{}, min(q0 + 2 * QS, qlast));   // in flight under two slices' math
+    const bf16_t* qs = sQ[par];
+    const bf16_t* gs = sG[par];
     f32x16 S, D;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      S[i] = sL[buf][acc_row(i, h)];
-      D[i] = sD[buf][acc_row(i, h)];
+      S[i] = sL[par][acc_row(i, h)];
+      D[i] = sD[par][acc_row(i, h)];
     }
 #pragma unroll
     for (int s = 0; s < NQ; ++s) {
@@ -1320,8 +1334,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(BwdParams p) {
         dK[dt] = mfma_bf16(da, cat(tr_read(qs + o0), tr_read(qs + o1)), dK[dt]);
       }
     }
-    if (j + 1 < nsl) put(buf ^ 1);
+    if (j + 1 < nsl) put(std::integral_constant<int, par ^ 1>{}, par ^ 1);
     __syncthreads();
+  };
+  for (int j = 0; j < nsl; j += 2) {
+    slice(S0_{}, j);
+    if (j + 1 < nsl) slice(S1_{}, j + 1);
   }
   // ---- dK (scaled), dV: rows = keys (registers), cols = dims (lanes)
 #pragma unroll
