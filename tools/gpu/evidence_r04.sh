@@ -7,7 +7,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/ev4
+O=$R/gpurun_out/${EVDIR:-ev4}
 mkdir -p $O/pmc $O/c2 $O/c5
 cd $R
 PT="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
