@@ -647,7 +647,7 @@ struct DmaTile {
 };
 
 template <int P, typename Tio, typename Tbc, int MODE, bool SP>
-__global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFwdArgs a, const int seg_len,
+__global__ __launch_bounds__(kBlock, 2) void scan_fwd_w2_kernel(const MttsScanFwdArgs a, const int seg_len,
                                                                 float* __restrict__ seg) {
   constexpr int NS = kN / P;
   constexpr int NP2 = NS / 2;
@@ -696,11 +696,25 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
   const int gcol = ((tid % CPR) ^ DT::swz(lrow)) * EPC;
   const bool lvalid = c0 + gcol < a.dim;           // whole chunk (dim % EPC == 0)
   const int gcol_c = lvalid ? gcol : 0;            // out-of-range chunks read column c0 (discarded)
-  const Tio* __restrict__ gu = (const Tio*)a.u + (int64_t)b * a.u_bs + c0 + gcol_c;
-  const Tio* __restrict__ gd = (const Tio*)a.delta + (int64_t)b * a.delta_bs + c0 + gcol_c;
-  const Tio* __restrict__ gz = has_z ? (const Tio*)a.z + (int64_t)b * a.z_bs + c0 + gcol_c : gu;
   const int64_t z_ls = has_z ? a.z_ls : a.u_ls;
-  Tio* __restrict__ go = (Tio*)a.out + (int64_t)b * a.out_bs + c0 + gcol;
+  // u / delta / z / out through buffer descriptors over the block's channel
+  // columns of the batch row (as scan_fwd_c1_kernel; host: spans below 2 GiB):
+  // a lane-constant byte offset + the tile's row origin in the scalar offset.
+  // Rows at or past L read 0 (rows of a later segment read real values that
+  // are never used); stores past the segment's last row are dropped.
+  const int ncol = min(CPB, a.dim - c0);
+  auto span = [&](int64_t ls, int rows) { return (uint32_t)(((int64_t)(rows - 1) * ls + ncol) * ES); };
+  const i32x4 ru = rsrc4((const Tio*)a.u + (int64_t)b * a.u_bs + c0, span(a.u_ls, L));
+  const i32x4 rd = rsrc4((const Tio*)a.delta + (int64_t)b * a.delta_bs + c0, span(a.delta_ls, L));
+  const i32x4 rz = has_z ? rsrc4((const Tio*)a.z + (int64_t)b * a.z_bs + c0, span(a.z_ls, L)) : ru;
+  const uint32_t vu = (uint32_t)((lrow * a.u_ls + gcol_c) * ES), vd = (uint32_t)((lrow * a.delta_ls + gcol_c) * ES);
+  const uint32_t vz = (uint32_t)((lrow * z_ls + gcol_c) * ES);
+  const uint64_t opp = (uint64_t)(uintptr_t)((Tio*)a.out + (int64_t)b * a.out_bs + c0);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(   // wave-uniform: no waterfall
+      (void*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(opp >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)opp)),
+      0, __builtin_amdgcn_readfirstlane((int)span(a.out_ls, t_end)), 0x00020000);
+  const uint32_t vo = lvalid ? (uint32_t)((lrow * a.out_ls + gcol) * ES) : 0xFFFFFFF0u;
 
   const int e0 = tid * VPT;
   const int st_s = e0 / (2 * kN), st_col = e0 % (2 * kN);
@@ -749,15 +763,13 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
     ldg_asm<SW, SHALF>(stg, st0 + (int64_t)min(t0 + st_s, L - 1) * st_ls + (st_col % kN));
   };
   auto dma_tile = [&](int t0, int buf) __attribute__((always_inline)) {
-    const int t = t0 + lrow;
-    const int tc = t < t_end ? t : t_begin;        // rows past the segment: any in-range row (masked)
-    auto lds = [&](int q) { return (void*)&sX[buf][q][wave * 64 * EPC]; };
+    auto lds = [&](int q) { return lds_u32(&sX[buf][q][wave * 64 * EPC]); };
 #ifdef MTTS_DIAG_NOMEM
     return;  // timing-only build: the tile images keep stale contents
 #endif
-    dma16(gu + (int64_t)tc * a.u_ls, lds(0));
-    dma16(gd + (int64_t)tc * a.delta_ls, lds(1));
-    if constexpr (NA == 3) dma16(gz + (int64_t)tc * z_ls, lds(2));
+    dma16b(ru, vu, (int)(t0 * a.u_ls * ES), lds(0));
+    dma16b(rd, vd, (int)(t0 * a.delta_ls * ES), lds(1));
+    if constexpr (NA == 3) dma16b(rz, vz, (int)(t0 * z_ls * ES), lds(2));
   };
   auto stage_bc = [&](int buf) __attribute__((always_inline)) {
     float v[VPT];
@@ -780,13 +792,13 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_w2_kernel(const MttsScanFw
     }
   };
   auto store_tile = [&](int t0, int buf) __attribute__((always_inline)) {
-    const int t = t0 + lrow;
     const uint4 v = *reinterpret_cast<const uint4*>(&sX[buf][0][tid * EPC]);
 #ifdef MTTS_DIAG_NOMEM
-    if (v.x == 0x12345u && v.y == 0x777u) go[0] = (Tio)0;  // keep the tile alive, never true
+    if (v.x == 0x12345u && v.y == 0x777u) sX[buf][0][0] = (Tio)0;  // keep the tile alive, never true
     return;
 #endif
-    if (lvalid && t < t_end) *reinterpret_cast<uint4*>(go + (int64_t)t * a.out_ls) = v;
+    __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, ro, vo,
+                                           (int)(t0 * a.out_ls * ES), 0);
   };
   // element (row, local channel) of an array image
   auto at = [&](int row, int ch) __attribute__((always_inline)) {
@@ -2061,7 +2073,11 @@ static void launch_fwd_sp(const MttsScanFwdArgs* a, const FwdPlan& pl, hipStream
     else launch_c1<Tio, Tbc, SP, false>(a, st);
     return;
   }
-  if (wide_io_ok(a)) {
+  // the LDS-DMA kernel addresses rows through buffer descriptors: a batch
+  // row's byte span (and the last tile's row origin) below 2 GiB
+  const int64_t es = a->dtype_io == MTTS_BF16 ? 2 : 4;
+  auto fits = [&](int64_t ls) { return (int64_t)(a->seqlen + 64) * ls * es < (1ll << 31); };
+  if (wide_io_ok(a) && fits(a->u_ls) && fits(a->delta_ls) && fits(a->out_ls) && (!a->z || fits(a->z_ls))) {
     if (pl.K > 1)
       hipLaunchKernelGGL((scan_fwd_w2_kernel<P, Tio, Tbc, kState, SP>), dim3(nbx, a->batch, pl.K - 1),
                          dim3(kBlock), 0, st, *a, pl.seg_len, seg);
