@@ -130,6 +130,36 @@ def test_fully_masked_rows_are_nan_and_others_exact(dtype, T, S, hd):
     close(out[[0, 2]], ref[[0, 2]], 2e-5 if dtype == torch.float32 else 2e-2)
 
 
+@pytest.mark.parametrize("T,S,hd", [(200, 333, 64), (256, 1100, 64), (130, 700, 128), (300, 260, 128)])
+def test_rows_past_the_ends_are_not_used(T, S, hd):
+    """Buffer-addressed K / V / Q / dO rows (long-key forward, dQ and dK/dV
+    kernels): q / kv / dout as row views of larger tensors whose rows past
+    T / S hold NaN.  Forward and backward must equal the runs on contiguous
+    copies bit for bit and stay finite (no row past the end is read into a
+    result, whatever the buffer range check does with the scalar offset)."""
+    from mtts import attn_kernels as A
+    B, H = 2, 4
+    q, kv, kpm = make(B, T, S, H, hd, torch.bfloat16, seed=T + S)
+    d = H * hd
+    pad = 40
+
+    def big(t, rows):
+        bt = torch.full((t.shape[0], rows + pad, t.shape[2]), float("nan"), device="cuda", dtype=t.dtype)
+        bt[:, :rows] = t
+        return bt[:, :rows]
+
+    qv, kvv = big(q, T), big(kv, S)
+    out, lse = A.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+    out2, lse2 = A.attention_fwd(qv, kvv[..., :d], kvv[..., d:], H, kpm, want_lse=True)
+    assert torch.isfinite(out2).all() and torch.equal(out, out2) and torch.equal(lse, lse2)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    do = torch.randn(out.shape, device="cuda", generator=g).to(out.dtype)
+    r1 = A.attention_bwd(q, kv[..., :d], kv[..., d:], H, kpm, out, lse, do)
+    r2 = A.attention_bwd(qv, kvv[..., :d], kvv[..., d:], H, kpm, out2, lse2, big(do, T))
+    for a, b in zip(r1, r2):
+        assert torch.isfinite(b).all() and torch.equal(a, b)
+
+
 @pytest.mark.parametrize("S", [24, 128, 200, 1000])
 def test_decode_fully_masked_rows_are_nan(S):
     """q_len = 1 (both decode kernels): a fully masked key side gives NaN rows

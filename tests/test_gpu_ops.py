@@ -168,6 +168,38 @@ def test_scan_c1_kernel_vs_oracle(B, L, D, io, bc, with_z, strided):
     close(out.float(), out_w.float(), rtol=tol, name=f"{kernel} vs w2 out")
 
 
+@pytest.mark.parametrize("path,segs", [(1, None), (2, None), (2, 3), (3, None)])
+@pytest.mark.parametrize("L", [37, 1003])
+@pytest.mark.parametrize("io", ["f32", "bf16"])
+def test_scan_rows_past_L_neither_read_nor_written(path, segs, L, io):
+    """The buffer-addressed forward kernels (c1, the P-lane LDS-DMA kernel)
+    and the narrow kernel on row views of larger tensors: rows >= L of u /
+    delta / z / B / C hold NaN and the output rows >= L hold a sentinel.  The
+    outputs must equal the run on contiguous copies bit for bit, stay finite,
+    and the sentinel rows must be untouched (no tile row past L is used or
+    stored, whatever the buffer range check does with the scalar offset)."""
+    from mtts import _lib, ops
+    B, D, pad = 2, 512, 40
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16}[io]
+    u, dl, A, Bm, Cm, Dp, z, bias, h0 = _scan_inputs(B, L, D, dt, dt, L + path)
+
+    def big(t, fill):
+        bt = torch.full((t.shape[0], L + pad, t.shape[2]), fill, device=DEV, dtype=t.dtype)
+        bt[:, :L] = t
+        return bt
+
+    nan = float("nan")
+    ub, db_, zb, Bb, Cb = big(u, nan), big(dl, nan), big(z, nan), big(Bm, nan), big(Cm, nan)
+    ob = torch.full((B, L + pad, D), 7.0, device=DEV, dtype=dt)
+    with _lib.override(scan_path=path, scan_segs=segs):
+        ref, rlast, _ = ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, h0=h0, want_last=True)
+        out, last, _ = ops.scan_fwd(ub[:, :L], db_[:, :L], A, Bb[:, :L], Cb[:, :L], Dp, zb[:, :L], bias, True,
+                                    h0=h0, want_last=True, out=ob[:, :L])
+    assert torch.isfinite(out).all() and torch.isfinite(last).all()
+    assert torch.equal(out, ref) and torch.equal(last, rlast)
+    assert (ob[:, L:] == 7.0).all(), "a store landed past row L"
+
+
 def test_scan_c1_north_star_width():
     """At the north-star width (B=32, D=2048: the c1 kernel is the default)
     with a shorter L: c1 against the P=4 LDS-DMA kernel on every element, and
