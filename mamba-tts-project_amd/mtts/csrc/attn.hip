@@ -387,8 +387,6 @@ __global__ __launch_bounds__(256, 4) void attn_fwd_db_kernel(MttsAttnFwdArgs a) 
     for (int s = 0; s < NQ; ++s) QF[u][s] = qv ? *(const s16x8*)(qp + 16 * s + 8 * h) : s16x8{};
   }
 
-  // (round 4: the block origin rides in the VECTOR offset -- the buffer range
-  // check covers voffset, not the scalar offset -- so rows past kv_len read 0)
   // Loads are issued unconditionally and consumed only in put(): a select or
   // branch on the loaded data in fetch() would make the compiler wait for
   // them before the block's MFMAs, which is exactly what this kernel avoids.
@@ -415,10 +413,10 @@ __global__ __launch_bounds__(256, 4) void attn_fwd_db_kernel(MttsAttnFwdArgs a) 
     const int sk = (int)(k0 * a.k_ls * 2);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      pk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, ok_[i] + (uint32_t)sk, 0, 0));
-      pv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, ok_[i] + (uint32_t)sk, 0, 0));
+      pk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, ok_[i], sk, 0));
+      pv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, ok_[i], sk, 0));
     }
-    praw = __builtin_amdgcn_raw_buffer_load_b8(rm, (uint32_t)(lane + k0), 0, 0);
+    praw = __builtin_amdgcn_raw_buffer_load_b8(rm, (uint32_t)lane, k0, 0);
   };
   auto put = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
@@ -1078,10 +1076,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
     const int sk = (int)(k0 * f.k_ls * 2);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      pk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, ok_[i] + (uint32_t)sk, 0, 0));
-      pv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, ok_[i] + (uint32_t)sk, 0, 0));
+      pk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, ok_[i], sk, 0));
+      pv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, ok_[i], sk, 0));
     }
-    praw = __builtin_amdgcn_raw_buffer_load_b8(rm, (uint32_t)(lane + k0), 0, 0);
+    praw = __builtin_amdgcn_raw_buffer_load_b8(rm, (uint32_t)lane, k0, 0);
   };
   auto put = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
@@ -1265,12 +1263,12 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
     const int sq = (int)(q0 * f.q_ls * 2), sg = (int)(q0 * a.do_ls * 2);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      pq[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, oq_[i] + (uint32_t)sq, 0, 0));
-      pg[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, og_[i] + (uint32_t)sg, 0, 0));
+      pq[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, oq_[i], sq, 0));
+      pg[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, og_[i], sg, 0));
     }
     const uint32_t ol = (uint32_t)(tid & (QS - 1)) * 4;
-    pl[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, ol + (uint32_t)(q0 * 4), 0, 0));
-    pd[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, ol + (uint32_t)(q0 * 4), 0, 0));
+    pl[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, ol, q0 * 4, 0));
+    pd[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, ol, q0 * 4, 0));
   };
   auto put = [&](auto set_c, int buf) __attribute__((always_inline)) {
     constexpr int st = decltype(set_c)::value;

@@ -699,10 +699,9 @@ __global__ __launch_bounds__(kBlock, 2) void scan_fwd_w2_kernel(const MttsScanFw
   const int64_t z_ls = has_z ? a.z_ls : a.u_ls;
   // u / delta / z / out through buffer descriptors over the block's channel
   // columns of the batch row (as scan_fwd_c1_kernel; host: spans below 2 GiB):
-  // a lane-constant byte offset plus the tile's row origin, both in the
-  // vector offset (the part the range check covers).  Rows at or past L read
-  // 0 (rows of a later segment read real values that are never used); stores
-  // past the segment's last row are dropped.
+  // a lane-constant byte offset + the tile's row origin in the scalar offset.
+  // Rows at or past L read 0 (rows of a later segment read real values that
+  // are never used); stores past the segment's last row are dropped.
   const int ncol = min(CPB, a.dim - c0);
   auto span = [&](int64_t ls, int rows) { return (uint32_t)(((int64_t)(rows - 1) * ls + ncol) * ES); };
   const i32x4 ru = rsrc4((const Tio*)a.u + (int64_t)b * a.u_bs + c0, span(a.u_ls, L));
@@ -768,10 +767,9 @@ __global__ __launch_bounds__(kBlock, 2) void scan_fwd_w2_kernel(const MttsScanFw
 #ifdef MTTS_DIAG_NOMEM
     return;  // timing-only build: the tile images keep stale contents
 #endif
-    // row origins in the VECTOR offset (the range check covers voffset only)
-    dma16b(ru, vu + (uint32_t)(t0 * a.u_ls * ES), 0, lds(0));
-    dma16b(rd, vd + (uint32_t)(t0 * a.delta_ls * ES), 0, lds(1));
-    if constexpr (NA == 3) dma16b(rz, vz + (uint32_t)(t0 * z_ls * ES), 0, lds(2));
+    dma16b(ru, vu, (int)(t0 * a.u_ls * ES), lds(0));
+    dma16b(rd, vd, (int)(t0 * a.delta_ls * ES), lds(1));
+    if constexpr (NA == 3) dma16b(rz, vz, (int)(t0 * z_ls * ES), lds(2));
   };
   auto stage_bc = [&](int buf) __attribute__((always_inline)) {
     float v[VPT];
@@ -799,8 +797,8 @@ __global__ __launch_bounds__(kBlock, 2) void scan_fwd_w2_kernel(const MttsScanFw
     if (v.x == 0x12345u && v.y == 0x777u) sX[buf][0][0] = (Tio)0;  // keep the tile alive, never true
     return;
 #endif
-    __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, ro,
-                                           lvalid ? vo + (uint32_t)(t0 * a.out_ls * ES) : vo, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, ro, vo,
+                                           (int)(t0 * a.out_ls * ES), 0);
   };
   // element (row, local channel) of an array image
   auto at = [&](int row, int ch) __attribute__((always_inline)) {
@@ -1915,11 +1913,9 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
     for (int k = 0; k < DPT; ++k) {
       const int t = it * TT + k * RPD;   // rows past L read zeros (never stored)
       const uint32_t lk = lb + (uint32_t)(k * RPD * 64 * ES);
-      // the row origin rides in the VECTOR offset: the range check covers
-      // voffset (+ the instruction offset), not the scalar offset
-      dma16b(ru, vu + (uint32_t)(t * a.u_ls * ES), 0, lk);
-      dma16b(rd, vd + (uint32_t)(t * a.delta_ls * ES), 0, lk + IMG * ES);
-      if constexpr (HZ) dma16b(rz, vz + (uint32_t)(t * a.z_ls * ES), 0, lk + 2 * IMG * ES);
+      dma16b(ru, vu, (int)(t * a.u_ls * ES), lk);
+      dma16b(rd, vd, (int)(t * a.delta_ls * ES), lk + IMG * ES);
+      if constexpr (HZ) dma16b(rz, vz, (int)(t * a.z_ls * ES), lk + 2 * IMG * ES);
     }
   };
   auto compute_tile = [&](auto tail, int it, int buf) __attribute__((always_inline)) {
@@ -1988,9 +1984,7 @@ __global__ __launch_bounds__(256, 1) void scan_fwd_c1_kernel(const MttsScanFwdAr
 #if defined(MTTS_C1_DIAG_NOSTORE)
       asm volatile("" ::"v"(y));
 #else
-      // one 4- (2-) byte store per lane and step, the row origin in the scalar
-      // offset (not range-checked): tail tiles store only rows below L
-      if (TAIL && t0 + s >= L) return;
+      // one 4- (2-) byte store per lane and step; rows past L fall outside the range
       if constexpr (ES == 4)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(y), ro, (uint32_t)(lane * 4), (t0 + s) * (int)a.out_ls * 4, 0);
       else
