@@ -306,23 +306,33 @@ __global__ __launch_bounds__(512) void conv_bwd_tile_kernel(const MttsConvBwdArg
   const bool cok = c0 < f.dim;
   const int cc = cok ? c0 : 0;       // lanes past dim run on channel 0 and store nothing (no early exit: LDS sum below)
   const int b = blockIdx.z;
-  const int t0 = (blockIdx.y * 8 + wave) * TT;
+  const int t0 = __builtin_amdgcn_readfirstlane((blockIdx.y * 8 + wave) * TT);   // wave-uniform (scalar offsets)
   const int L = f.seqlen;
-  const T* xb = (const T*)f.x + (int64_t)b * f.x_bs + cc;
-  const T* gb = (const T*)a.dout + (int64_t)b * a.dout_bs + cc;
-  // x rows t0-3 .. t0+TT+2, dout rows t0 .. t0+TT+2 (g beyond L is 0)
+  // x rows t0-3 .. t0+TT+2, dout rows t0 .. t0+TT+2 as buffer loads (round
+  // 4): descriptors over the block's columns of the batch row, the lane's
+  // column in the vector offset, the row origin in the scalar offset; rows
+  // before 0 or at / past L fall outside the range and read 0 (rows < 0 are
+  // replaced by the prefix state below, rows >= L have g = 0) -- no clamps or
+  // 64-bit row arithmetic per load (host: row spans below 2 GiB)
   using RV = rawv_t<T, CPT>;
+  constexpr int ES = (int)sizeof(T);
+  const int cb = blockIdx.x * 64 * CPT, ncol = min(64 * CPT, f.dim - cb);
+  auto span = [&](int64_t ls) { return (int)(((int64_t)(L - 1) * ls + ncol) * ES); };
+  const __amdgpu_buffer_rsrc_t rxs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>((const T*)f.x + (int64_t)b * f.x_bs + cb), 0, span(f.x_ls), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rgs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>((const T*)a.dout + (int64_t)b * a.dout_bs + cb), 0, span(a.dout_ls), 0x00020000);
+  const uint32_t vcol = (uint32_t)(lane * CPT * ES);
+  auto ld = [&](const __amdgpu_buffer_rsrc_t& r, int row, int64_t ls) __attribute__((always_inline)) -> RV {
+    const int so = (int)(row * ls * ES);
+    if constexpr (sizeof(RV) == 16) return __builtin_bit_cast(RV, __builtin_amdgcn_raw_buffer_load_b128(r, vcol, so, 0));
+    else return __builtin_bit_cast(RV, __builtin_amdgcn_raw_buffer_load_b64(r, vcol, so, 0));
+  };
   RV rx[TT + 6], rg[TT + 3];
 #pragma unroll
-  for (int i = 0; i < TT + 6; ++i) {
-    const int t = min(max(t0 - 3 + i, 0), L - 1);
-    rx[i] = *reinterpret_cast<const RV*>(xb + (int64_t)t * f.x_ls);
-  }
+  for (int i = 0; i < TT + 6; ++i) rx[i] = ld(rxs, t0 - 3 + i, f.x_ls);
 #pragma unroll
-  for (int i = 0; i < TT + 3; ++i) {
-    const int t = min(t0 + i, L - 1);
-    rg[i] = *reinterpret_cast<const RV*>(gb + (int64_t)t * a.dout_ls);
-  }
+  for (int i = 0; i < TT + 3; ++i) rg[i] = ld(rgs, t0 + i, a.dout_ls);
   float w[kK][CPT], bias[CPT];
 #pragma unroll
   for (int q = 0; q < CPT; ++q) {
@@ -523,7 +533,9 @@ extern "C" int mtts_causal_conv1d_bwd(const MttsConvBwdArgs* a, void* stream) {
                    (uintptr_t)a->dx % 16 == 0 && (f.x_ls * es) % 16 == 0 && (f.x_bs * es) % 16 == 0 &&
                    (a->dout_ls * es) % 16 == 0 && (a->dout_bs * es) % 16 == 0 && (a->dx_ls * es) % 16 == 0 &&
                    (a->dx_bs * es) % 16 == 0;
-  const bool tiled = vec && (uintptr_t)f.w % 16 == 0 && !tiled_off();
+  // the tiled backward reads rows through buffer descriptors: spans below 2 GiB
+  auto fits = [&](int64_t ls) { return (int64_t)(f.seqlen + 16) * ls * es < (1ll << 31); };
+  const bool tiled = vec && (uintptr_t)f.w % 16 == 0 && !tiled_off() && fits(f.x_ls) && fits(a->dout_ls);
   int nparts;
   if (f.dtype == MTTS_F32) {
     if (vec) nparts = launch_bwd<float, 4>(a, st, part, tiled);
