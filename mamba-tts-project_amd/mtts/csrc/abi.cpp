@@ -7,7 +7,13 @@
 
 namespace mtts {
 static thread_local char g_err[512] = "";
-static int g_ovr[MTTS_OVR_COUNT] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
+// every key starts at MTTS_OVR_AUTO (-1), whatever MTTS_OVR_COUNT is
+struct OvrTable {
+  int v[MTTS_OVR_COUNT];
+  OvrTable() { for (int& x : v) x = -1; }
+};
+static OvrTable g_ovr_tab;
+static int* const g_ovr = g_ovr_tab.v;
 int override_of(int key) { return (key >= 0 && key < MTTS_OVR_COUNT) ? __atomic_load_n(&g_ovr[key], __ATOMIC_RELAXED) : -1; }
 void set_error(const char* fmt, ...) {
   va_list ap;

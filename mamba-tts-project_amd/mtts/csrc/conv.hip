@@ -225,6 +225,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(const MttsConvBwdArgs a, 
 // channels: the dw / db partials of the 8 tiles are summed through LDS, so
 // the partial slab has one row per 64 steps (C2: 10 MB instead of 21).
 
+typedef int i32x4c __attribute__((ext_vector_type(4)));
+
 template <typename T, int CPT>
 using rawv_t = typename std::conditional<sizeof(T) * CPT == 16, uint4, uint2>::type;
 
@@ -257,15 +259,29 @@ __global__ __launch_bounds__(256) void conv_fwd_tile_kernel(const MttsConvFwdArg
   const int c0 = (blockIdx.x * 256 + threadIdx.x) * CPT;
   if (c0 >= a.dim) return;
   const int b = blockIdx.z;
-  const int t0 = blockIdx.y * TT;
+  const int t0 = blockIdx.y * TT;   // block-uniform: the row origins below are scalar offsets
   const int L = a.seqlen;
-  const T* xb = (const T*)a.x + (int64_t)b * a.x_bs + c0;
+  // x rows t0-3 .. t0+TT-1 and the output rows as buffer accesses (round 5, as
+  // the tiled backward): descriptors over the block's columns of the batch row,
+  // the lane's column in the vector offset, the row origin in the scalar
+  // offset.  gfx950's range check covers voffset + soffset without 32-bit
+  // wrap (tools/ubench/buffer_oob_probe.hip, profiles/r05_buffer_oob_probe.txt):
+  // rows before 0 / at or past L read 0 (rows < 0 are replaced by the prefix
+  // state below) and stores past L are dropped -- no clamps or 64-bit row
+  // arithmetic per access (host: row spans below 2 GiB)
+  constexpr int ES = (int)sizeof(T);
+  const int cb = blockIdx.x * 256 * CPT, ncol = min(256 * CPT, a.dim - cb);
+  auto span = [&](int64_t ls) { return (int)(((int64_t)(L - 1) * ls + ncol) * ES); };
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>((const T*)a.x + (int64_t)b * a.x_bs + cb), 0, span(a.x_ls), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      (T*)a.out + (int64_t)b * a.out_bs + cb, 0, span(a.out_ls), 0x00020000);
+  const uint32_t vcol = (uint32_t)((c0 - cb) * ES);
+  const int xls = (int)a.x_ls * ES, ols = (int)a.out_ls * ES;
   uint4 raw[TT + 3];
 #pragma unroll
-  for (int i = 0; i < TT + 3; ++i) {   // rows outside [0, L) load a valid row, replaced below / never stored
-    const int t = min(max(t0 - 3 + i, 0), L - 1);
-    raw[i] = *reinterpret_cast<const uint4*>(xb + (int64_t)t * a.x_ls);
-  }
+  for (int i = 0; i < TT + 3; ++i)
+    raw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, vcol, (t0 - 3 + i) * xls, 0));
   float w[kK][CPT], bias[CPT];
 #pragma unroll
   for (int q = 0; q < CPT; ++q) {
@@ -283,7 +299,6 @@ __global__ __launch_bounds__(256) void conv_fwd_tile_kernel(const MttsConvFwdArg
     unpack16<T, CPT>(raw[1], x1);
     unpack16<T, CPT>(raw[2], x2);
   }
-  T* out = (T*)a.out + (int64_t)b * a.out_bs + c0;
 #pragma unroll
   for (int s = 0; s < TT; ++s) {
     float x3[CPT], o[CPT];
@@ -294,7 +309,20 @@ __global__ __launch_bounds__(256) void conv_fwd_tile_kernel(const MttsConvFwdArg
       o[q] = a.silu ? silu_f(v) : v;
       x0[q] = x1[q]; x1[q] = x2[q]; x2[q] = x3[q];
     }
-    if (t0 + s < L) stv<T, CPT>(out + (int64_t)(t0 + s) * a.out_ls, o);
+    uint4 wv;
+    if constexpr (sizeof(T) == 4) {
+      wv = make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
+    } else {
+      uint32_t qv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) qv[k] = (uint32_t)f2bf(o[2 * k]) | ((uint32_t)f2bf(o[2 * k + 1]) << 16);
+      wv = make_uint4(qv[0], qv[1], qv[2], qv[3]);
+    }
+    // the row origin goes into the VECTOR offset for stores: with a register
+    // soffset hipcc omits the wait states a VALU write of a >8-byte store's data
+    // registers needs after the store, and on gfx950 lanes 12-15 of each 16
+    // then stored the next row's values (the round-4 revert)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4c, wv), ro, vcol + (uint32_t)((t0 + s) * ols), 0, 0);
   }
 }
 
@@ -460,7 +488,9 @@ static bool tiled_off() { return override_of(MTTS_OVR_CONV_UNTILED) == 1; }
 template <typename T, int CPT>
 static void launch_fwd(const MttsConvFwdArgs* a, hipStream_t st) {
   if constexpr (sizeof(T) * CPT == 16) {
-   if (!tiled_off()) {
+   // buffer-addressed rows: spans below 2 GiB
+   auto fits = [&](int64_t ls) { return (int64_t)(a->seqlen + 16) * ls * (int64_t)sizeof(T) < (1ll << 31); };
+   if (!tiled_off() && fits(a->x_ls) && fits(a->out_ls)) {
     dim3 grid((a->dim / CPT + 255) / 256, (a->seqlen + kFwdTT - 1) / kFwdTT, a->batch);
     hipLaunchKernelGGL((conv_fwd_tile_kernel<T, CPT, kFwdTT>), grid, dim3(256), 0, st, *a);
     return;

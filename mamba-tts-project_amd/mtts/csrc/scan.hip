@@ -714,7 +714,10 @@ __global__ __launch_bounds__(kBlock, 2) void scan_fwd_w2_kernel(const MttsScanFw
       (void*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(opp >> 32)) << 32) |
                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)opp)),
       0, __builtin_amdgcn_readfirstlane((int)span(a.out_ls, t_end)), 0x00020000);
-  const uint32_t vo = lvalid ? (uint32_t)((lrow * a.out_ls + gcol) * ES) : 0xFFFFFFF0u;
+  // lanes past dim store nothing (a branch, not an out-of-range voffset: with
+  // the row origin in the scalar offset, voffset + soffset would wrap back into
+  // range -- tools/ubench/buffer_oob_probe.hip)
+  const uint32_t vo = (uint32_t)((lrow * a.out_ls + gcol_c) * ES);
 
   const int e0 = tid * VPT;
   const int st_s = e0 / (2 * kN), st_col = e0 % (2 * kN);
@@ -797,8 +800,11 @@ __global__ __launch_bounds__(kBlock, 2) void scan_fwd_w2_kernel(const MttsScanFw
     if (v.x == 0x12345u && v.y == 0x777u) sX[buf][0][0] = (Tio)0;  // keep the tile alive, never true
     return;
 #endif
-    __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, ro, vo,
-                                           (int)(t0 * a.out_ls * ES), 0);
+    // row origin in the vector offset, soffset 0: with a register soffset
+    // hipcc drops the store-data wait states (see conv_fwd_tile_kernel)
+    if (lvalid)
+      __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)v.x, (int)v.y, (int)v.z, (int)v.w}, ro,
+                                             vo + (uint32_t)(t0 * a.out_ls * ES), 0, 0);
   };
   // element (row, local channel) of an array image
   auto at = [&](int row, int ch) __attribute__((always_inline)) {
@@ -1199,6 +1205,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
       br[g * kPB + j] = dt;
       br[16 * kBrP + g * kPB + j] = dy;
     }
+    __builtin_amdgcn_wave_barrier();   // the wave's table writes precede the cross-lane f4 reads
     static_for<G>([&](auto gc) {
       constexpr int g = G - 1 - decltype(gc)::value;
       const f4 d4 = *reinterpret_cast<const f4*>(br + g * kPB);
@@ -1449,6 +1456,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       br[g * kPB + j] = dt[g];
       br[16 * kBrP + g * kPB + j] = dt[g] * uu[g];
     }
+    __builtin_amdgcn_wave_barrier();   // the wave's table writes precede the cross-lane f4 reads
     auto bcast_dt = [&](int g, f4& d4, f4& u4) __attribute__((always_inline)) {
       d4 = *reinterpret_cast<const f4*>(br + g * kPB);
       u4 = *reinterpret_cast<const f4*>(br + 16 * kBrP + g * kPB);

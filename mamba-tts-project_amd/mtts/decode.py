@@ -80,11 +80,14 @@ class DecodeEngine:
         self.reset()
 
     def reset(self):
-        # a flag left by the previous session must not surface in the next one:
-        # wait for its copy, then clear host and device flags (check_errors()
-        # before reset() is how a caller observes it)
+        # a flag left by the previous session must not surface in the next one,
+        # and must not be lost either (nn.Embedding raises on every such step,
+        # mamba_decoder.py:217): wait for its copy, clear host and device
+        # flags, reset the engine, then raise it
+        flagged = False
         if getattr(self, "_err_ev", None) is not None:
             self._err_ev.synchronize()
+            flagged = int(self._err_host[0]) != 0
             self._err_host.zero_()
             _err_flag(self._err_dev).zero_()
         self._err_host = None
@@ -97,6 +100,8 @@ class DecodeEngine:
         self.ctx = None
         self.graph = None
         self.states = None
+        if flagged:
+            raise IndexError("decode_step: last_token id out of range of token_embed (index out of range in self)")
 
     # -- conditioning context -------------------------------------------------
     def _build_ctx(self, text_hidden, z_style, text_mask, ref_hidden, ref_mask, cd):

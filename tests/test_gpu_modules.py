@@ -162,16 +162,42 @@ def test_style_pipeline_vs_reference(golden):
     assert torch.equal(lc.cpu(), torch.from_numpy(g["lengths_cap"]))
 
 
-def test_reference_module_runs_on_mamba_ssm_shim(golden, tmp_path):
-    """The reference's own mamba_decoder.py source, importing `mamba_ssm`
-    from this package, reproduces the reference goldens (fixture copies the
-    golden state_dict; the reference file itself is NOT shipped - this test
-    uses our drop-in module, which has the same import line)."""
+def test_mamba_ssm_shim_mixer_matches_oracle(golden):
+    """`from mamba_ssm import Mamba` (the reference's import line,
+    mamba_decoder.py:4) resolves to the HIP mixer, and a mixer built the way
+    the reference builds it (`Mamba(d_model, d_state=16, d_conv=4, expand=2)`,
+    mamba_decoder.py:26) with layer 0's golden weights computes the oracle's
+    mixer (`mamba_forward_ref`, pinned by the golden fixtures) under the
+    `(out, state)` contract of mamba_decoder.py:10-15: outputs, both states
+    and every input / parameter gradient at 1e-3, fp32.  (The reference file
+    itself is not shipped: the decoder goldens above are what it produced.)"""
     import importlib
     import mamba_ssm
+    import oracle.mamba_ref as R
     assert mamba_ssm.Mamba.__module__ == "mtts.mamba"
-    mod = importlib.import_module("mamba_decoder")
-    assert mod.Mamba is mamba_ssm.Mamba
+    assert importlib.import_module("mamba_decoder").Mamba is mamba_ssm.Mamba
+    g = golden("decoder.npz")
+    pre = "sd/layers.0.mamba."
+    sd = {k[len(pre):]: torch.from_numpy(v) for k, v in g.items() if k.startswith(pre)}
+    mix = mamba_ssm.Mamba(64, d_state=16, d_conv=4, expand=2)
+    mix.load_state_dict(sd)
+    mix = mix.to(DEV)
+    torch.manual_seed(3)
+    x = torch.randn(3, 37, 64, dtype=torch.float64)
+    G = torch.randn(3, 37, 64, dtype=torch.float64)
+    xg = x.float().to(DEV).requires_grad_(True)
+    out, (conv_state, ssm_state) = mix(xg)
+    (out * G.float().to(DEV)).sum().backward()
+    p = {k: v.double().requires_grad_(True) for k, v in sd.items()}
+    xr = x.clone().requires_grad_(True)
+    ro, (rc, rs) = R.mamba_forward_ref(p, "", xr)
+    (ro * G).sum().backward()
+    close(out, ro, name="mixer out")
+    close(conv_state, rc, name="conv_state")
+    close(ssm_state, rs, name="ssm_state")
+    close(xg.grad, xr.grad, name="dx")
+    for n, t in mix.named_parameters():
+        close(t.grad, p[n].grad, name=n)
 
 
 @pytest.mark.parametrize("mode", ["graph", "eager"])
@@ -246,7 +272,8 @@ def test_decode_engine_out_of_range_token_raises():
     the states) and flags it; the engine reads the flag without a host sync
     and raises IndexError at a later decode_step (best-effort, deferred) or at
     the blocking check_errors(), then clears it (the following steps run
-    normally); reset() drops a pending flag so a new session starts clean."""
+    normally); reset() raises a pending flag, clearing it, so a new session
+    starts clean and no error is lost."""
     import mamba_decoder
     torch.manual_seed(1)
     m = mamba_decoder.MambaTTSDecoder(10, d_model=1024, n_layers=2, n_heads=8, d_ff=2048, d_style=256).to(DEV).eval()
@@ -277,6 +304,8 @@ def test_decode_engine_out_of_range_token_raises():
             eng.check_errors()
         eng.check_errors()
         m.decode_step(bad, text, z, st, 5)
+        with pytest.raises(IndexError, match="out of range"):   # reset() raises a pending flag, then clears it
+            eng.reset()
         eng.reset()
         lg, st = m.decode_step(good, text, z, [None, None], 0)
         torch.cuda.synchronize()

@@ -347,6 +347,55 @@ def test_conv1d_tiled_vs_oracle_with_state(shape, dtype):
     close(db2, db, rtol=1e-5, name="db tiled vs untiled")
 
 
+@pytest.mark.parametrize("untiled", [0, 1])
+@pytest.mark.parametrize("with_state", [False, True])
+@pytest.mark.parametrize("L,D", [(37, 64), (130, 2048), (1003, 200)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv1d_rows_outside_0_L_neither_read_nor_written(dtype, L, D, with_state, untiled):
+    """The buffer-addressed tiled conv kernels put a tile's row origin in the
+    scalar offset, so their first tile issues loads for rows -3..-1 and their
+    last tile rows past L (read as 0 by the range check, which covers voffset +
+    soffset: profiles/r05_buffer_oob_probe.txt).  Here x / dout are row views
+    of larger tensors whose rows before 0 and from L on hold NaN, and out / dx
+    are row views of sentinel-filled tensors: results must equal the run on
+    contiguous copies bit for bit, stay finite, and the sentinel rows must be
+    untouched.  Channel-last with the in_proj row stride (2D), D % 256 != 0
+    cases included (partial channel blocks)."""
+    from mtts import _lib, ops
+    torch.manual_seed(5)
+    B, pad = 2, 24
+    nan = float("nan")
+    w = torch.randn(D, 4, device=DEV) * 0.5
+    b = torch.randn(D, device=DEV) * 0.1
+    st = torch.randn(B, D, 4, device=DEV) if with_state else None
+    xz = torch.randn(B, L, 2 * D, device=DEV).to(dtype)
+    go = torch.randn(B, L, D, device=DEV).to(dtype)
+
+    def poisoned(t, fill):
+        bt = torch.full((t.shape[0], L + 2 * pad, t.shape[2]), fill, device=DEV, dtype=t.dtype)
+        bt[:, pad:pad + L] = t
+        return bt
+
+    xzb, gob = poisoned(xz, nan), poisoned(go, nan)
+    ob = torch.full((B, L + 2 * pad, D), 7.0, device=DEV, dtype=dtype)
+    dxb = torch.full((B, L + 2 * pad, 2 * D), 7.0, device=DEV, dtype=dtype)
+    with _lib.override(conv_untiled=untiled):
+        ref, _ = ops.conv_fwd(xz[..., :D], w, b, True, state_in=st, want_state=True)
+        dref = torch.zeros_like(xz)
+        _, dwr, dbr = ops.conv_bwd(xz[..., :D], w, b, go, True, dx=dref[..., :D], state_in=st)
+        out, _ = ops.conv_fwd(xzb[:, pad:pad + L, :D], w, b, True, state_in=st, want_state=True,
+                              out=ob[:, pad:pad + L])
+        _, dw, db = ops.conv_bwd(xzb[:, pad:pad + L, :D], w, b, gob[:, pad:pad + L], True,
+                                 dx=dxb[:, pad:pad + L, :D], state_in=st)
+    assert torch.isfinite(out).all() and torch.isfinite(dw).all() and torch.isfinite(db).all()
+    assert torch.equal(out, ref)
+    assert torch.equal(dxb[:, pad:pad + L, :D], dref[..., :D])
+    assert torch.equal(dw, dwr) and torch.equal(db, dbr)
+    assert (ob[:, :pad] == 7.0).all() and (ob[:, pad + L:] == 7.0).all(), "a conv store landed outside [0, L)"
+    assert (dxb[:, :pad] == 7.0).all() and (dxb[:, pad + L:] == 7.0).all(), "a dx store landed outside [0, L)"
+    assert (dxb[..., D:] == 7.0).all(), "dx wrote outside its half"
+
+
 def test_state_update_vs_golden(golden):
     from mtts import ops
     g = golden("state_update.npz")

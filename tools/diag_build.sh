@@ -2,8 +2,11 @@
 # Timing-only variants of libmtts.so (one source rebuilt with diag macros):
 #   tools/diag_build.sh NAME "-DFLAG ..." [source.hip, default scan.hip]
 #     ->  mamba-tts-project_amd/mtts/libmtts_NAME.so
-# Use with MTTS_LIB=<path> (mtts/_lib.py) or tools/gemm_diag.py.  Outputs of
-# these builds are wrong by design.
+# Use with MTTS_LIB=<path> (mtts/_lib.py), e.g. from tools/scan_lib_ab.py or
+# tools/bench_mgemm.py.  Outputs of these builds are wrong by design.  Macros:
+#   scan.hip: MTTS_DIAG_{NOMEM,NOCOMPUTE,NOSCALAR,NODPP,NOEXP}, MTTS_C1_DIAG_{NODMA,NOSTORE},
+#             MTTS_FWD_NB=<tile buffers>
+#   gemm.hip: MTTS_GEMM_DIAG_{NODMA,NOREAD,NOBAR,FIXK,SAMETILE}
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 CS=$R/mamba-tts-project_amd/mtts/csrc
