@@ -93,6 +93,7 @@ def train_bench(args, rank, world, dev):
     import mamba_decoder
     from mtts.optim import FusedClipAdam
     from mtts.loss import cross_entropy
+    from mtts import wgrad
     c = dict(C2)
     torch.manual_seed(0)
     model = mamba_decoder.MambaTTSDecoder(c["vocab"], d_model=c["d_model"], n_layers=c["n_layers"],
@@ -114,7 +115,8 @@ def train_bench(args, rank, world, dev):
             dp.zero_grad()         # grads are views into the flat all-reduce buffer
         else:
             opt.zero_grad(set_to_none=True)
-        loss.backward()
+        with wgrad.deferred():     # projection weight gradients grouped per layer (mtts/wgrad.py)
+            loss.backward()
         if dp is not None:
             dp.finish()
         opt.step()

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 8
+#define MTTS_ABI_VERSION 9
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -264,8 +264,13 @@ int mtts_layernorm_fwd(const MttsLNArgs* a, void* stream);
 int mtts_layernorm_rows_packed(const MttsLNArgs* a, void* y_packed, void* stream);
 
 /* Backward: dy (M, N) -> dx (M, N) [+= dx_acc if given: dx = dx_acc + LN'],
- * dw, db (N) fp32, dgamma/dbeta (G, N) fp32 (when gamma).  Uses the saved
- * mean/rstd and the normalised input (x, or x_sum when res was fused). */
+ * dw, db (N) fp32, dgamma/dbeta (G, N) fp32 (when gamma; row stride dgb_rs,
+ * 0 = N, so both can live in one (G, 2N) gamma|beta gradient).  Uses the
+ * saved mean/rstd and the normalised input (x, or x_sum when res was fused).
+ * dx_colsum (optional, N fp32): the column sums of dx over all M rows, as
+ * stored (dtype-rounded) -- the bias gradient of the linear layer whose
+ * output is this LayerNorm's input (mamba_decoder.py:77/:88 out_proj / ff[2]
+ * bias), so that layer needs no column-sum launch of its own. */
 typedef struct {
   MttsLNArgs f;
   const void* dy;   int64_t dy_rs;
@@ -276,6 +281,8 @@ typedef struct {
   float* dgamma;
   float* dbeta;
   void* workspace;  /* mtts_layernorm_bwd_workspace() bytes */
+  float* dx_colsum; /* optional (ABI 9) */
+  int64_t dgb_rs;   /* row stride of dgamma / dbeta (ABI 9; 0 = cols) */
 } MttsLNBwdArgs;
 
 int64_t mtts_layernorm_bwd_workspace(int rows, int cols, int rows_per_group);
@@ -597,6 +604,15 @@ typedef struct {
 
 int64_t mtts_gemm_workspace(const MttsGemmArgs* a);
 int mtts_gemm(const MttsGemmArgs* a, void* stream);
+
+/* Grouped weight gradients (ABI 9): `n` (1..16) TN problems, each C_i =
+ * A_i^T B_i (+ C_i when beta_i = 1) with fp32 out, no epilogue, no split-K,
+ * in ONE launch; every output tile reduces its problem's whole K in one
+ * workgroup (no partial slabs, no reduce pass).  Put the longest-K problems
+ * first.  The deferred weight-gradient engine (mtts/wgrad.py) gathers a decoder
+ * layer's projection weight gradients (mamba_decoder.py:29-43 in/out_proj,
+ * MHA q/kv/out, FFN) into one such launch. */
+int mtts_gemm_grouped(const MttsGemmArgs* probs, int n, void* stream);
 
 /* ------------------------------------------------------------------------
  * Skinny bf16 GEMMs of the Mamba mixer's inner projections (csrc/skinny.hip).

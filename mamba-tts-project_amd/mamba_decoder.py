@@ -28,14 +28,15 @@ import torch.nn.functional as F
 from mtts.mamba import Mamba
 from mtts.attention import CrossAttention
 from mtts import ops
-from mtts.linear import cast_scope, ffn, linear
+from mtts.linear import BiasGradSlot, cast_scope, ffn, linear
 from mtts.decode import DecodeEngine
 from mtts.embed import embed_sum
 
 
 class StyleMLPAll(torch.autograd.Function):
     """All layers' FiLM conditioning tanh(z W_l^T + b_l) at once (reference
-    mamba_decoder.py:52-55, 82-84): forward one baddbmm + tanh + cast; the
+    mamba_decoder.py:52-55, 82-84): forward one baddbmm + tanh (fp32 outputs:
+    the FiLM LayerNorm kernel reads them as they are, no cast); the
     backward takes the n_layers gamma|beta gradients together (one stack),
     one tanh-backward, one bmm for the weight gradients, one sum for the
     biases and one for z -- instead of ~8 small launches per layer (and no
@@ -48,8 +49,7 @@ class StyleMLPAll(torch.autograd.Function):
         b = torch.stack(bs)                                               # (L, 2d)
         gb = torch.tanh(torch.baddbmm(b[:, None, :], z[None].expand(len(ws), -1, -1), W.transpose(1, 2)))
         ctx.save_for_backward(z, W, gb)
-        out = gb.to(cd)
-        return tuple(out[i] for i in range(len(ws)))
+        return tuple(gb[i] for i in range(len(ws)))
 
     @staticmethod
     def backward(ctx, *grads):
@@ -89,19 +89,26 @@ class MambaTTSDecoderLayer(nn.Module):
 
     def forward(self, x, text_hidden, z_style, text_mask=None, mamba_state=None):
         with cast_scope():
-            x, ff_out, new_state = self.forward_fused(x, None, text_hidden, z_style, text_mask, mamba_state)
+            x, ff_out, new_state = self.forward_fused(x, None, text_hidden, z_style, text_mask, mamba_state,
+                                                      ff_slot=False)
         return x + ff_out, new_state                                          # :88-89
 
-    def forward_fused(self, x, pending, text_hidden, z_style, text_mask=None, mamba_state=None, kpm=None, gb=None):
+    def forward_fused(self, x, pending, text_hidden, z_style, text_mask=None, mamba_state=None, kpm=None, gb=None,
+                      ff_slot=True):
         """Same math as forward(); the input residual `x + pending` and the
         output residual `x + ff_out` are left to the neighbouring fused
         residual+LayerNorm kernels.  `gb` (B, 2d): this layer's
         style_mlp(z_style) when the decoder computed all layers' at once.
+        Bias gradients of out_proj (:77) and ff[2] (:88) come from the fused
+        residual+LayerNorm backward that consumes those outputs (BiasGradSlot;
+        `ff_slot`: ff_out feeds only the next fused LayerNorm, which reads the
+        slot attached to it as `_mtts_dbias_slot`).
         Returns (x, ff_out, new_state)."""
         T = x.shape[1]
         # 1) (x += pending) ; h = norm_mamba(x) ; Mamba   (mamba_decoder.py:59-64)
         h, xs = ops.layer_norm(x if pending is None else pending, self.norm_mamba.weight, self.norm_mamba.bias,
-                               self.norm_mamba.eps, res=None if pending is None else x)
+                               self.norm_mamba.eps, res=None if pending is None else x,
+                               colsum_slot=getattr(pending, "_mtts_dbias_slot", None))
         if pending is not None:
             x = xs
         h_mamba, new_state = self.mamba(h, mamba_state)
@@ -111,17 +118,21 @@ class MambaTTSDecoderLayer(nn.Module):
         key_padding_mask = kpm                     # precomputed once per decoder forward
         if key_padding_mask is None and text_mask is not None:
             key_padding_mask = ~text_mask                                   # :68-70 (sic)
+        attn_slot = BiasGradSlot()
         attn_out, _ = self.cross_attn(query=h, key=text_hidden, value=text_hidden,
-                                      key_padding_mask=key_padding_mask)
+                                      key_padding_mask=key_padding_mask, _dbias_slot=attn_slot)
 
-        # 3) x = x + attn ; h = gamma * norm_ff(x) + beta   (fused, :78-86)
+        # 3) x = x + attn ; h = gamma * norm_ff(x) + beta   (fused, :78-86);
+        # gamma | beta as ONE fp32 (B, 2d) tensor (its gradient written in place)
         if gb is None:
             gb = self.style_mlp(z_style.to(self.style_mlp[0].weight.dtype))
-        gamma, beta = torch.chunk(gb.to(h.dtype), 2, dim=-1)
         h, x = ops.layer_norm(attn_out, self.norm_ff.weight, self.norm_ff.bias, self.norm_ff.eps, res=x,
-                              gamma=gamma, beta=beta, rows_per_group=T)
+                              rows_per_group=T, film=gb, colsum_slot=attn_slot)
         f0, f2 = self.ff[0], self.ff[2]
-        ff_out = ffn(h, f0.weight, f0.bias, f2.weight, f2.bias)             # :88 (gelu(ff0) -> ff2)
+        slot = BiasGradSlot() if ff_slot else None
+        ff_out = ffn(h, f0.weight, f0.bias, f2.weight, f2.bias, dbias_slot=slot)   # :88 (gelu(ff0) -> ff2)
+        if slot is not None:
+            ff_out._mtts_dbias_slot = slot
         return x, ff_out, new_state
 
 
@@ -187,7 +198,8 @@ class MambaTTSDecoder(nn.Module):
     def _tail(self, x, pending=None):
         """norm_out(x [+ pending]) -> head (mamba_decoder.py:184-185)."""
         h, _ = ops.layer_norm(x if pending is None else pending, self.norm_out.weight, self.norm_out.bias,
-                              self.norm_out.eps, res=None if pending is None else x)
+                              self.norm_out.eps, res=None if pending is None else x,
+                              colsum_slot=getattr(pending, "_mtts_dbias_slot", None))
         return linear(h, self.head.weight, self.head.bias)
 
     def _gemm_weights(self):
@@ -202,7 +214,7 @@ class MambaTTSDecoder(nn.Module):
     def _style_all(self, z_style, cd):
         """Every layer's style_mlp(z_style) = tanh(z W_l^T + b_l) (:52-55, applied
         at :82-84) in ONE batched GEMM over the stacked layer weights (fp32, the
-        parameters' dtype), cast to the compute dtype once (StyleMLPAll).
+        parameters' dtype, kept fp32 for the FiLM LayerNorm kernel: StyleMLPAll).
         Returns n_layers (B, 2d) tensors, or None when the layers' style MLPs
         differ in shape / dtype."""
         lins = [l.style_mlp[0] for l in self.layers]

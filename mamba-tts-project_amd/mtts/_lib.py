@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -105,7 +105,7 @@ class LNArgs(C.Structure):
 class LNBwdArgs(C.Structure):
     _fields_ = [("f", LNArgs), ("dy", vp), ("dy_rs", i64), ("dx_acc", vp), ("dxacc_rs", i64),
                 ("dx", vp), ("dx_rs", i64), ("dw", vp), ("db", vp), ("dgamma", vp), ("dbeta", vp),
-                ("workspace", vp)]
+                ("workspace", vp), ("dx_colsum", vp), ("dgb_rs", i64)]
 
 
 class AttnFwdArgs(C.Structure):
@@ -155,6 +155,7 @@ _SIGS = {
     "mtts_pack_rows_weight": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_gemm_workspace": ([C.POINTER(GemmArgs)], i64),
     "mtts_gemm": ([C.POINTER(GemmArgs), vp], i32),
+    "mtts_gemm_grouped": ([C.POINTER(GemmArgs), i32, vp], i32),
     "mtts_gemm_skinny": ([C.POINTER(SkinnyArgs), vp], i32),
     "mtts_gemm_skinny_workspace": ([C.POINTER(SkinnyArgs)], i64),
     "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),

@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import attn_kernels
+from . import wgrad as WG
 from .linear import _want_t, cast_scope, cast_weight, cast_weight_t, colsum, linear, proj, wgrad
 
 
@@ -55,7 +56,8 @@ class InProjFn(torch.autograd.Function):
             dquery = (dq2 @ Wc[:d]).view(qshape) if ctx.needs_input_grad[0] else None
             dkey = (dkv2 @ Wc[d:]).view(kshape) if ctx.needs_input_grad[1] else None
         dW = db = None
-        if ctx.needs_input_grad[2]:
+        if ctx.needs_input_grad[2] and not WG.submit([(dq2, x2, ctx.weight, (0, d)),
+                                                      (dkv2, k2, ctx.weight, (d, 3 * d))]):
             dW = torch.empty(3 * d, d, device=x2.device, dtype=torch.float32)
             wgrad(dq2, x2, out=dW[:d])
             wgrad(dkv2, k2, out=dW[d:])
@@ -87,11 +89,14 @@ class CrossAttention(nn.Module):
         nn.init.constant_(self.in_proj_bias, 0.0)
         nn.init.constant_(self.out_proj.bias, 0.0)
 
-    def forward(self, query, key, value, key_padding_mask=None, need_weights=False):
+    def forward(self, query, key, value, key_padding_mask=None, need_weights=False, _dbias_slot=None):
+        """`_dbias_slot` (internal, linear.BiasGradSlot): out_proj's bias
+        gradient is delivered by the consumer of the output (the decoder
+        layer's fused residual + LayerNorm backward)."""
         with cast_scope():
-            return self._forward(query, key, value, key_padding_mask)
+            return self._forward(query, key, value, key_padding_mask, _dbias_slot)
 
-    def _forward(self, query, key, value, key_padding_mask):
+    def _forward(self, query, key, value, key_padding_mask, dbias_slot=None):
         cd = query.dtype
         d, H = self.embed_dim, self.num_heads
         W, b = self.in_proj_weight, self.in_proj_bias
@@ -106,7 +111,7 @@ class CrossAttention(nn.Module):
             k = linear(key.to(cd), W, b, rows=(d, 2 * d))
             v = linear(value.to(cd), W, b, rows=(2 * d, 3 * d))
             o = attn_kernels.attention(q, k, v, H, key_padding_mask, p_drop)
-        out = linear(o, self.out_proj.weight, self.out_proj.bias)
+        out = linear(o, self.out_proj.weight, self.out_proj.bias, dbias_slot=dbias_slot)
         return out, None
 
     def _single_key(self, query, key, value):

@@ -39,6 +39,7 @@
 
 namespace {
 using mtts::bf16_t;
+using mtts::block_sync;
 using mtts::kLn2;
 using mtts::kLog2e;
 
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(MttsAttnFwdArgs a) {
   for (int dt = 0; dt < ND; ++dt) O[dt] = f32x16{};
 
   for (int k0 = 0; k0 < a.kv_len; k0 += kKB) {
-    __syncthreads();
+    block_sync();
     for (int i = tid; i < kKB * HD / CH; i += nthr) {
       const int row = i / (HD / CH), cc = (i % (HD / CH)) * CH;
       const int key = k0 + row;
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(MttsAttnFwdArgs a) {
         sMask[1] = (uint32_t)(bal >> 32);
       }
     }
-    __syncthreads();
+    block_sync();
 #pragma unroll
     for (int t = 0; t < kKB / 32; ++t) {
       if (k0 + t * 32 >= a.kv_len) break;
@@ -285,21 +286,22 @@ constexpr float kDeferMax = 8.f;
 // more than kDeferMax, so in the steady state the O accumulators are not
 // touched by VALU (P <= 2^8 before its bf16 rounding; lse = m + log l holds
 // for any m).
-// max of 16 MFMA scores as 8 v_max3_f32 (inline asm: fmaxf on values the
-// compiler cannot prove canonical gets a v_max x, x quieting pass per operand)
-__device__ __forceinline__ float max3_raw(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+// max of 16 MFMA scores as 8 v_maximum3_f32: __builtin_elementwise_maximum
+// (IEEE maximum, NaN-propagating) needs no quieting pass on MFMA results the
+// compiler cannot prove canonical (fmaxf got a v_max x, x per operand), and,
+// unlike the round-4 inline-asm v_max3_f32, leaves the MFMA -> VALU and
+// VALU -> v_permlane32_swap wait states to the compiler: the asm form read
+// stale S / t now and then (attention outputs varied by a bf16 ulp from run
+// to run, tools/dbg/race_probe.py, round 5)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 __device__ __forceinline__ float max16_xor32(const f32x16& S) {
-  float t = max3_raw(S[0], S[1], S[2]);
+  float t = max3f(S[0], S[1], S[2]);
 #pragma unroll
-  for (int i = 3; i < 16; i += 2) t = max3_raw(t, S[i], S[i + 1 < 16 ? i + 1 : i]);
+  for (int i = 3; i < 16; i += 2) t = max3f(t, S[i], S[i + 1 < 16 ? i + 1 : i]);
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
-  float m2;
-  asm("v_max_f32 %0, %1, %2" : "=v"(m2) : "v"(__uint_as_float(r[0])), "v"(__uint_as_float(r[1])));
-  return m2;
+  return __builtin_elementwise_maximum(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
 template <int ND>
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(256, 4) void attn_fwd_db_kernel(MttsAttnFwdArgs a) 
     fetch(0);
     put(0);
   }
-  __syncthreads();
+  block_sync();
   for (int j = 0; j < nblk; ++j) {
     const int buf = j & 1, k0 = j * kKB;
     fetch(min(k0 + kKB, (nblk - 1) * kKB));   // in flight under this block's math
@@ -504,7 +506,7 @@ __global__ __launch_bounds__(256, 4) void attn_fwd_db_kernel(MttsAttnFwdArgs a) 
       }
     }
     if (j + 1 < nblk) put(buf ^ 1);
-    __syncthreads();
+    block_sync();
   }
 
 #pragma unroll
@@ -591,7 +593,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_short_kernel(MttsAttnFwdArgs 
       sMask[2 * wave + 1] = (uint32_t)(bal >> 32);
     }
   }
-  __syncthreads();
+  block_sync();
 
   for (int sl = 0; sl < nsl; ++sl) {
     if (sl + 1 < nsl) load_q(sl + 1, QN);   // in flight under this slice
@@ -711,7 +713,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
 
   for (int kg = MODE == kBwdKV ? kv_kg : 0; kg < (MODE == kBwdKV ? kv_kg + 1 : nkg); ++kg) {
     const int kg0 = kg * KG;
-    __syncthreads();
+    block_sync();
     {
       const T* kb = (const T*)f.k + b * f.k_bs + hh * HD;
       const T* vb = (const T*)f.v + b * f.v_bs + hh * HD;
@@ -770,7 +772,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
     };
     if (MODE != kBwdQ || kg == 0) load_slice(qbeg);
     for (int q0 = qbeg; q0 < qend; q0 += 32) {
-      __syncthreads();
+      block_sync();
       // ---- stage Q, dO images; delta = rowsum(dO * O); -lse/scale
       // (mode 2: its single slice once, kept across key groups)
       if (MODE != kBwdQ || kg == 0) {
@@ -806,7 +808,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
         if (tid < 32) sL[tid] = q0 + tid < qend ? -plse * inv_scale : 0.f;  // P = exp2(c (S + L))
         if (MODE != kBwdQ && q0 + 32 < qend) load_slice(q0 + 32);   // next slice, in flight under this one
       }
-      __syncthreads();
+      block_sync();
       // ---- S = Q K^T - lse/scale and dP = dO V^T - delta (key on the lane)
       f32x16 S, D;
 #pragma unroll
@@ -886,7 +888,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
               f32x4{D[4 * g4], D[4 * g4 + 1], D[4 * g4 + 2], D[4 * g4 + 3]};
       }
       if constexpr (MODE == kBwdKV) continue;   // dQ comes from the mode-2 launch
-      __syncthreads();
+      block_sync();
       // ---- dQ[q][dims of tile dt] = scale * dS K over the group's keys
       for (int dt = wave; dt < ND; dt += NW) {
         f32x16 Q = MODE == kBwdQ ? QA[(dt - wave) / NW] : f32x16{};
@@ -1105,7 +1107,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
     fetch(0);
     put(0);
   }
-  __syncthreads();
+  block_sync();
   // hd 128: the next block's 32 staging registers do not fit beside Q / dO /
   // dQ (256 VGPRs); it is loaded after this block's math instead
   constexpr bool kPrefetch = HD == 64;
@@ -1149,7 +1151,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
       if constexpr (!kPrefetch) fetch(k0 + KB);
       put(buf ^ 1);
     }
-    __syncthreads();
+    block_sync();
   }
   // ---- dQ^T tile dt: lane = query, registers = dims dt*32 + acc_row(i, h)
   if (qv) {
@@ -1298,7 +1300,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
     put(S0_{}, 0);
     fetch(S1_{}, min(qbeg + QS, qlast));
   }
-  __syncthreads();
+  block_sync();
   // slice j (LDS buffer j & 1); register set j & 1 is free (its slice went to
   // LDS at the end of iteration j-1) and takes slice j+2, set (j+1) & 1
   // holds slice j+1
@@ -1335,7 +1337,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
       }
     }
     if (j + 1 < nsl) put(std::integral_constant<int, par ^ 1>{}, par ^ 1);
-    __syncthreads();
+    block_sync();
   };
   for (int j = 0; j < nsl; j += 2) {
     slice(S0_{}, j);
@@ -1497,7 +1499,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(MttsAttnFwdArgs a) {
   if (gl == 0) sm[g] = m, sl[g] = l;
 #pragma unroll
   for (int e = 0; e < 8; ++e) sacc[g][d0 + e] = acc[e];
-  __syncthreads();
+  block_sync();
   if (threadIdx.x < HD) {
     float M = -INFINITY;
     for (int i = 0; i < NG; ++i) M = fmaxf(M, sm[i]);
@@ -1587,7 +1589,7 @@ __global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
   }
   m = groups_max<G>(m, lane);
   if ((threadIdx.x & 63) == 0) swm[wave] = m;
-  __syncthreads();
+  block_sync();
   const float M = fmaxf(fmaxf(swm[0], swm[1]), fmaxf(swm[2], swm[3]));
   float l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1605,7 +1607,7 @@ __global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
     for (int e = 0; e < 8; ++e) sacc[wave][d0 + e] = acc[e];
     if (gl == 0) swl[wave] = l;
   }
-  __syncthreads();
+  block_sync();
   if (threadIdx.x < HD) {
     const float L = (swl[0] + swl[1]) + (swl[2] + swl[3]);
     const float o = (sacc[0][threadIdx.x] + sacc[1][threadIdx.x]) + (sacc[2][threadIdx.x] + sacc[3][threadIdx.x]);

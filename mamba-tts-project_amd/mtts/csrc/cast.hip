@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void cast_multi_kernel(const MttsCastDesc* __r
       tile[r][cq] = v.x; tile[r][cq + 1] = v.y; tile[r][cq + 2] = v.z; tile[r][cq + 3] = v.w;
     }
     if (!dstT) return;
-    __syncthreads();
+    block_sync();
     const int rq = (tid % 16) * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void cast_multi_kernel(const MttsCastDesc* __r
       }
     }
     if (!dstT) return;
-    __syncthreads();
+    block_sync();
     for (int i = 0; i < 16; ++i) {
       const int c = i * 4 + tid / 64, r = tid % 64;
       if (r0 + r < d.rows && c0 + c < d.cols) dstT[(int64_t)(c0 + c) * d.rows + r0 + r] = f2bf(tile[r][c]);

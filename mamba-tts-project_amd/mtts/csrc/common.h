@@ -23,7 +23,7 @@ struct ColsumJob {
   int nparts, ppg;
   int64_t out_gstride;
 };
-// up to 4 colsum jobs over slabs of one width and part stride, one launch
+// up to 5 colsum jobs over slabs of one width and part stride, one launch
 void colsum_multi(const ColsumJob* jobs, int n, int ncols, int64_t pstride, hipStream_t st);
 
 #define MTTS_CHECK(cond, ...)                                                 \
@@ -100,6 +100,23 @@ __device__ __forceinline__ float softplus_grad(float x) {
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return fast_rcp(1.f + __builtin_amdgcn_exp2f(-x * kLog2e)); }
 __device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
+
+// ---------------------------------------------------------------- workgroup barrier
+// Every workgroup barrier of the library: this wave's own LDS operations
+// complete (lgkmcnt(0)), THEN s_barrier.  hipcc's __syncthreads() alone is a
+// bare s_barrier on gfx950 (LLVM assumes every wave observes LDS operations in
+// one global order and drops the wait), but a ds_write issued before it is
+// not always visible to another wave's ds_read issued after it:
+// tools/ubench/lds_order_probe.hip counted 836,032 stale neighbour-wave
+// reads in 2.6e9 with the bare barrier and 0 with the wait
+// (profiles/r05_lds_order_probe.txt), and the scan backward's carry kernel
+// drifted from run to run under GPU sharing (tools/dbg/race_probe.py).
+// vmcnt / expcnt are left alone (in-flight LDS-DMA keeps its own counted
+// waits).
+__device__ __forceinline__ void block_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0); vmcnt(63), expcnt(7): no wait
+  __syncthreads();
+}
 
 // ---------------------------------------------------------------- cross-lane
 // DPP quad_perm controls

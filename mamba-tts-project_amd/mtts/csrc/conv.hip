@@ -437,7 +437,7 @@ __global__ __launch_bounds__(512) void conv_bwd_tile_kernel(const MttsConvBwdArg
       red[wave - 1][q * (kK + 1) + kK][lane] = db[q];
     }
   }
-  __syncthreads();
+  block_sync();
   if (wave == 0 && cok) {
     float* pp = part + ((int64_t)(b * gridDim.y + blockIdx.y) * f.dim + c0) * (kK + 1);
 #pragma unroll

@@ -640,14 +640,26 @@ __device__ __forceinline__ void store_tile_buf(const GemmParams& p, f32x4 (&acc)
   if constexpr (OUT_F32) {
     const __amdgpu_buffer_rsrc_t r = brsrc((const float*)p.c + (int64_t)split * p.split_stride,
                                            (uint32_t)((int64_t)p.m * p.ldc * 4));
+    const bool acc_old = p.beta != 0.f;   // uniform: C = beta C + A B (splits == 1 only)
 #pragma unroll
     for (int MB = 0; MB < 8; ++MB) {
       const int row = m0 + wr * 128 + MB * 16 + rl;
+      f32x4 old[4];
+      if (acc_old) {
+#pragma unroll
+        for (int NB = 0; NB < 4; ++NB) {
+          const int col = n0 + wc * 64 + NB * 16 + cl;
+          const uint32_t off = (row < p.m && col < p.n) ? (uint32_t)((row * p.ldc + col) * 4) : kOOB;
+          old[NB] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+        }
+      }
 #pragma unroll
       for (int NB = 0; NB < 4; ++NB) {
         const int col = n0 + wc * 64 + NB * 16 + cl;
         const uint32_t off = (row < p.m && col < p.n) ? (uint32_t)((row * p.ldc + col) * 4) : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[MB][NB]), r, off, 0, 0);
+        f32x4 v = acc[MB][NB];
+        if (acc_old) v += p.beta * old[NB];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, off, 0, 0);
       }
     }
   } else {
@@ -775,17 +787,20 @@ struct PLoader {
   }
 };
 
-template <bool AK, bool BKM, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char lds[kLds];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-
-  // XCD-aware work order: the ids one XCD holds at a time are consecutive
+// XCD-aware work order: the ids one XCD holds at a time are consecutive
+__device__ __forceinline__ int xcd_work_id() {
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+}
+
+// the ping-pong tile of work item `wid` of problem `p` (the kernels below)
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__device__ __forceinline__ void gemm_pp_body(const GemmParams& p, const int wid) {
+  __shared__ __attribute__((aligned(16))) char lds[kLds];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
   const int nk = p.k / kBK;
   const int G = nk;                                                  // K-tiles of the item
 
@@ -910,6 +925,38 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
   store_tile_buf<EPI, OUT_F32>(p, acc, bias, cur.m0, cur.n0, wr, wc, lane, cur.split);
 }
 
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
+  gemm_pp_body<AK, BKM, EPI, OUT_F32>(p, xcd_work_id());
+}
+
+// Grouped weight gradients (round 5): up to kGroupMax TN problems in ONE
+// launch, each tile over the problem's WHOLE K (no split-K slabs, no
+// split_reduce pass).  The host orders the problems longest-K first; tiles of
+// a problem are consecutive work ids (an XCD walks one problem's tiles).
+constexpr int kGroupMax = 16;
+struct GroupParams {
+  GemmParams p[kGroupMax];
+  int tile_end[kGroupMax];   // exclusive prefix sums of the problems' tile counts
+  int n;
+};
+
+template <bool AK, bool BKM, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(kThreads, 1) void gemm_pp_grouped_kernel(const GroupParams G) {
+  const int wid = xcd_work_id();
+  int i = 0, t0 = 0;
+#pragma unroll
+  for (int j = 0; j + 1 < kGroupMax; ++j)
+    if (j + 1 < G.n && wid >= G.tile_end[j]) { i = j + 1; t0 = G.tile_end[j]; }
+  // static indices only (a dynamic index into the kernel-argument struct
+  // would copy it to scratch)
+  GemmParams q = G.p[0];
+#pragma unroll
+  for (int j = 1; j < kGroupMax; ++j)
+    if (i == j) q = G.p[j];
+  gemm_pp_body<AK, BKM, EPI, OUT_F32>(q, wid - t0);
+}
+
 // out[i] = beta*out[i] + sum_s slab[s][i] (fixed order); rows x cols with row strides
 __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ slabs, int64_t sstride, int splits,
                                                            int rows, int cols, int64_t lds_, float* out, int64_t ldo,
@@ -1031,5 +1078,41 @@ extern "C" int mtts_gemm(const MttsGemmArgs* a, void* stream) {
                        (int64_t)M * N, splits, M, N, (int64_t)N, (float*)a->c, a->ldc, a->beta);
     MTTS_LAUNCH_CHECK("gemm split reduce");
   }
+  return MTTS_OK;
+}
+
+extern "C" int mtts_gemm_grouped(const MttsGemmArgs* probs, int n, void* stream) {
+  using namespace mtts;
+  MTTS_CHECK(probs && n >= 1 && n <= kGroupMax, "gemm_grouped: 1 <= n <= %d problems", kGroupMax);
+  GroupParams G{};
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const MttsGemmArgs* a = probs + i;
+    MTTS_CHECK(a->a && a->b && a->c, "gemm_grouped[%d]: null pointer", i);
+    const int M = a->m, N = a->n, K = a->k;
+    MTTS_CHECK(a->layout == MTTS_GEMM_TN && a->out_dtype == 0 && a->epilogue == 0 && a->splits <= 1,
+               "gemm_grouped[%d]: TN, fp32 out, no epilogue, no split-K only", i);
+    MTTS_CHECK(M > 0 && N > 0 && K > 0 && K % kBK == 0, "gemm_grouped[%d]: m=%d n=%d k=%d (k %% 64 == 0)", i, M, N, K);
+    MTTS_CHECK(N % 8 == 0 && M % 8 == 0, "gemm_grouped[%d]: m, n must be multiples of 8", i);
+    MTTS_CHECK(((uintptr_t)a->a | (uintptr_t)a->b) % 16 == 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
+               a->lda >= M && a->ldb >= N, "gemm_grouped[%d]: A / B alignment or leading dimension", i);
+    MTTS_CHECK(a->ldc % 4 == 0 && (uintptr_t)a->c % 16 == 0 && a->ldc >= N, "gemm_grouped[%d]: C alignment / ldc", i);
+    MTTS_CHECK(a->beta == 0.f || a->beta == 1.f, "gemm_grouped[%d]: beta must be 0 or 1", i);
+    MTTS_CHECK((int64_t)(kBK - 1) * a->lda + M < (1ll << 31) && (int64_t)(kBK - 1) * a->ldb + N < (1ll << 31) &&
+               (int64_t)M * a->ldc * 4 < (1ll << 31), "gemm_grouped[%d]: operand / C span exceeds the 32-bit offsets", i);
+    GemmParams& p = G.p[i];
+    p.a = (const bf16_t*)a->a; p.b = (const bf16_t*)a->b; p.c = a->c;
+    p.lda = a->lda; p.ldb = a->ldb; p.ldc = a->ldc;
+    p.m = M; p.n = N; p.k = K;
+    p.tiles_m = (M + kTile - 1) / kTile; p.tiles_n = (N + kTile - 1) / kTile;
+    p.splits = 1; p.split_stride = 0; p.beta = a->beta;
+    p.group = std::min(p.tiles_m, 4);
+    tiles += p.tiles_m * p.tiles_n;
+    G.tile_end[i] = tiles;
+  }
+  G.n = n;
+  hipLaunchKernelGGL((gemm_pp_grouped_kernel<false, false, 0, true>), dim3(tiles), dim3(kThreads), 0,
+                     (hipStream_t)stream, G);
+  MTTS_LAUNCH_CHECK("gemm_grouped");
   return MTTS_OK;
 }

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
     sa = sum_xor32(sum_xor16(sa));
     sb = sum_xor32(sum_xor16(sb));
     if (g == 0) { psum[wave][r] = sa; psum[wave][16 + r] = sb; }
-    __syncthreads();
+    block_sync();
     float ma = 0.f, mb = 0.f;
     for (int w = 0; w < KS; ++w) { ma += psum[w][r]; mb += psum[w][16 + r]; }
     ma /= a.K;
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
     qa = sum_xor32(sum_xor16(qa));
     qb = sum_xor32(sum_xor16(qb));
     if (g == 0) { psq[wave][r] = qa; psq[wave][16 + r] = qb; }
-    __syncthreads();
+    block_sync();
     float va = 0.f, vb = 0.f;
     for (int w = 0; w < KS; ++w) { va += psq[w][r]; vb += psq[w][16 + r]; }
     const float ra = 1.f / sqrtf(va / a.K + a.ln_eps), rb = 1.f / sqrtf(vb / a.K + a.ln_eps);
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(64 * kMaxKS) void gemv16_kernel(const MttsRowsArgs 
   }
   red[wave][0][lane] = acc0;
   if (two) red[wave][1][lane] = acc1;
-  __syncthreads();
+  block_sync();
   if (!mok) return;
 
   // ---- fixed-order sum over the KS waves + epilogue

@@ -100,8 +100,9 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
   const int row0 = blockIdx.x * RB;
   const bool film = f.gamma != nullptr;
   const int grp = film ? row0 / f.rows_per_group : 0;
+  const bool csum = a.dx_colsum != nullptr;
   float wv[NV][VEC], bv[NV][VEC], gv[NV][VEC];
-  float pdw[NV][VEC], pdb[NV][VEC], pdg[NV][VEC], pdbe[NV][VEC];
+  float pdw[NV][VEC], pdb[NV][VEC], pdg[NV][VEC], pdbe[NV][VEC], pdx[NV][VEC];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c0 = (k * 64 + lane) * VEC;
@@ -111,7 +112,7 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < VEC; ++q) {
       if (!film) gv[k][q] = 1.f;
-      pdw[k][q] = pdb[k][q] = pdg[k][q] = pdbe[k][q] = 0.f;
+      pdw[k][q] = pdb[k][q] = pdg[k][q] = pdbe[k][q] = pdx[k][q] = 0.f;
     }
   }
   const T* xsrc = (const T*)((f.res && f.x_sum) ? f.x_sum : f.x);
@@ -176,29 +177,36 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
         for (int q = 0; q < VEC; ++q) o[q] += t[q];
       }
       st_vec<T, VEC>((T*)a.dx + (int64_t)row * a.dx_rs + c0, o);
+      if (csum) {   // column sums of dx as stored (the upstream linear's bias gradient)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) pdx[k][q] += sizeof(T) == 2 ? bf2f(f2bf(o[q])) : o[q];
+      }
     }
   }
   // block partials: reduce the waves through LDS, then one write per column
+  // slabs: 0 dw, 1 db, 2 dgamma, 3 dbeta (FiLM), 4 dx column sums (dx_colsum)
   extern __shared__ float sm[];  // [kLnBwdWaves][cols]
-  const int nk = film ? 4 : 2;
-  for (int which = 0; which < nk; ++which) {
+  for (int which = 0; which < 5; ++which) {
+    if ((which == 2 || which == 3) && !film) continue;   // block-uniform
+    if (which == 4 && !csum) continue;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c0 = (k * 64 + lane) * VEC;
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
-        const float val = which == 0 ? pdw[k][q] : which == 1 ? pdb[k][q] : which == 2 ? pdg[k][q] : pdbe[k][q];
+        const float val = which == 0 ? pdw[k][q] : which == 1 ? pdb[k][q] : which == 2 ? pdg[k][q]
+                        : which == 3 ? pdbe[k][q] : pdx[k][q];
         sm[wave * n + c0 + q] = val;
       }
     }
-    __syncthreads();
+    block_sync();
     for (int c = threadIdx.x; c < n; c += 64 * kLnBwdWaves) {
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < kLnBwdWaves; ++w) s += sm[w * n + c];
       part[((int64_t)which * gridDim.x + blockIdx.x) * n + c] = s;
     }
-    __syncthreads();
+    block_sync();
   }
 }
 
@@ -309,7 +317,7 @@ extern "C" int64_t mtts_layernorm_bwd_workspace(int rows, int cols, int rows_per
   t.rows_per_group = rows_per_group;
   const int rb = ln_rb(&t);
   const int64_t nblk = (rows + rb - 1) / rb;
-  return 4 * nblk * cols * 4 + 256;
+  return 5 * nblk * cols * 4 + 256;
 }
 
 extern "C" int mtts_layernorm_bwd(const MttsLNBwdArgs* a, void* stream) {
@@ -320,9 +328,11 @@ extern "C" int mtts_layernorm_bwd(const MttsLNBwdArgs* a, void* stream) {
   MTTS_CHECK(!a->f.gamma || (a->dgamma && a->dbeta), "layernorm_bwd: FiLM needs dgamma/dbeta");
   const MttsLNArgs& f = a->f;
   hipStream_t st = (hipStream_t)stream;
+  MTTS_CHECK(a->dgb_rs == 0 || a->dgb_rs >= f.cols, "layernorm_bwd: dgb_rs < cols");
   if (f.rows == 0) {
     (void)hipMemsetAsync(a->dw, 0, f.cols * 4, st);
     (void)hipMemsetAsync(a->db, 0, f.cols * 4, st);
+    if (a->dx_colsum) (void)hipMemsetAsync(a->dx_colsum, 0, f.cols * 4, st);
     return MTTS_OK;
   }
   const int rb = ln_rb(&f);
@@ -333,14 +343,15 @@ extern "C" int mtts_layernorm_bwd(const MttsLNBwdArgs* a, void* stream) {
   const int nblk = (f.rows + rb - 1) / rb;
   const int64_t slab = (int64_t)nblk * f.cols;
   // dw, db (and dgamma, dbeta per FiLM row group) in one launch
-  ColsumJob jobs[4] = {{part, a->dw, nblk, nblk, 0}, {part + slab, a->db, nblk, nblk, 0}};
+  ColsumJob jobs[5] = {{part, a->dw, nblk, nblk, 0}, {part + slab, a->db, nblk, nblk, 0}};
   int nj = 2;
   if (f.gamma) {
     const int bpg = f.rows_per_group / rb;
-    jobs[2] = {part + 2 * slab, a->dgamma, nblk, bpg, (int64_t)f.cols};
-    jobs[3] = {part + 3 * slab, a->dbeta, nblk, bpg, (int64_t)f.cols};
-    nj = 4;
+    const int64_t gs = a->dgb_rs > 0 ? a->dgb_rs : (int64_t)f.cols;
+    jobs[nj++] = {part + 2 * slab, a->dgamma, nblk, bpg, gs};
+    jobs[nj++] = {part + 3 * slab, a->dbeta, nblk, bpg, gs};
   }
+  if (a->dx_colsum) jobs[nj++] = {part + 4 * slab, a->dx_colsum, nblk, nblk, 0};
   colsum_multi(jobs, nj, f.cols, f.cols, st);
   MTTS_LAUNCH_CHECK("layernorm_bwd_reduce");
   return MTTS_OK;

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(kCeBlock) void ce_fwd_kernel(const T* __restrict__ 
     ws[threadIdx.x >> 6][0] = loss;
     ws[threadIdx.x >> 6][1] = cnt;
   }
-  __syncthreads();
+  block_sync();
   if (threadIdx.x == 0) {
     float a = 0.f, c = 0.f;
     for (int w = 0; w < kCeBlock / 64; ++w) { a += ws[w][0]; c += ws[w][1]; }
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kCeBlock) void ce_sum_kernel(const float* __restric
     ws[threadIdx.x >> 6][0] = a;
     ws[threadIdx.x >> 6][1] = c;
   }
-  __syncthreads();
+  block_sync();
   if (threadIdx.x == 0) {
     float sa = 0.f, sc = 0.f;
     for (int w = 0; w < kCeBlock / 64; ++w) { sa += ws[w][0]; sc += ws[w][1]; }

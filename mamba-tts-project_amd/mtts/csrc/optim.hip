@@ -36,7 +36,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
+  block_sync();
   float s = 0.f;
   if (threadIdx.x == 0) {
     for (int i = 0; i < kAdamBlock / 64; ++i) s += red[i];

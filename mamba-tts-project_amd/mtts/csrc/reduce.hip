@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ part,
   }
   float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   red[w][lane] = s;
-  __syncthreads();
+  block_sync();
   if (w == 0 && c < ncols) out[(int64_t)g * out_gstride + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
@@ -40,10 +40,10 @@ void colsum(const float* part, int nparts, int ppg, int64_t pstride, int ncols, 
                      pstride, ncols, out, out_gstride);
 }
 
-// Up to 4 column-sum jobs over slabs of the same width in ONE launch
-// (blockIdx.z = job): the LayerNorm backward's dw / db / dgamma / dbeta.
+// Up to 5 column-sum jobs over slabs of the same width in ONE launch
+// (blockIdx.z = job): the LayerNorm backward's dw / db / dgamma / dbeta / dx sums.
 struct ColsumJobs {
-  ColsumJob j[4];
+  ColsumJob j[5];
   int ncols;
   int64_t pstride;
 };
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const ColsumJobs J) {
   }
   const float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   red[w][lane] = s;
-  __syncthreads();
+  block_sync();
   if (w == 0 && c < J.ncols)
     jb.out[(int64_t)g * jb.out_gstride + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void colsum_rows_kernel(const T* __restrict__ 
   }
 #pragma unroll
   for (int e = 0; e < EPL; ++e) red[w][lane * EPL + e] = acc[e];
-  __syncthreads();
+  block_sync();
   for (int q = threadIdx.x; q < CB; q += 256) {
     const int cc = blockIdx.x * CB + q;
     if (cc < cols) part[(int64_t)blockIdx.y * cols + cc] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);

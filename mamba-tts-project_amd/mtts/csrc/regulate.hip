@@ -29,16 +29,16 @@ __device__ void dur_scan(const float* __restrict__ dur, int T, long long* ends, 
     ends[t] = s;
   }
   part[i] = s;
-  __syncthreads();
+  block_sync();
   for (int off = 1; off < kRegBlock; off <<= 1) {
     const long long v = i >= off ? part[i - off] : 0;
-    __syncthreads();
+    block_sync();
     part[i] += v;
-    __syncthreads();
+    block_sync();
   }
   const long long base = i > 0 ? part[i - 1] : 0;
   for (int t = t0; t < t1; ++t) ends[t] += base;
-  __syncthreads();
+  block_sync();
 }
 
 template <typename T, int EV>

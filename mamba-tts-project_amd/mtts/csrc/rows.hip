@@ -125,7 +125,7 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
         for (int q = 0; q < 8; ++q) sx += bf2f((bf16_t)xa[u][q]);
       sx += __shfl_xor(sx, 32);
       if (lane < 32) psum[wave][i] = sx;
-      __syncthreads();
+      block_sync();
       mean = 0.f;
 #pragma unroll
       for (int w = 0; w < KS; ++w) mean += psum[w][i];
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
         for (int q = 0; q < 8; ++q) { const float d = bf2f((bf16_t)xa[u][q]) - mean; sq = fmaf(d, d, sq); }
       sq += __shfl_xor(sq, 32);
       if (lane < 32) psq[wave][i] = sq;
-      __syncthreads();
+      block_sync();
       float var = 0.f;
 #pragma unroll
       for (int w = 0; w < KS; ++w) var += psq[w][i];
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
         for (int q = 0; q < 8; ++q) s1 += bf2f((bf16_t)v[q]);
       }
       psum[part][r] = s1;
-      __syncthreads();
+      block_sync();
       float t1 = 0.f;
       for (int w = 0; w < np; ++w) t1 += psum[w][r];
       const float mr = t1 / a.K;
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
         for (int q = 0; q < 8; ++q) { const float d = bf2f((bf16_t)v[q]) - mr; s2 = fmaf(d, d, s2); }
       }
       psq[part][r] = s2;
-      __syncthreads();
+      block_sync();
       float t2 = 0.f;
       mean = 0.f;
       for (int w = 0; w < np; ++w) { mean += psum[w][i]; t2 += psq[w][i]; }
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
   // acc register r: output row (batch) acc_row(r, h), column n0 + i
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[wave][acc_row(r, h)][i] = acc[r];
-  __syncthreads();
+  block_sync();
   float part[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -232,14 +232,14 @@ __global__ __launch_bounds__(64 * KS) void gemm_rows_kernel(const MttsRowsArgs a
         __hip_atomic_store(slab + kg * 1024 + threadIdx.x + e * 64 * KS, part[e], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      block_sync();
       if (threadIdx.x == 0) {
         const int old = __hip_atomic_fetch_add(a.splitk_count + tile, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == KG - 1;
         if (last) __hip_atomic_store(a.splitk_count + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = last;
       }
-      __syncthreads();
+      block_sync();
       if (!s_last) return;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // invalidates this CU's L1: other CUs' slabs
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

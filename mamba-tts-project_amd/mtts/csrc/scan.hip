@@ -446,7 +446,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_fwd_kernel(const MttsScanFwdAr
       constexpr int r = decltype(rc)::value;
       const int it = it0 + r;
       if (it < ntiles) {
-        __syncthreads();
+        block_sync();
         load_any(it + NR - 1, ring[(r + NR - 1) % NR]);
         const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
         if (it < nfull) compute_tile(FalseT{}, t0, it & 1, ring[r]);
@@ -939,7 +939,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_fwd_w2_kernel(const MttsScanFw
   int buf = 0, prev = NB - 1;
   for (int it = 0; it < ntiles; ++it) {
     const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
-    __syncthreads();  // tile it in LDS (every wave's DMA drained); outputs of tile it-1 complete
+    block_sync();  // tile it in LDS (every wave's DMA drained); outputs of tile it-1 complete
     if constexpr (MODE == kFull)
       if (it > 0) store_tile(t0 - TT, prev);        // read before this lane's DMA below refills the chunk
     const bool more = it + 1 < ntiles;
@@ -957,7 +957,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_fwd_w2_kernel(const MttsScanFw
     buf = buf + 1 == NB ? 0 : buf + 1;
   }
   if constexpr (MODE == kFull) {
-    __syncthreads();
+    block_sync();
     store_tile(t_begin + (ntiles - 1) * TT, prev);
     if (k == K - 1 && a.last_state && cvalid) {
       float hv[NS];
@@ -1175,7 +1175,7 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
     const int it = ntiles - 1 - q;
     const int t0 = __builtin_amdgcn_readfirstlane(t_begin + it * TT);
     const int buf = q & 1;
-    __syncthreads();
+    block_sync();
     if (it > 0) {
       if constexpr (WIDE) load_w(t0 - TT);
       else load(t0 - TT, nx, ng, nz);
@@ -1420,7 +1420,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
     float uu[kGB], xr[kGB], dt[kGB], zz[kGB], go[kGB], hs[kNSB];
     const int buf = WIDE ? (k & 1) : 0;
     if constexpr (WIDE) {
-      __syncthreads();  // staged inputs + B/C of this chunk visible
+      block_sync();  // staged inputs + B/C of this chunk visible
 #pragma unroll
       for (int g = 0; g < kGB; ++g) {
         const int sx = (g * kPB + j) * PIT + cl;
@@ -1461,7 +1461,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
       d4 = *reinterpret_cast<const f4*>(br + g * kPB);
       u4 = *reinterpret_cast<const f4*>(br + 16 * kBrP + g * kPB);
     };
-    if constexpr (!WIDE) __syncthreads();
+    if constexpr (!WIDE) block_sync();
 
     // ---- replay the chunk forward: h history in registers (state pairs, packed f32)
     f2 hh[kSub][2];
@@ -1591,7 +1591,7 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
         if (has_z) stf(dz0 + (int64_t)(tg + j) * a.dz_ls + c, dzv);
       }
     }
-    __syncthreads();
+    block_sync();
     // block sum of the chunk's dB/dC -> slab[b][blk][t][2N]
     for (int q = threadIdx.x; q < kSub * 2 * kN; q += kBlock) {
       float sum = 0.f;

@@ -125,21 +125,21 @@ __global__ __launch_bounds__(256) void skinny_n_kernel(SkinnyP p) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) red[wave - 2][i * NB + j][lane] = acc[i][j];
   }
-  __syncthreads();
+  block_sync();
   if (wave < 2) {
 #pragma unroll
     for (int i = 0; i < MB; ++i)
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] += red[wave][i * NB + j][lane];
   }
-  __syncthreads();
+  block_sync();
   if (wave == 1) {
 #pragma unroll
     for (int i = 0; i < MB; ++i)
 #pragma unroll
       for (int j = 0; j < NB; ++j) red[0][i * NB + j][lane] = acc[i][j];
   }
-  __syncthreads();
+  block_sync();
   if (wave == 0) {
 #pragma unroll
     for (int i = 0; i < MB; ++i)
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(512) void tn_skinny_kernel(TnP p) {
     load(0);
     store(0);
   }
-  __syncthreads();
+  block_sync();
   // (a two-deep register ring measured equal / slower: tools/skinny_ab.py)
   for (int t = 0; t < ntile; ++t) {
     const int buf = t & 1;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(512) void tn_skinny_kernel(TnP p) {
       }
     }
     if (t + 1 < ntile) store(buf ^ 1);
-    __syncthreads();
+    block_sync();
   }
   float* sl = p.slab + (int64_t)blockIdx.y * p.m * p.n;
   const int li = lane & 15, g4 = (lane >> 4) * 4;

@@ -30,6 +30,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from . import wgrad
+
 
 class GradAllReduce:
     def __init__(self, params, bucket_mb: float = 128.0, group=None, first_bucket_mb: float = 8.0,
@@ -40,7 +42,12 @@ class GradAllReduce:
         order = list(reversed(self.params))
         dev = order[0].device
         dtype = order[0].dtype
-        total = sum(p.numel() for p in order)
+        # every parameter's view starts on a 256-byte boundary (the deferred
+        # weight-gradient GEMMs, mtts.wgrad, store 16-byte pieces straight
+        # into it); the padding stays zero and rides along in the all-reduce
+        al = max(1, 256 // torch.empty(0, dtype=dtype).element_size())
+        pad = lambda n: -(-n // al) * al  # noqa: E731
+        total = sum(pad(p.numel()) for p in order)
         self.flat = torch.zeros(total, device=dev, dtype=dtype)
         cap_rest = max(1, int(bucket_mb * 1024 * 1024 // self.flat.element_size()))
         cap = max(1, int(min(first_bucket_mb, bucket_mb) * 1024 * 1024 // self.flat.element_size()))
@@ -58,7 +65,7 @@ class GradAllReduce:
             self.views[p] = self.flat[off:off + n].view_as(p)
             p.grad = self.views[p]
             self.bucket_of[p] = len(self.buckets)
-            off += n
+            off += pad(n)
             count += 1
             if off - start >= cap:
                 self.buckets.append([start, off, count])
@@ -70,6 +77,15 @@ class GradAllReduce:
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
+        # deferred weight gradients (mtts.wgrad) are written straight into the
+        # bucket views and announced through the engine's listener
+        for p, v in self.views.items():
+            p._mtts_grad_view = v
+        wgrad.add_listener(self._deferred_ready)
+
+    def _deferred_ready(self, p):
+        if p in self.views:
+            self._hook(p)
 
     def zero_grad(self):
         """Start a step: drop the gradients (p.grad = None).  Autograd then
@@ -83,6 +99,11 @@ class GradAllReduce:
         self.handles = [None] * len(self.buckets)
 
     def _hook(self, p):
+        if p.grad is None:
+            # autograd runs post-accumulate hooks even when a backward returned
+            # no gradient for p -- the deferred weight gradients (mtts.wgrad)
+            # do exactly that and announce p through the engine's listener
+            return
         v = self.views[p]
         if p.grad is not v and p.grad.data_ptr() != v.data_ptr():
             # autograd allocated a fresh gradient (the optimizer's zero_grad
@@ -146,3 +167,7 @@ class GradAllReduce:
     def remove(self):
         for h in self.hooks:
             h.remove()
+        wgrad.remove_listener(self._deferred_ready)
+        for p in self.views:
+            if getattr(p, "_mtts_grad_view", None) is not None:
+                del p._mtts_grad_view

@@ -27,6 +27,7 @@ import torch
 
 from . import _lib as L
 from . import gemm as G
+from . import wgrad as WG
 
 _scope = {"token": 0, "depth": 0}
 _cast_plans = {}
@@ -203,13 +204,29 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4, out: torch.Tensor 
     return r
 
 
+class BiasGradSlot:
+    """Hand-off of a bias gradient computed by a downstream kernel: the
+    LayerNorm backward that consumes a linear layer's output (and nothing else
+    does) sums its dx columns in the same pass (ops.LayerNormFn colsum_slot),
+    so the linear's backward skips its own column-sum launches."""
+    __slots__ = ("value",)
+
+    def __init__(self):
+        self.value = None
+
+    def take(self, n):
+        v, self.value = self.value, None
+        return v if (v is not None and v.numel() == n) else None
+
+
 class LinearFn(torch.autograd.Function):
     """y = x @ weight[r0:r1]^T + bias[r0:r1] in dtype of x.  Gradients for the
     full weight/bias (zero outside [r0, r1) when a row slice is used)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, r0, r1):
+    def forward(ctx, x, weight, bias, r0, r1, slot=None):
         cd = x.dtype
+        ctx.slot = slot
         w = cast_weight(weight, cd)
         if r0 is not None:
             w = w[r0:r1]
@@ -242,7 +259,7 @@ class LinearFn(torch.autograd.Function):
             else:
                 dx = (dy2 @ w).view(xshape)
         dW = db = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not WG.submit([(dy2, x2, ctx.weight, None if r0 is None else (r0, r1))]):
             g = wgrad(dy2, x2).to(wdt)
             if r0 is not None:
                 full = torch.zeros(wshape, device=g.device, dtype=wdt)
@@ -250,19 +267,22 @@ class LinearFn(torch.autograd.Function):
                 g = full
             dW = g
         if bdt is not None and ctx.needs_input_grad[2]:
-            gb = colsum(dy2).to(bdt)
+            gb = ctx.slot.take(dy2.shape[1]) if ctx.slot is not None else None
+            gb = (gb if gb is not None else colsum(dy2)).to(bdt)
             if r0 is not None:
                 full = torch.zeros(wshape[0], device=gb.device, dtype=bdt)
                 full[r0:r1] = gb
                 gb = full
             db = gb
-        return dx, dW, db, None, None
+        return dx, dW, db, None, None, None
 
 
-def linear(x, weight, bias=None, rows=None):
-    """Functional form; `rows=(r0, r1)` selects a row slice of weight/bias."""
+def linear(x, weight, bias=None, rows=None, dbias_slot=None):
+    """Functional form; `rows=(r0, r1)` selects a row slice of weight/bias;
+    `dbias_slot` (BiasGradSlot): the bias gradient arrives from the consumer's
+    backward (the caller guarantees the output feeds only that consumer)."""
     r0, r1 = (None, None) if rows is None else rows
-    return LinearFn.apply(x, weight, bias, r0, r1)
+    return LinearFn.apply(x, weight, bias, r0, r1, dbias_slot)
 
 
 class FFNFn(torch.autograd.Function):
@@ -274,8 +294,9 @@ class FFNFn(torch.autograd.Function):
     the TN kernel straight into fp32."""
 
     @staticmethod
-    def forward(ctx, h, w1, b1, w2, b2):
+    def forward(ctx, h, w1, b1, w2, b2, slot=None):
         cd = h.dtype
+        ctx.slot = slot
         W1, B1, W2, B2 = cast_weight(w1, cd), cast_weight(b1, cd), cast_weight(w2, cd), cast_weight(b2, cd)
         h2 = h.reshape(-1, h.shape[-1])
         pre = torch.empty(h2.shape[0], W1.shape[0], device=h.device, dtype=cd)
@@ -302,18 +323,24 @@ class FFNFn(torch.autograd.Function):
             else:
                 dh = dpre @ W1
             dh = dh.view(hshape)
-        dW1 = wgrad(dpre, h2).to(w1dt) if ctx.needs_input_grad[1] else None
+        dW1 = dW2 = None   # both straight to the grouped engine when deferral is on (mtts.wgrad)
+        if ctx.needs_input_grad[1] and not WG.submit([(dpre, h2, w1, None)]):
+            dW1 = wgrad(dpre, h2).to(w1dt)
         db1 = colsum(dpre).to(b1dt) if ctx.needs_input_grad[2] else None
-        dW2 = wgrad(dy2, a).to(w2dt) if ctx.needs_input_grad[3] else None
-        db2 = colsum(dy2).to(b2dt) if ctx.needs_input_grad[4] else None
-        return dh, dW1, db1, dW2, db2
+        if ctx.needs_input_grad[3] and not WG.submit([(dy2, a, w2, None)]):
+            dW2 = wgrad(dy2, a).to(w2dt)
+        db2 = None
+        if ctx.needs_input_grad[4]:
+            db2 = ctx.slot.take(dy2.shape[1]) if ctx.slot is not None else None
+            db2 = (db2 if db2 is not None else colsum(dy2)).to(b2dt)
+        return dh, dW1, db1, dW2, db2, None
 
 
-def ffn(h, w1, b1, w2, b2):
+def ffn(h, w1, b1, w2, b2, dbias_slot=None):
     """gelu(h W1^T + b1) W2^T + b2: the fused bf16 path when the shapes allow
     it (bf16 activations, d_model / d_ff multiples of 64), else the
-    per-op path (LinearFn + F.gelu)."""
+    per-op path (LinearFn + F.gelu).  dbias_slot: see linear()."""
     if (G.ENABLED and G.FFN_FUSED and h.dtype == torch.bfloat16 and h.is_cuda and h.shape[-1] % 64 == 0 and w1.shape[0] % 64 == 0
             and h.stride(-1) == 1 and h.is_contiguous()):
-        return FFNFn.apply(h, w1, b1, w2, b2)
-    return linear(torch.nn.functional.gelu(linear(h, w1, b1)), w2, b2)
+        return FFNFn.apply(h, w1, b1, w2, b2, dbias_slot)
+    return linear(torch.nn.functional.gelu(linear(h, w1, b1)), w2, b2, dbias_slot=dbias_slot)

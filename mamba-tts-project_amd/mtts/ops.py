@@ -98,7 +98,7 @@ def scan_fwd(u, delta, A, Bm, Cm, D=None, z=None, delta_bias=None, softplus=True
 
 
 def scan_bwd(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, ckpt, dout,
-             du=None, ddelta=None, dz=None, dB=None, dC=None, need_dh0=False, a_is_log=False):
+             du=None, ddelta=None, dz=None, dB=None, dC=None, need_dh0=False, a_is_log=False, workspace=None):
     """Backward of scan_fwd.  du/ddelta/dz may be preallocated (strided)
     views to write into; dB/dC (B, L, N) fp32 views likewise.
     Returns du, ddelta, dz, dB, dC, dA, dD, ddelta_bias, dh0 (with a_is_log
@@ -123,7 +123,8 @@ def scan_bwd(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, ckpt, dout,
     dD = torch.empty(Dm, device=dev, dtype=torch.float32)
     dbias = torch.empty(Dm, device=dev, dtype=torch.float32)
     dh0 = torch.empty(Bsz, Dm, N, device=dev, dtype=torch.float32) if need_dh0 else None
-    ws = torch.empty(L.lib().mtts_selective_scan_bwd_workspace(Bsz, Dm, Ln, N), device=dev, dtype=torch.uint8)
+    ws = workspace if workspace is not None else \
+        torch.empty(L.lib().mtts_selective_scan_bwd_workspace(Bsz, Dm, Ln, N), device=dev, dtype=torch.uint8)
     dummy_out = dout  # the forward's `out` is not read by the backward
     b = L.ScanBwdArgs()
     b.f = _scan_args(u, delta, A, Bm, Cm, D, z, delta_bias, softplus, h0, dummy_out, None, ckpt, a_is_log)
@@ -379,8 +380,12 @@ def layernorm_fwd(x, w, b, eps=1e-5, res=None, gamma=None, beta=None, rows_per_g
     return y, mean, rstd, x_sum
 
 
-def layernorm_bwd(xn, w, b, eps, gamma, beta, rows_per_group, mean, rstd, dy, dx_acc=None):
-    """xn: the normalised input (x, or x + res).  Returns dx, dw, db, dgamma, dbeta."""
+def layernorm_bwd(xn, w, b, eps, gamma, beta, rows_per_group, mean, rstd, dy, dx_acc=None, dgb=None,
+                  dx_colsum=None):
+    """xn: the normalised input (x, or x + res).  Returns dx, dw, db, dgamma, dbeta.
+    dgb: an fp32 (G, 2N) buffer receiving dgamma | dbeta side by side (then
+    returned as the two halves); dx_colsum: an fp32 (N) buffer receiving the
+    column sums of dx (the bias gradient of the linear that produced x)."""
     dy = dy if dy.stride(-1) == 1 else dy.contiguous()
     if dy.dtype != xn.dtype:
         dy = dy.to(xn.dtype)
@@ -391,8 +396,11 @@ def layernorm_bwd(xn, w, b, eps, gamma, beta, rows_per_group, mean, rstd, dy, dx
     db = torch.empty(cols, device=xn.device, dtype=torch.float32)
     film = gamma is not None
     G = rows // rows_per_group if film else 0
-    dg = torch.empty(G, cols, device=xn.device, dtype=torch.float32) if film else None
-    dbe = torch.empty(G, cols, device=xn.device, dtype=torch.float32) if film else None
+    if film and dgb is not None:
+        dg, dbe = dgb[:, :cols], dgb[:, cols:]
+    else:
+        dg = torch.empty(G, cols, device=xn.device, dtype=torch.float32) if film else None
+        dbe = torch.empty(G, cols, device=xn.device, dtype=torch.float32) if film else None
     ws = torch.empty(L.lib().mtts_layernorm_bwd_workspace(rows, cols, rows_per_group if film else 0),
                      device=xn.device, dtype=torch.uint8)
     bb = L.LNBwdArgs()
@@ -405,20 +413,32 @@ def layernorm_bwd(xn, w, b, eps, gamma, beta, rows_per_group, mean, rstd, dy, dx
         bb.dx_acc, bb.dxacc_rs = dx_acc.data_ptr(), _rows(dx_acc)[1]
     bb.dx, bb.dx_rs = dx.data_ptr(), _rows(dx)[1]
     bb.dw, bb.db, bb.dgamma, bb.dbeta, bb.workspace = dw.data_ptr(), db.data_ptr(), L.ptr(dg), L.ptr(dbe), ws.data_ptr()
+    bb.dgb_rs = dg.stride(0) if film else 0
+    bb.dx_colsum = L.ptr(dx_colsum)
     L.call("mtts_layernorm_bwd", bb)
     return dx, dw, db, dg, dbe
 
 
 class LayerNormFn(torch.autograd.Function):
     """y = FiLM(LN(x [+ res])); returns (y, x_sum) where x_sum = x + res (or x).
-    gamma/beta: (G, N) with G = rows / rows_per_group."""
+    FiLM parameters either as gamma / beta (G, N) or as ONE (G, 2N) tensor
+    `film` = gamma | beta (the layout of tanh(style_mlp(z)), mamba_decoder.py
+    :82-84), whose gradient is then written in place, side by side (no split /
+    cat).  `colsum_slot` (a linear.BiasGradSlot): the backward also writes the
+    column sums of dx into it -- the bias gradient of the linear layer whose
+    output is x, when x feeds nothing but this LayerNorm."""
 
     @staticmethod
-    def forward(ctx, x, res, w, b, gamma, beta, eps, rows_per_group):
+    def forward(ctx, x, res, w, b, gamma, beta, eps, rows_per_group, film, colsum_slot):
+        if film is not None:
+            n = x.shape[-1]
+            gamma, beta = film[:, :n], film[:, n:]
         y, mean, rstd, x_sum = layernorm_fwd(x, w, b, eps, res, gamma, beta, rows_per_group)
         xn = x_sum if res is not None else x
         ctx.eps, ctx.rpg = eps, rows_per_group
         ctx.has_res = res is not None
+        ctx.has_film = film is not None
+        ctx.slot = colsum_slot
         ctx.dtypes = (w.dtype, b.dtype, None if gamma is None else gamma.dtype)
         ctx.save_for_backward(xn, w, b, gamma, beta, mean, rstd)
         if res is None:
@@ -431,16 +451,30 @@ class LayerNormFn(torch.autograd.Function):
         xn, w, b, gamma, beta, mean, rstd = ctx.saved_tensors
         if dsum is not None and dsum.numel() == 0:
             dsum = None
-        dx, dw, db, dg, dbe = layernorm_bwd(xn, w, b, ctx.eps, gamma, beta, ctx.rpg, mean, rstd, dy, dx_acc=dsum)
+        n = xn.shape[-1]
+        dgb = None
+        if ctx.has_film:
+            dgb = torch.empty(gamma.shape[0], 2 * n, device=xn.device, dtype=torch.float32)
+        csum = None
+        if ctx.slot is not None:
+            csum = torch.empty(n, device=xn.device, dtype=torch.float32)
+        dx, dw, db, dg, dbe = layernorm_bwd(xn, w, b, ctx.eps, gamma, beta, ctx.rpg, mean, rstd, dy, dx_acc=dsum,
+                                            dgb=dgb, dx_colsum=csum)
+        if csum is not None:
+            ctx.slot.value = csum
         wd, bd, gd = ctx.dtypes
         dres = dx if ctx.has_res else None
+        if ctx.has_film:
+            return (dx, dres, dw.to(wd), db.to(bd), None, None, None, None, dgb.to(gd), None)
         return (dx, dres, dw.to(wd), db.to(bd), None if dg is None else dg.to(gd),
-                None if dbe is None else dbe.to(gd), None, None)
+                None if dbe is None else dbe.to(gd), None, None, None, None)
 
 
-def layer_norm(x, w, b, eps=1e-5, res=None, gamma=None, beta=None, rows_per_group=1):
-    """Returns (y, x_sum) with x_sum = x + res (an empty tensor when res is None)."""
-    return LayerNormFn.apply(x, res, w, b, gamma, beta, eps, rows_per_group)
+def layer_norm(x, w, b, eps=1e-5, res=None, gamma=None, beta=None, rows_per_group=1, film=None, colsum_slot=None):
+    """Returns (y, x_sum) with x_sum = x + res (an empty tensor when res is None).
+    film: (G, 2N) gamma | beta in one tensor (instead of gamma / beta);
+    colsum_slot: see LayerNormFn."""
+    return LayerNormFn.apply(x, res, w, b, gamma, beta, eps, rows_per_group, film, colsum_slot)
 
 
 # ---------------------------------------------------------------------------

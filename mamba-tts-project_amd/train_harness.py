@@ -42,6 +42,7 @@ import codec_tokens as ct
 import mamba_decoder
 import style_cross_attention as sca
 import text_encoder as te
+from mtts import wgrad
 from mtts.optim import FusedClipAdam
 
 C5Models = namedtuple("C5Models", "text_encoder dur_predictor style_pipe decoder")
@@ -154,7 +155,8 @@ class TrainStep:
         else:
             for p in self.params:
                 p.grad = None                                                      # optim.zero_grad(), :232
-        total.backward()                                                           # :233
+        with wgrad.deferred():      # projection weight gradients grouped per layer (mtts/wgrad.py)
+            total.backward()                                                       # :233
         if self.dp is not None:
             self.dp.finish()
 

@@ -104,6 +104,72 @@ def test_tn_beta_accumulate_into_row_slice():
     assert torch.equal(full[:512], before[:512]) and torch.equal(full[1024:], before[1024:])
 
 
+def test_tn_beta_accumulate_single_split():
+    """beta = 1 with ONE split runs the ping-pong kernel itself (no reduce
+    pass): its fp32 epilogue adds beta * C (it stored over C before round 5)."""
+    torch.manual_seed(9)
+    dy, x = rnd(1024, 512), rnd(1024, 768)
+    full = torch.randn(3 * 512, 768, device=dev)
+    before = full.clone()
+    G.mm_tn(dy, x, out=full[512:1024], beta=1.0, splits=1)
+    ref = before[512:1024] + dy.float().t() @ x.float()
+    assert rel(full[512:1024], ref) < 1e-5
+    assert torch.equal(full[:512], before[:512]) and torch.equal(full[1024:], before[1024:])
+
+
+def _grouped(probs):
+    import ctypes
+    from mtts import _lib as L
+    arr = (L.GemmArgs * len(probs))()
+    for a, (dy, x, out, beta) in zip(arr, probs):
+        a.m, a.n, a.k, a.layout, a.splits, a.out_dtype = dy.shape[1], x.shape[1], dy.shape[0], G.TN, 1, 0
+        a.lda, a.ldb, a.ldc = dy.stride(0), x.stride(0), out.stride(0)
+        a.a, a.b, a.c, a.beta = dy.data_ptr(), x.data_ptr(), out.data_ptr(), beta
+    lib = L.lib()
+    return lib.mtts_gemm_grouped(arr, len(probs), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+
+def test_tn_grouped_matches_each_problem():
+    """mtts_gemm_grouped: one C2 decoder layer's projection weight gradients
+    (in_proj 4096x1024, out_proj 1024x2048, q and out 1024x1024 over 16384
+    tokens, text K/V 2048x1024 over 1024 tokens, FFN 2048x1024 / 1024x2048)
+    plus ragged ones, with row-slice outputs and beta = 1 accumulation, in
+    ONE launch, against fp32 products of the same bf16 operands."""
+    torch.manual_seed(11)
+    T, Tt = 16384, 1024
+    shapes = [(T, 4096, 1024), (T, 1024, 2048), (T, 1024, 1024), (Tt, 2048, 1024), (T, 2048, 1024),
+              (T, 1024, 2048), (1088, 264, 520), (64, 8, 8)]
+    probs, refs = [], []
+    inproj = torch.randn(3 * 1024, 1024, device=dev)
+    before = inproj.clone()
+    for i, (k, m, n) in enumerate(shapes):
+        dy, x = rnd(k, m, scale=0.5), rnd(k, n, scale=0.5)
+        if i == 2:        # q rows of the packed MHA in-projection, accumulated
+            out, beta = inproj[:1024], 1.0
+            ref = before[:1024] + dy.float().t() @ x.float()
+        elif i == 3:      # k/v rows of it, written
+            out, beta = inproj[1024:], 0.0
+            ref = dy.float().t() @ x.float()
+        else:
+            out, beta = torch.full((m, n), float("nan"), device=dev), 0.0
+            ref = dy.float().t() @ x.float()
+        probs.append((dy, x, out, beta))
+        refs.append((out, ref))
+    probs.sort(key=lambda t: -t[0].shape[0])
+    assert _grouped(probs) == 0
+    for i, (out, ref) in enumerate(refs):
+        assert torch.isfinite(out).all(), i
+        assert rel(out, ref) < 1e-5, i
+
+
+def test_tn_grouped_rejects_bad_problems():
+    dy, x = rnd(128, 256), rnd(128, 256)
+    out = torch.empty(256, 256, device=dev)
+    assert _grouped([(dy, x, out, 0.5)]) != 0          # beta must be 0 or 1
+    assert _grouped([(rnd(100, 256), rnd(100, 256), out, 0.0)]) != 0   # k % 64
+    assert _grouped([(dy, x, out, 0.0)] * 17) != 0     # at most 16 problems
+
+
 def test_default_splits_fill_the_chip():
     assert G.tn_splits(4096, 1024, 16384) * 16 * 4 >= 256
     assert G.tn_splits(1024, 1024, 16384) == 16

@@ -447,6 +447,48 @@ def test_layernorm_res_film_fwd_bwd(dtype, cols, rows, film):
         close(bet.grad, Bt.grad, rtol=tol, name="dbeta")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols,rows", [(1024, 128), (512, 100), (64, 7)])
+def test_layernorm_film_tensor_and_dx_colsum(dtype, cols, rows):
+    """ONE (G, 2N) gamma | beta FiLM tensor (gradient written in place, side by
+    side) equals separate gamma / beta; the backward's fused column sums of dx
+    (colsum_slot, the upstream linear's bias gradient) equal the column sums of
+    the dx it stores, as stored (dtype-rounded), in fp32."""
+    from mtts import ops
+    from mtts.linear import BiasGradSlot, colsum
+    torch.manual_seed(cols + rows)
+    G = 2 if rows % 2 == 0 else 1
+    rpg = rows // G
+    x = torch.randn(rows, cols, device=DEV, dtype=dtype)
+    res = torch.randn(rows, cols, device=DEV, dtype=dtype)
+    w = 1 + 0.1 * torch.randn(cols, device=DEV)
+    b = 0.1 * torch.randn(cols, device=DEV)
+    gb = torch.randn(G, 2 * cols, device=DEV)
+    gy = torch.randn(rows, cols, device=DEV, dtype=dtype)
+    gs = torch.randn(rows, cols, device=DEV, dtype=dtype)
+    outs = []
+    for mode in ("split", "tensor"):
+        xx, rr = x.clone().requires_grad_(True), res.clone().requires_grad_(True)
+        if mode == "split":
+            gam = gb[:, :cols].clone().requires_grad_(True)
+            bet = gb[:, cols:].clone().requires_grad_(True)
+            slot = None
+            y, xs = ops.layer_norm(xx, w, b, 1e-5, res=rr, gamma=gam, beta=bet, rows_per_group=rpg)
+        else:
+            film = gb.clone().requires_grad_(True)
+            slot = BiasGradSlot()
+            y, xs = ops.layer_norm(xx, w, b, 1e-5, res=rr, rows_per_group=rpg, film=film, colsum_slot=slot)
+        (y.float() * gy.float()).sum().add((xs.float() * gs.float()).sum()).backward()
+        dfilm = torch.cat([gam.grad, bet.grad], 1) if mode == "split" else film.grad
+        outs.append((y, xx.grad, rr.grad, dfilm, slot))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+    assert outs[1][3].shape == (G, 2 * cols) and torch.equal(outs[0][3], outs[1][3])
+    cs = outs[1][4].take(cols)
+    assert cs is not None and cs.dtype == torch.float32
+    close(cs, colsum(outs[1][1]), rtol=1e-5, name="dx column sums")
+
+
 def test_upstream_signature_ops(golden):
     """mamba-ssm-signature wrappers ((B, D, L) layout) incl. autograd."""
     from mtts import ops

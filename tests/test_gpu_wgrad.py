@@ -1,0 +1,174 @@
+"""Deferred, grouped weight gradients (mtts/wgrad.py, csrc/gemm.hip
+mtts_gemm_grouped) against the immediate per-projection path, on a bf16
+decoder whose projections take the TN route (d_model 256): every parameter
+gradient of a training step, gradient accumulation into existing .grad,
+listener notification, and world-2 data parallelism with the gradients
+written straight into GradAllReduce's bucket views.  The two paths sum the
+same bf16 products in a different order (whole-K tiles vs split-K slabs):
+fp32 gradients agree to 1e-4 of each tensor's scale."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+D, L_, H, DFF, DS, T, TT, B = 256, 2, 4, 512, 16, 512, 64, 2
+
+
+def _model(seed=0):
+    import mamba_decoder
+    torch.manual_seed(seed)
+    m = mamba_decoder.MambaTTSDecoder(10, d_model=D, n_layers=L_, n_heads=H, d_ff=DFF, d_style=DS,
+                                      max_len=1024).cuda()
+    m.compute_dtype = torch.bfloat16
+    return m
+
+
+def _batch(n=B, seed=7):
+    g = torch.Generator().manual_seed(seed)
+    tok = torch.randint(0, 10, (n, T), generator=g).cuda()
+    text = torch.randn(n, TT, D, generator=g).cuda()
+    z = torch.randn(n, DS, generator=g).cuda()
+    mask = torch.ones(n, TT, dtype=torch.bool).cuda()
+    mask[0, 50:] = False
+    return tok, text, z, mask
+
+
+def _loss(m, tok, text, z, mask):
+    from mtts.loss import cross_entropy
+    logits = m(tok, text, z, text_mask=mask)
+    return cross_entropy(logits.view(-1, 10), tok.view(-1), ignore_index=0)
+
+
+def _grads(m):
+    return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+
+def _check(a, b, tol=1e-4):
+    assert set(a) == set(b), set(a) ^ set(b)
+    for n in a:
+        err = (a[n] - b[n]).abs().max().item()
+        scale = max(b[n].abs().max().item(), 1e-6)
+        assert err <= tol * scale, f"{n}: {err:.3e} > {tol} * {scale:.3e}"
+
+
+def test_deferred_grouped_equals_immediate(monkeypatch):
+    from mtts import wgrad
+    m = _model()
+    batch = _batch()
+    launches = []
+    real = wgrad._launch
+    monkeypatch.setattr(wgrad, "_launch", lambda probs: launches.append(len(probs)) or real(probs))
+    out = {}
+    for defer in (False, True):
+        m.zero_grad(set_to_none=True)
+        with wgrad.deferred(defer):
+            _loss(m, *batch).backward()
+        out[defer] = _grads(m)
+    # in_proj, out_proj (Mamba), q + kv (two jobs), out (MHA), FFN up / down per layer
+    assert sum(launches) == L_ * 7 and len(launches) >= 1, launches
+    assert not wgrad._E.jobs and not wgrad._E.callback_queued
+    _check(out[True], out[False])
+
+
+def test_deferred_accumulates_into_existing_grads():
+    from mtts import wgrad
+    m = _model()
+    batch = _batch()
+    m.zero_grad(set_to_none=True)
+    _loss(m, *batch).backward()
+    once = _grads(m)
+    m.zero_grad(set_to_none=True)
+    for _ in range(2):
+        with wgrad.deferred():
+            _loss(m, *batch).backward()
+    twice = _grads(m)
+    _check(twice, {n: 2 * g for n, g in once.items()})
+
+
+def test_listener_once_per_parameter():
+    from mtts import wgrad
+    m = _model()
+    seen = []
+    fn = seen.append
+    wgrad.add_listener(fn)
+    try:
+        m.zero_grad(set_to_none=True)
+        with wgrad.deferred():
+            _loss(m, *_batch()).backward()
+    finally:
+        wgrad.remove_listener(fn)
+    ids = [id(p) for p in seen]
+    assert len(ids) == len(set(ids)) == L_ * 6      # the MHA in-projection weight once (two jobs)
+    for p in seen:
+        assert p.grad is not None and torch.isfinite(p.grad).all()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, port, q):
+    import faulthandler
+    import sys
+    faulthandler.dump_traceback_later(120, exit=True)   # a hung collective names itself
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mamba-tts-project_amd")]
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    from mtts import wgrad
+    from mtts.dp import GradAllReduce
+    m = _model()
+    dp = GradAllReduce(list(m.parameters()), bucket_mb=1.0)
+    tok, text, z, mask = _batch(2 * B)
+    sl = slice(rank * B, (rank + 1) * B)
+    out = []
+    for defer in (False, True):
+        dp.zero_grad()
+        with wgrad.deferred(defer):
+            _loss(m, tok[sl], text[sl], z[sl], mask[sl]).backward()
+        dp.finish()
+        torch.cuda.synchronize()
+        out.append({n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters()})   # numpy: no fd sharing
+    q.put((rank, out))
+    dp.remove()
+    dist.destroy_process_group()
+
+
+def test_deferred_world2_dp_matches_single_process():
+    """Two gloo ranks on cuda:0: the deferred gradients land in the bucket
+    views and the listener launches the buckets.  The averaged gradients equal
+    the same ranks' immediate-path (split-K) ones to 1e-4, and one process's
+    gradient of the mean of the two shards' losses to 2e-2 (bf16 activations:
+    per-shard and joint graphs round the activation gradients differently,
+    and small sums such as pos_embed's cancel)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=150) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m = _model()
+    tok, text, z, mask = _batch(2 * B)
+    m.zero_grad(set_to_none=True)
+    sum(_loss(m, tok[r * B:(r + 1) * B], text[r * B:(r + 1) * B], z[r * B:(r + 1) * B], mask[r * B:(r + 1) * B])
+        for r in range(2)).div(2).backward()
+    ref = {n: g.cpu() for n, g in _grads(m).items()}
+    for rank, (imm, dfr) in res:
+        imm = {n: torch.from_numpy(g) for n, g in imm.items()}
+        dfr = {n: torch.from_numpy(g) for n, g in dfr.items()}
+        _check(dfr, imm)
+        _check(dfr, ref, tol=2e-2)

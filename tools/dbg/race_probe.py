@@ -1,0 +1,152 @@
+"""Bitwise determinism of the training-step kernels under GPU sharing: NPROC
+processes run the same probe on cuda:0 at once; each op is run REPS times on
+fixed inputs and compared bit for bit with its first result.  A kernel with an
+intra-workgroup race (LDS read before its write is visible, a missing wait)
+shows up as mismatches when other work shares its CUs.
+  NPROC=2 python tools/dbg/race_probe.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mamba-tts-project_amd")]
+import torch  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+REPS = int(os.environ.get("REPS", "30"))
+
+
+def probes(dev):
+    from mtts import attn_kernels as AK
+    from mtts import gemm as G
+    from mtts import ops
+    g = torch.Generator(device="cpu").manual_seed(3)
+    bf = torch.bfloat16
+    r = lambda *s, sc=1.0, dt=bf: (torch.randn(*s, generator=g) * sc).to(dev, dt)  # noqa: E731
+    out = {}
+    only = os.environ.get("ONLY")
+    for (B, T, S, d, H) in [(2, 512, 64, 256, 4), (8, 2048, 128, 1024, 8)]:
+        q, kv, dout = r(B, T, d), r(B, S, 2 * d), r(B, T, d)
+        kpm = torch.zeros(B, S, dtype=torch.bool, device=dev)
+        kpm[0, S - 14:] = True
+        o, lse = AK.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+
+        def attn(q=q, kv=kv, o=o, lse=lse, dout=dout, kpm=kpm, H=H, d=d):
+            dkv = torch.empty_like(kv)
+            dq, _, _ = AK.attention_bwd(q, kv[..., :d], kv[..., d:], H, kpm, o, lse, dout, dk=dkv[..., :d],
+                                        dv=dkv[..., d:])
+            o2, _ = AK.attention_fwd(q, kv[..., :d], kv[..., d:], H, kpm, want_lse=True)
+            return [dq, dkv, o2]
+        out[f"attn B{B} T{T} S{S} d{d}"] = attn
+        x, res, dy = r(B * T, d), r(B * T, d), r(B * T, d)
+        w, b = torch.randn(d, device=dev), torch.randn(d, device=dev)
+        gb = torch.randn(B, 2 * d, device=dev)
+
+        def ln(x=x, res=res, dy=dy, w=w, b=b, gb=gb, T=T, d=d):
+            xx = x.clone().requires_grad_(True)
+            film = gb.clone().requires_grad_(True)
+            from mtts.linear import BiasGradSlot
+            slot = BiasGradSlot()
+            y, xs = ops.layer_norm(xx, w, b, 1e-5, res=res, rows_per_group=T, film=film, colsum_slot=slot)
+            (y.float() * dy.float()).sum().backward()
+            return [y, xs, xx.grad, film.grad, slot.value]
+        out[f"ln+film d{d}"] = ln
+    # scan / conv at C2 shape
+    B, L, D = 8, 2048, 2048
+    u, dl, z, dy = r(B, L, D), r(B, L, D, sc=0.3), r(B, L, D), r(B, L, D)
+    A = -torch.rand(D, 16, device=dev) - 0.1
+    Bm, Cm = r(B, L, 16), r(B, L, 16)
+    Dp, bias = torch.randn(D, device=dev), torch.randn(D, device=dev) * 0.1
+
+    y0, last0, ck0 = ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, want_last=True, want_ckpt=True)
+
+    def scan_fwd():
+        y, last, ck = ops.scan_fwd(u, dl, A, Bm, Cm, Dp, z, bias, True, want_last=True, want_ckpt=True)
+        return [y, last, ck]
+    out["scan fwd C2 (y, last, ckpt)"] = scan_fwd
+
+    from mtts import _lib
+
+    def scan_bwd(segs=None):
+        with _lib.override(scan_bwd_segs=segs):
+            gr = ops.scan_bwd(u, dl, A, Bm, Cm, Dp, z, bias, True, None, ck0, dy)
+        return [t for t in gr if t is not None]
+    out["scan bwd C2 (du, ddelta, dz, dB, dC, dA, dD, dbias)"] = scan_bwd
+    out["scan bwd C2 one segment (no carry kernel)"] = lambda: scan_bwd(1)
+    from mtts import _lib as LL
+    nws = LL.lib().mtts_selective_scan_bwd_workspace(B, D, L, 16)
+    nblk = D // 64
+    nslab, K6 = B * nblk * L * 32, 6
+
+    def scan_bwd_ws():
+        ws = torch.zeros(nws, device=dev, dtype=torch.uint8)
+        gr = ops.scan_bwd(u, dl, A, Bm, Cm, Dp, z, bias, True, None, ck0, dy, workspace=ws)
+        f = ws[:(nws // 4) * 4].view(torch.float32)
+        npar = B * K6 * D * 18
+        return [f[:nslab], f[nslab:nslab + npar], f[nslab + npar:nslab + npar + B * K6 * D * 17], gr[0]]
+    out["scan bwd C2 workspace (slab, par, seg, du)"] = scan_bwd_ws
+    u32, dl32, z32, dy32 = (t.float() for t in (u, dl, z, dy))
+    ck32 = ops.scan_fwd(u32, dl32, A, Bm.float(), Cm.float(), Dp, z32, bias, True, want_ckpt=True)[2]
+    out["scan bwd C2 fp32"] = lambda: [t for t in ops.scan_bwd(u32, dl32, A, Bm.float(), Cm.float(), Dp, z32, bias, True,
+                                                                None, ck32, dy32) if t is not None]
+    xz = r(B, L, 2 * D)
+    cw, cb = torch.randn(D, 4, device=dev) * 0.5, torch.randn(D, device=dev) * 0.1
+
+    def conv():
+        o, _ = ops.conv_fwd(xz[..., :D], cw, cb, True)
+        dxz = torch.zeros_like(xz)
+        _, dw, db = ops.conv_bwd(xz[..., :D], cw, cb, dy, True, dx=dxz[..., :D])
+        return [o, dxz, dw, db]
+    out["conv C2"] = conv
+    a1, w1 = r(16384, 1024), r(4096, 1024)
+    dyy, xx = r(16384, 4096), r(16384, 1024)
+
+    def gemm():
+        return [G.mm_nt(a1, w1), G.mm_tn(dyy, xx)]
+    out["gemm nt/tn"] = gemm
+    return out
+
+
+def worker(rank, q):
+    torch.cuda.set_device(0)
+    ps = probes("cuda")
+    res = {}
+    only = os.environ.get("ONLY")
+    for name, fn in ps.items():
+        if only and not any(o in name for o in only.split(",")):
+            continue
+        ref = [t.clone() if t is not None else None for t in fn()]
+        bad = 0
+        which = {}
+        for _ in range(REPS):
+            got = fn()
+            diff = False
+            for i, (a, b) in enumerate(zip(got, ref)):
+                if a is None or torch.equal(a, b):
+                    continue
+                diff = True
+                ne = (a != b) & ~(torch.isnan(a) & torch.isnan(b))
+                idx = ne.nonzero()
+                w = which.setdefault(i, [0, 0, None, tuple(a.shape)])
+                w[0] += 1
+                w[1] = max(w[1], int(ne.sum()))
+                if w[2] is None and len(idx):
+                    w[2] = (idx[0].tolist(), idx[-1].tolist(), float((a.float() - b.float()).abs().max()))
+            bad += diff
+        torch.cuda.synchronize()
+        res[name] = bad
+        print(f"[proc {rank}] {name}: {bad}/{REPS} runs differ; per output (runs, max #elements, first/last index, "
+              f"max |diff|, shape): {which}", flush=True)
+    q.put(res)
+
+
+if __name__ == "__main__":
+    n = int(os.environ.get("NPROC", "2"))
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    ps = [ctx.Process(target=worker, args=(i, qq)) for i in range(n)]
+    for p in ps:
+        p.start()
+    for _ in range(n):
+        qq.get(timeout=600)
+    for p in ps:
+        p.join(60)

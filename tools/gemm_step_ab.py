@@ -11,6 +11,7 @@ import bench  # noqa: E402
 import mamba_decoder  # noqa: E402
 from mtts import gemm as G  # noqa: E402
 from mtts.optim import FusedClipAdam  # noqa: E402
+from mtts import wgrad  # noqa: E402
 
 c = dict(bench.C2)
 torch.manual_seed(0)
@@ -26,7 +27,8 @@ def step():
     logits = model(tokens, text, z, text_mask=mask)
     loss = torch.nn.functional.cross_entropy(logits.float().view(-1, 10), tokens.view(-1), ignore_index=0)
     opt.zero_grad(set_to_none=True)
-    loss.backward()
+    with wgrad.deferred():
+        loss.backward()
     opt.step()
     return loss
 

@@ -1,8 +1,9 @@
-"""Which Python call sites launch the torch glue kernels (fill / copy / cat /
-elementwise) of the C2 training step: torch.profiler (with stacks) over one
-step after warm-up; GPU time and launch count grouped by kernel family and by
-the innermost frame in mtts/ or mamba_decoder.py of the launching op.
-python tools/glue_sources.py"""
+"""Which ops launch the small kernels (fills, copies, casts, column sums,
+split-K reduces, ...) of the C2 training step: torch.profiler over one step
+after warm-up; every GPU kernel is attributed to its chain of CPU ops (the
+autograd Function / module op that issued it and the aten op under it), and
+the kernels are grouped by (issuing chain, kernel family) with launch count
+and GPU time per step.   python tools/glue_sources.py [--all]"""
 import os
 import sys
 from collections import defaultdict
@@ -14,6 +15,8 @@ from torch.profiler import ProfilerActivity, profile  # noqa: E402
 import bench  # noqa: E402
 import mamba_decoder  # noqa: E402
 from mtts.optim import FusedClipAdam  # noqa: E402
+from mtts import loss as mloss  # noqa: E402
+from mtts import wgrad  # noqa: E402
 
 c = dict(bench.C2)
 torch.manual_seed(0)
@@ -26,37 +29,52 @@ opt = FusedClipAdam(list(model.parameters()), lr=1e-4, max_grad_norm=1.0)
 
 def step():
     logits = model(tokens, text, z, text_mask=mask)
-    loss = torch.nn.functional.cross_entropy(logits.float().view(-1, 10), tokens.view(-1), ignore_index=0)
+    loss = mloss.cross_entropy(logits.view(-1, logits.shape[-1]), tokens.view(-1), ignore_index=0)
     opt.zero_grad(set_to_none=True)
-    loss.backward()
+    with wgrad.deferred():
+        loss.backward()
     opt.step()
 
 
 for _ in range(3):
     step()
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
     step()
     torch.cuda.synchronize()
 
-GLUE = ("Fill", "copy", "Cat", "elementwise", "reduce_kernel", "index", "fill")
-by_site = defaultdict(lambda: [0, 0.0])
+BIG = ("gemm_pp_kernel", "gemm_kernel", "scan_", "attn_", "ln_fwd", "ln_bwd", "conv_", "adam_kernel", "Cijk",
+       "skinny", "small_k", "sumsq", "cast_multi", "embed", "ce_")
+show_all = "--all" in sys.argv
+
+
+def family(name):
+    for f in ("FillFunctor", "copy_kernel", "copyBuffer", "CatArray", "colsum_rows", "colsum_multi", "colsum",
+              "split_reduce", "reduce_kernel", "elementwise", "index"):
+        if f in name:
+            return f
+    return name[:60]
+
+
+groups = defaultdict(lambda: [0, 0.0])
 for ev in prof.events():
     if ev.device_type != torch.autograd.DeviceType.CPU:
         continue
-    kern = [k for k in ev.kernels] if hasattr(ev, "kernels") else []
-    if not kern:
-        continue
-    site = "?"
-    for fr in ev.stack or []:
-        if "mtts/" in fr or "mamba_decoder.py" in fr or "bench.py" in fr:
-            site = fr.split("/")[-1]
-            break
-    for k in kern:
-        if any(g in k.name for g in GLUE):
-            key = (ev.name, site)
-            by_site[key][0] += 1
-            by_site[key][1] += k.duration / 1e3 if hasattr(k, "duration") else 0.0
-rows = sorted(by_site.items(), key=lambda kv: -kv[1][1])
-for (op, site), (n, us) in rows[:40]:
-    print(f"{us:9.1f} us {n:4d}  {op:40s} {site}")
+    for k in getattr(ev, "kernels", []) or []:
+        if not show_all and any(b in k.name for b in BIG):
+            continue
+        chain = []
+        p = ev
+        while p is not None and len(chain) < 4:
+            chain.append(p.name)
+            p = p.cpu_parent
+        # the outermost interesting frame: an autograd Function / module op
+        fn = next((n for n in reversed(chain) if "Backward" in n or n.startswith("mtts") or "Fn" in n), chain[-1])
+        key = (fn, chain[0], family(k.name))
+        groups[key][0] += 1
+        groups[key][1] += k.duration if hasattr(k, "duration") else 0.0
+
+tot = sum(v[1] for v in groups.values())
+print(f"{'us/step':>9} {'n':>4}  {'issuing op':34s} {'aten op':26s} kernel family   (total {tot:.0f} us)")
+for (fn, op, fam), (n, us) in sorted(groups.items(), key=lambda kv: -kv[1][1])[:60]:
+    print(f"{us:9.1f} {n:4d}  {fn[:34]:34s} {op[:26]:26s} {fam}")
