@@ -31,6 +31,7 @@ import torch.nn.functional as F
 
 from . import gemm as G
 from . import ops
+from . import wgrad as WG
 from .linear import cast_scope, cast_weight, cast_weight_t, linear, wgrad
 
 
@@ -95,7 +96,11 @@ class MambaInnerFn(torch.autograd.Function):
         else:
             dx_dbl[..., :r] = (ddelta @ Wdt).float()
         dt2 = x_dbl.view(-1, r + 2 * N)[:, :r]
-        dW_dt = G.mm_skinny_tn(dd2, dt2) if G.skinny_tn_ok(dd2, dt2) else wgrad(dd2, dt2)
+        # the skinny weight gradients ride in the layer's grouped launch when
+        # deferral is on (mtts.wgrad: 16 tiles in otherwise idle CUs)
+        dW_dt = None
+        if not WG.submit([(dd2, dt2, W_dt, None)], narrow=True):
+            dW_dt = G.mm_skinny_tn(dd2, dt2) if G.skinny_tn_ok(dd2, dt2) else wgrad(dd2, dt2)
         # x_proj: x_dbl = u @ W_x^T  ->  du += d(x_dbl) W_x (accumulated by the GEMM), dW_x
         gx = dx_dbl.to(cd).view(-1, r + 2 * N)
         du2 = du.view(-1, di)
@@ -105,7 +110,9 @@ class MambaInnerFn(torch.autograd.Function):
         else:
             du2.addmm_(gx, Wx)
         u2 = u.reshape(-1, di)
-        dW_x = G.mm_skinny_tn(u2, gx, trans_c=True) if G.skinny_tn_ok(u2, gx) else wgrad(gx, u2)
+        dW_x = None
+        if not WG.submit([(gx, u2, W_x, None)], narrow=True):
+            dW_x = G.mm_skinny_tn(u2, gx, trans_c=True) if G.skinny_tn_ok(u2, gx) else wgrad(gx, u2)
         # the conv's left history (a prefilled conv_state) enters the
         # recomputed pre-activations and the weight gradient
         _, dw, db = ops.conv_bwd(x, conv_w, conv_b, du, True, dx=dxz[..., :di], state_in=conv_state_in)
@@ -113,8 +120,9 @@ class MambaInnerFn(torch.autograd.Function):
         if conv_state_in is not None and ctx.needs_input_grad[8]:
             dstate = _conv_state_grad(x, conv_w, conv_b, conv_state_in, du)
         dA_log = dA_log.to(A_log.dtype)
-        return (dxz, dw.reshape(conv_w.shape).to(conv_w.dtype), db.to(conv_b.dtype), dW_x.to(W_x.dtype),
-                dW_dt.to(W_dt.dtype), dA_log, dD.to(D.dtype), dbias.to(dt_bias.dtype), dstate,
+        return (dxz, dw.reshape(conv_w.shape).to(conv_w.dtype), db.to(conv_b.dtype),
+                None if dW_x is None else dW_x.to(W_x.dtype), None if dW_dt is None else dW_dt.to(W_dt.dtype),
+                dA_log, dD.to(D.dtype), dbias.to(dt_bias.dtype), dstate,
                 None if dh0 is None else dh0.to(h0.dtype))
 
 

@@ -16,6 +16,10 @@ workgroup, straight into the fp32 master gradient (no slabs, no reduce pass,
 no per-GEMM launch).  The rest of the queue is flushed by a callback at the
 end of the backward pass, before `loss.backward()` returns.
 
+The grouped launches run on a side stream (SIDE_STREAM), so the next
+layer's data-gradient kernels fill the CUs the ~224 long tiles leave idle;
+the end-of-backward callback makes the caller's stream wait for it.
+
 Gradient semantics are autograd's: a parameter whose .grad is None gets a
 fresh gradient (or its data-parallel bucket view, mtts.dp), one whose .grad
 exists is accumulated into (beta = 1).  Listeners (mtts.dp.GradAllReduce)
@@ -40,6 +44,10 @@ from . import gemm as G
 
 GROUP_TILES = 192       # flush once the queue holds this many 256x256 output tiles
 MAX_PROBLEMS = 16       # mtts_gemm_grouped's problem limit
+# run the grouped launches on a side stream (the layer's long tiles leave some
+# CUs idle for the next layer's data-gradient kernels); the end-of-backward
+# callback joins the streams
+SIDE_STREAM = False   # measured: no gain (31.8-32.0 ms either way, profiles/r05_c2_ab_side_stream.txt)
 
 _depth = 0
 
@@ -62,10 +70,13 @@ class _Engine:
         self.callback_queued = False
         self.done = set()        # ids of params whose gradient is complete this backward
         self.listeners = []
+        self.side = {}           # device index -> side stream
+        self.used_side = None    # (main, side) streams of this backward
 
     def reset_pass(self):
         self.callback_queued = False
         self.done = set()
+        self.used_side = None
 
 
 _E = _Engine()
@@ -88,8 +99,8 @@ def deferred(enable: bool = True):
         yield
     finally:
         _depth -= 1
-        if _depth == 0 and _E.jobs:   # a backward that raised midway: finish what was queued
-            flush()
+        if _depth == 0 and (_E.jobs or _E.used_side is not None):   # a backward that raised midway
+            _end_of_backward()
 
 
 def add_listener(fn):
@@ -102,22 +113,35 @@ def remove_listener(fn):
         _E.listeners.remove(fn)
 
 
-def _eligible(dy, x, param):
+def _eligible(dy, x, param, narrow=False):
     return (active() and param is not None and param.requires_grad and param.dtype == torch.float32
-            and param.dim() == 2 and dy.shape[1] >= 256 and x.shape[1] >= 256 and G.tn_ok(dy, x))
+            and param.dim() == 2 and (narrow or (dy.shape[1] >= 256 and x.shape[1] >= 256)) and G.tn_ok(dy, x))
 
 
 def _end_of_backward():
     flush()
+    if _E.used_side is not None:   # gradients complete before anything after the backward
+        main, side = _E.used_side
+        main.wait_stream(side)
     _E.reset_pass()
 
 
-def submit(jobs) -> bool:
+def _side_stream(dev):
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _E.side.get(i)
+    if st is None:
+        st = _E.side[i] = torch.cuda.Stream(device=i)
+    return st
+
+
+def submit(jobs, narrow=False) -> bool:
     """Queue [(dy (K, m) bf16, x (K, n) bf16, param, rows (r0, r1) | None), ...]
     -- the weight gradient(s) of ONE parameter, dW[rows] = dy^T x -- when the
     engine is active and every job takes the TN route; returns False (nothing
-    queued) otherwise, and the caller computes them immediately."""
-    if not jobs or not all(_eligible(dy, x, p) for dy, x, p, _ in jobs):
+    queued) otherwise, and the caller computes them immediately.  `narrow`:
+    also when a side is below 256 (Mamba's x_proj / dt_proj: a few mostly
+    empty tiles that ride in CUs the layer's long tiles leave idle)."""
+    if not jobs or not all(_eligible(dy, x, p, narrow) for dy, x, p, _ in jobs):
         return False
     param = jobs[0][2]
     for dy, x, p, rows in jobs:
@@ -144,6 +168,21 @@ def flush():
     jobs, _E.jobs, _E.tiles = _E.jobs, [], 0
     if not jobs:
         return
+    if not (SIDE_STREAM and _E.callback_queued):
+        _flush(jobs)
+        return
+    main = torch.cuda.current_stream()
+    side = _side_stream(jobs[0].dy.device)
+    side.wait_stream(main)          # the layer's dy / x are complete
+    _E.used_side = (main, side)
+    for j in jobs:                  # the caching allocator must not reuse them before the side stream is done
+        j.dy.record_stream(side)
+        j.x.record_stream(side)
+    with torch.cuda.stream(side):
+        _flush(jobs, side)
+
+
+def _flush(jobs, side=None):
     # destinations: accumulate into an existing .grad; else the data-parallel
     # bucket view (mtts.dp) or a fresh tensor (zeroed when this flush does not
     # cover all of its rows)
@@ -165,6 +204,8 @@ def flush():
         else:
             g = torch.empty(p.shape, device=p.device, dtype=torch.float32) if full else \
                 torch.zeros(p.shape, device=p.device, dtype=torch.float32)
+        if side is not None:
+            g.record_stream(side)
         dest[id(p)] = (g, 0.0 if full else 1.0, True)
     probs, fixups = [], []
     for j in jobs:
@@ -172,6 +213,8 @@ def flush():
         out = g if j.rows is None else g[j.rows[0]:j.rows[1]]
         if not _addressable(out):   # e.g. a view at an odd offset of a caller's flat buffer
             tmp = torch.empty(out.shape, device=out.device, dtype=torch.float32)
+            if side is not None:
+                tmp.record_stream(side)
             fixups.append((out, tmp, beta))
             out, beta = tmp, 0.0
         probs.append((j.dy, j.x, out, beta))

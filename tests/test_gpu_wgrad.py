@@ -68,8 +68,8 @@ def test_deferred_grouped_equals_immediate(monkeypatch):
         with wgrad.deferred(defer):
             _loss(m, *batch).backward()
         out[defer] = _grads(m)
-    # in_proj, out_proj (Mamba), q + kv (two jobs), out (MHA), FFN up / down per layer
-    assert sum(launches) == L_ * 7 and len(launches) >= 1, launches
+    # in_proj, x_proj, dt_proj, out_proj (Mamba), q + kv (two jobs), out (MHA), FFN up / down per layer
+    assert sum(launches) == L_ * 9 and len(launches) >= 1, launches
     assert not wgrad._E.jobs and not wgrad._E.callback_queued
     _check(out[True], out[False])
 
@@ -102,7 +102,7 @@ def test_listener_once_per_parameter():
     finally:
         wgrad.remove_listener(fn)
     ids = [id(p) for p in seen]
-    assert len(ids) == len(set(ids)) == L_ * 6      # the MHA in-projection weight once (two jobs)
+    assert len(ids) == len(set(ids)) == L_ * 8      # the MHA in-projection weight once (two jobs)
     for p in seen:
         assert p.grad is not None and torch.isfinite(p.grad).all()
 

@@ -15,9 +15,10 @@ import mamba_decoder  # noqa: E402
 assert mamba_decoder.__file__.startswith(PKG), (mamba_decoder.__file__, PKG)
 from mtts.loss import cross_entropy  # noqa: E402
 from mtts.optim import FusedClipAdam  # noqa: E402
-try:   # the deferred grouped weight gradients (round 5); DEFER=0 turns them off
-    from mtts.wgrad import deferred as _deferred  # noqa: E402
-    defer = lambda: _deferred(os.environ.get("DEFER", "1") == "1")  # noqa: E731
+try:   # the deferred grouped weight gradients (round 5); DEFER=0 turns them off, SIDE=0 the side stream
+    from mtts import wgrad as _wg  # noqa: E402
+    defer = lambda: _wg.deferred(os.environ.get("DEFER", "1") == "1")  # noqa: E731
+    _wg.SIDE_STREAM = os.environ.get("SIDE", "1") == "1"
 except ImportError:
     import contextlib  # noqa: E402
     defer = contextlib.nullcontext
@@ -53,5 +54,5 @@ for _ in range(3):
     e1.synchronize()
     ts.append(e0.elapsed_time(e1) / 5)
 ts.sort()
-print(f"{'base' if 'AB_ROOT' in os.environ else 'new '}{' defer=' + os.environ['DEFER'] if 'DEFER' in os.environ else ''} C2 step {ts[1]:.2f} ms (windows {', '.join(f'{t:.2f}' for t in ts)})",
+print(f"{'base' if 'AB_ROOT' in os.environ else 'new '}{' defer=' + os.environ['DEFER'] if 'DEFER' in os.environ else ''}{' side=' + os.environ['SIDE'] if 'SIDE' in os.environ else ''} C2 step {ts[1]:.2f} ms (windows {', '.join(f'{t:.2f}' for t in ts)})",
       flush=True)
