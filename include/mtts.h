@@ -64,7 +64,8 @@ enum {
   MTTS_OVR_ATTN_BWD = 6,      /* attention backward: 1 fused one-pass kernel, 2 split dQ + dK/dV passes */
   MTTS_OVR_ATTN_GENERIC = 7,  /* 1: generic MFMA attention kernels only (no short-key / long-key / q_len-1 kernels) */
   MTTS_OVR_CONV_UNTILED = 8,  /* 1: the untiled causal-conv kernels */
-  MTTS_OVR_COUNT = 9
+  MTTS_OVR_GEMM_TILE = 9,     /* NT bf16 GEMM: 1 eight-wave ping-pong tile, 2 four-wave 128x128-per-wave tile */
+  MTTS_OVR_COUNT = 10
 };
 int mtts_set_override(int key, int value);
 int mtts_get_override(int key);

@@ -221,7 +221,7 @@ def call_raw(name, *args):
 
 # kernel-path override keys (include/mtts.h MTTS_OVR_*): test / measurement hooks
 OVERRIDES = {"scan_path": 0, "scan_p": 1, "scan_segs": 2, "scan_bwd_segs": 3, "gemm_narrow": 4,
-             "attn_chunks": 5, "attn_bwd": 6, "attn_generic": 7, "conv_untiled": 8}
+             "attn_chunks": 5, "attn_bwd": 6, "attn_generic": 7, "conv_untiled": 8, "gemm_tile": 9}
 SCAN_C1, SCAN_W2, SCAN_NARROW = 1, 2, 3
 ATTN_BWD_FUSED, ATTN_BWD_SPLIT = 1, 2
 

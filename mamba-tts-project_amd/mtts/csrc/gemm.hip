@@ -957,6 +957,135 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_grouped_kernel(const Grou
   gemm_pp_body<AK, BKM, EPI, OUT_F32>(q, wid - t0);
 }
 
+// ---------------------------------------------------------------------------
+// Four-wave form (round 5, NT): the same 256x256 output tile on 4 waves
+// (2 M x 2 N, one per SIMD), 128x128 per wave (8x8 16x16 accumulator blocks,
+// 256 registers), so a 32-deep K-step reads 8 A + 8 B fragments for 64 MFMAs:
+// 0.25 fragment reads per MFMA against the 8-wave tile's 0.375.
+//  * K-steps of 32 go by LDS-DMA into a ring of 4 stages of 32 KiB (A then B,
+//    16 row-blocks of 16 rows x 64 B each); a wave stages row-blocks
+//    4w..4w+3 of A and of B, one DMA per MFMA group.
+//  * one barrier per K-step.  Top of step g: this wave's DMAs of step g+1
+//    retired (counted vmcnt) and its fragment reads of step g retired
+//    (lgkmcnt 0), barrier -> every wave's DMAs of g+1 have landed and every
+//    read of step g's stage is done; then step g+4 is staged into step g's
+//    stage and step g+1's fragments are read between step g's 64 MFMAs.
+//  * bank swizzle of a row-block (16 rows of 4 16-B chunks): chunk c of row r
+//    at slot 4r + (c ^ (-(r>>2) & 3)), written by the DMA's source address;
+//    each ds_read_b128 lane group (rows 0-3 and 12-15 at chunk c, rows 4-11
+//    at chunk c^1) then covers 16 distinct 16-B slots.
+constexpr int kW4Threads = 256;
+constexpr int kW4BK = 32;
+constexpr int kW4Stages = 4;
+constexpr int kW4Stage = 32768;
+
+__device__ __forceinline__ int w4_slot(int r, int c) { return 4 * r + (c ^ (-(r >> 2) & 3)); }
+
+template <int EPI>
+__global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[kW4Stages * kW4Stage];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nk = p.k / kW4BK;
+  const WorkItem it = work_item(p, xcd_work_id());
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+
+  // DMA source offsets: lane -> (row r, chunk c) of the slot 16*lane it writes
+  uint32_t oa[4], ob[4];
+  {
+    const int r = lane >> 2;
+    const int c = (lane & 3) ^ (-(r >> 2) & 3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int row = it.m0 + (4 * wave + i) * 16 + r;
+      row = row < p.m ? row : p.m - 1;
+      oa[i] = (uint32_t)((int64_t)row * p.lda * 2) + c * 16;
+      int col = it.n0 + (4 * wave + i) * 16 + r;
+      col = col < p.n ? col : p.n - 1;
+      ob[i] = (uint32_t)((int64_t)col * p.ldb * 2) + c * 16;
+    }
+  }
+  const char* abase = (const char*)p.a;
+  const char* bbase = (const char*)p.b;
+  auto stage1 = [&](int g, int slot, int j) {   // DMA j (0-3: A block, 4-7: B block) of K-step g
+    const uint32_t st = lds0 + slot * kW4Stage + wave * 4096;
+    if (j < 4) glds16(abase + g * (kW4BK * 2), oa[j & 3], st + (j & 3) * 1024);
+    else glds16(bbase + g * (kW4BK * 2), ob[j & 3], st + 16384 + (j & 3) * 1024);
+  };
+  // fragment addresses: one VGPR per operand, the block offset an immediate
+  const char* fra = lds + wr * 8192 + w4_slot(lane & 15, lane >> 4) * 16;
+  const char* frb = fra - wr * 8192 + 16384 + wc * 8192;
+  auto fa = [&](int g, int mb) -> s16x8 { return *(const lds_s16x8*)(fra + (g & 3) * kW4Stage + mb * 1024); };
+  auto fb = [&](int g, int nb) -> s16x8 { return *(const lds_s16x8*)(frb + (g & 3) * kW4Stage + nb * 1024); };
+
+  f32x4 acc[2][8][4];   // [column half][16-row block][16-column block]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int g = 0; g < kW4Stages; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) stage1(g < nk ? g : nk - 1, g, j);
+  wait_ops<24>();   // K-step 0 landed
+  sbar();
+  // A fragment j is dead after MFMA group j and is reloaded there with the
+  // next K-step's; the B fragments serve every group: double-buffered
+  s16x8 fA[8], fB[2][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    fA[j] = fa(0, j);
+    fB[0][j] = fb(0, j);
+  }
+
+  // One uniform step (no tail code: a separate tail made the register
+  // allocator shuttle the 256 accumulators between register files): K-step
+  // g+4 is staged as min(g+4, nk-1) (the last steps re-stage K-step nk-1
+  // into slots already consumed) and the next step's fragments are always
+  // read (past the end: stale slots, never used), so every step issues 8
+  // DMAs and waits with the same count; the loop ends with vmcnt(0).
+  auto step = [&](int g, auto cur_c) {
+    constexpr int CUR = decltype(cur_c)::value;
+    wait_ops<16>();   // K-step g+1 landed (g+2, g+3 in flight)
+    barrier();        // lgkmcnt(0) + s_barrier
+    const int gs = g + 4 < nk ? g + 4 : nk - 1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __builtin_amdgcn_sched_barrier(0);
+      stage1(gs, (g + 4) & 3, j);
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb)
+        acc[nb >> 2][j][nb & 3] = mfma(fB[CUR][nb], fA[j], acc[nb >> 2][j][nb & 3]);
+      fA[j] = fa(g + 1, j);
+      fB[1 - CUR][j] = fb(g + 1, j);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int g = 0; g < nk; g += 2) {   // nk is even (K % 64 == 0)
+    step(g, std::integral_constant<int, 0>{});
+    step(g + 1, std::integral_constant<int, 1>{});
+  }
+  wait_ops<0>();   // the re-staged DMAs: none may land after the workgroup ends
+  // pin the accumulators to the accumulator file across the loop exit (the
+  // bias / GELU epilogues otherwise lead the allocator to shuttle them
+  // between register files inside the loop)
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[h][i][j]));
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {   // every DMA retired: the bias loads are the only VMEM in flight
+    f32x4 bias[4] = {};
+    load_bias<EPI>(p, it.n0, 2 * wc + h, lane, bias);
+    store_tile_buf<EPI, false>(p, acc[h], bias, it.m0, it.n0, wr, 2 * wc + h, lane, 0);
+  }
+}
+
 // out[i] = beta*out[i] + sum_s slab[s][i] (fixed order); rows x cols with row strides
 __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ slabs, int64_t sstride, int splits,
                                                            int rows, int cols, int64_t lds_, float* out, int64_t ldo,
@@ -988,6 +1117,12 @@ void launch(const GemmParams& p, int nwg, hipStream_t st) {
   if (!pp_ok) {
     hipLaunchKernelGGL((gemm_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
     return;
+  }
+  if constexpr (AK && BKM && !F32) {
+    if (override_of(MTTS_OVR_GEMM_TILE) == 2) {
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI>), dim3(nwg), dim3(kW4Threads), 0, st, p);
+      return;
+    }
   }
   hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, EPI, F32>), dim3(nwg), dim3(kThreads), 0, st, p);
 }

@@ -213,14 +213,38 @@ def test_ffn_fused_matches_per_op_path():
         assert rel(a, b) < 2e-2, nm
 
 
-@pytest.fixture(params=["pingpong", "narrow"])
+@pytest.fixture(params=["pingpong", "narrow", "fourwave"])
 def gemm_mode(request):
-    """The ping-pong kernel (default) or the single-group kernel with 8-byte
+    """The ping-pong kernel (default), the single-group kernel with 8-byte
     epilogue stores (the fallback for 8-byte-aligned outputs; forced with the
-    gemm_narrow override)."""
+    gemm_narrow override) or the four-wave 128x128-per-wave NT tile (gemm_tile
+    override 2; TN problems keep the ping-pong kernel)."""
     from mtts import _lib as L
-    with L.override(gemm_narrow=1 if request.param == "narrow" else None):
+    with L.override(gemm_narrow=1 if request.param == "narrow" else None,
+                    gemm_tile=2 if request.param == "fourwave" else None):
         yield request.param
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 128), (1000, 264, 192), (300, 1032, 1024),
+                                   (37, 8, 64), (4096, 96, 2048), (1024, 2048, 320)])
+def test_nt_four_wave_tile(m, n, k):
+    """The four-wave tile at K = 2 .. 64 K-steps of 32 (K = 64: the prologue's
+    re-staged steps and the stale-slot reads past the end), ragged M / N
+    edges, every epilogue."""
+    from mtts import _lib as L
+    torch.manual_seed(m + 3 * n + k)
+    a, b = rnd(m, k), rnd(n, k)
+    ref = a.float() @ b.float().t()
+    with L.override(gemm_tile=2):
+        assert rel(G.mm_nt(a, b), ref) < 1e-2
+        bias = rnd(n, dtype=torch.float32)
+        assert rel(G.mm_nt(a, b, bias=bias), ref + bias) < 1e-2
+        pre = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+        act = G.mm_nt(a, b, bias=bias, gelu_aux=pre)
+        assert rel(pre, ref + bias) < 1e-2 and gelu_matches(act, pre)
+        aux = rnd(m, n, scale=3.0)
+        g = G.mm_nt(a, b, dgelu_aux=aux)
+        assert rel(g, torch.ops.aten.gelu_backward(ref.to(torch.bfloat16), aux)) < 1e-2
 
 
 @pytest.mark.parametrize("m,n,k", [(16384, 4096, 1024), (16484, 4104, 1024), (4096, 2048, 128), (8192, 1024, 2048)])
