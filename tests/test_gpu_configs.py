@@ -293,13 +293,89 @@ def test_c2_shape_two_layer_decoder_vs_oracle(dtype):
 
 
 # --------------------------------------------------------------------------- C5
+# Measured errors of the C5 decoder test below (relative to the reference's
+# max |value|, MI355X, this seed; layer index dropped, max over the two
+# layers) -> bound = 3x measured.  Measured in round 5
+# (profiles/r05_c5_parity_measured_errors.txt).
+C5_BF16_MEASURED = {
+    "loss": 7.57e-05,
+    "logits": 7.01e-03,
+    "dtoken_embed.weight": 2.78e-03,
+    "dpos_embed.weight": 4.44e-03,
+    "dquant_embed.weight": 3.28e-03,
+    "dlayers.norm_mamba.weight": 3.78e-03,
+    "dlayers.norm_mamba.bias": 3.71e-03,
+    "dlayers.mamba.A_log": 5.65e-03,
+    "dlayers.mamba.D": 4.54e-03,
+    "dlayers.mamba.in_proj.weight": 3.52e-03,
+    "dlayers.mamba.conv1d.weight": 3.95e-03,
+    "dlayers.mamba.conv1d.bias": 3.70e-03,
+    "dlayers.mamba.x_proj.weight": 1.48e-02,
+    "dlayers.mamba.dt_proj.weight": 5.44e-03,
+    "dlayers.mamba.dt_proj.bias": 5.58e-03,
+    "dlayers.mamba.out_proj.weight": 3.53e-03,
+    "dlayers.norm_cross.weight": 4.43e-03,
+    "dlayers.norm_cross.bias": 3.62e-03,
+    "dlayers.cross_attn.in_proj_weight": 3.71e-03,
+    "dlayers.cross_attn.in_proj_bias": 3.39e-03,
+    "dlayers.cross_attn.out_proj.weight": 3.45e-03,
+    "dlayers.cross_attn.out_proj.bias": 3.40e-03,
+    "dlayers.norm_ff.weight": 3.36e-03,
+    "dlayers.norm_ff.bias": 3.71e-03,
+    "dlayers.ff.0.weight": 2.57e-03,
+    "dlayers.ff.0.bias": 2.58e-03,
+    "dlayers.ff.2.weight": 3.14e-03,
+    "dlayers.ff.2.bias": 3.25e-03,
+    "dlayers.style_mlp.0.weight": 4.33e-03,
+    "dlayers.style_mlp.0.bias": 4.33e-03,
+    "dnorm_out.weight": 2.06e-03,
+    "dnorm_out.bias": 2.86e-03,
+    "dhead.weight": 1.36e-03,
+    "dhead.bias": 1.81e-03}
+C5_BF16_BOUNDS = {   # 3x measured, rounded down to 2 significant digits
+    "loss": 0.00022,
+    "logits": 0.021,
+    "dtoken_embed.weight": 0.0083,
+    "dpos_embed.weight": 0.013,
+    "dquant_embed.weight": 0.0098,
+    "dlayers.norm_mamba.weight": 0.011,
+    "dlayers.norm_mamba.bias": 0.011,
+    "dlayers.mamba.A_log": 0.016,
+    "dlayers.mamba.D": 0.013,
+    "dlayers.mamba.in_proj.weight": 0.01,
+    "dlayers.mamba.conv1d.weight": 0.011,
+    "dlayers.mamba.conv1d.bias": 0.011,
+    "dlayers.mamba.x_proj.weight": 0.044,
+    "dlayers.mamba.dt_proj.weight": 0.016,
+    "dlayers.mamba.dt_proj.bias": 0.016,
+    "dlayers.mamba.out_proj.weight": 0.01,
+    "dlayers.norm_cross.weight": 0.013,
+    "dlayers.norm_cross.bias": 0.01,
+    "dlayers.cross_attn.in_proj_weight": 0.011,
+    "dlayers.cross_attn.in_proj_bias": 0.01,
+    "dlayers.cross_attn.out_proj.weight": 0.01,
+    "dlayers.cross_attn.out_proj.bias": 0.01,
+    "dlayers.norm_ff.weight": 0.01,
+    "dlayers.norm_ff.bias": 0.011,
+    "dlayers.ff.0.weight": 0.0077,
+    "dlayers.ff.0.bias": 0.0077,
+    "dlayers.ff.2.weight": 0.0094,
+    "dlayers.ff.2.bias": 0.0097,
+    "dlayers.style_mlp.0.weight": 0.012,
+    "dlayers.style_mlp.0.bias": 0.012,
+    "dnorm_out.weight": 0.0061,
+    "dnorm_out.bias": 0.0085,
+    "dhead.weight": 0.004,
+    "dhead.bias": 0.0054}
+
+
 def test_c5_train_shape_two_layer_decoder_bf16():
     """train.py's decoder call (configs[4]'s shape): 5 FACodec streams of 1024
     frames flattened to T_audio=5120, the voice prompt embedded through the
     decoder's tables as 5120 reference keys in front of 128 text keys
     (T_kv=5248), codec_ce_loss, backward; 2 layers of d_model=1024, bf16,
-    B=1.  vs the float64 oracle: loss 1e-2, logits 5e-2, gradients of the
-    token table and the first layer's projections 1e-1 of their scale."""
+    B=1.  vs the float64 oracle: the loss, the logits and EVERY parameter
+    gradient, each bounded by 3x its measured error (C5_BF16_BOUNDS)."""
     import codec_tokens as ct
     m = _decoder(1024, 2, d_ff=2048, num_quantizers=5)
     m.compute_dtype = torch.bfloat16
@@ -326,11 +402,14 @@ def test_c5_train_shape_two_layer_decoder_bf16():
                                      ref_hidden=r_ref, ref_mask=r_mask)
     r_loss = R.codec_ce_loss_ref(r_logits, audio)
     r_loss.backward()
-    close(loss, r_loss.detach(), rtol=1e-2, name="C5 loss")
-    close(logits.float(), r_logits.detach(), rtol=5e-2, name="C5 logits")
-    for n in ("token_embed.weight", "layers.0.mamba.in_proj.weight", "layers.0.cross_attn.in_proj_weight",
-              "layers.1.ff.2.weight", "head.weight"):
-        close(dict(m.named_parameters())[n].grad, p[n].grad, rtol=1e-1, name=f"C5 d{n}")
+    errs = {"loss": _rel_err(loss, r_loss.detach()), "logits": _rel_err(logits.float(), r_logits.detach())}
+    for n, prm in m.named_parameters():
+        k = "d" + re.sub(r"^layers\.\d+\.", "layers.", n)
+        errs[k] = max(errs.get(k, 0.0), _rel_err(prm.grad, p[n].grad))
+    print("C5 bf16 measured errors (of max|ref|): " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    bad = [f"{k}: {e:.3e} > {C5_BF16_BOUNDS.get(k)}" for k, e in errs.items()
+           if C5_BF16_BOUNDS.get(k) is None or not e <= C5_BF16_BOUNDS[k]]
+    assert not bad, "; ".join(bad)
 
 
 # --------------------------------------------------------------------------- contract fixes
