@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 9
+#define MTTS_ABI_VERSION 10
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -614,6 +614,44 @@ int mtts_gemm(const MttsGemmArgs* a, void* stream);
  * layer's projection weight gradients (mamba_decoder.py:29-43 in/out_proj,
  * MHA q/kv/out, FFN) into one such launch. */
 int mtts_gemm_grouped(const MttsGemmArgs* probs, int n, void* stream);
+
+/* ------------------------------------------------------------------------
+ * fp32 MFMA GEMM over WINDOWED row matrices (csrc/convgemm.hip, ABI 10): the
+ * text encoder's / duration predictor's convolutions as direct implicit-GEMM
+ * convolutions (FastSpeech2 PositionwiseFeedForward Conv1d k = 9 / 1 and
+ * VariancePredictor Conv k = 3; reference text_encoder.py:80-85, 118-122,
+ * 131-209 -> the un-vendored FastSpeech2 modules; replaces nn.Conv1d there).
+ * Row r of an operand starts at ptr + (r / seg_rows) * seg_stride +
+ * (r % seg_rows) * row_stride (elements) and is contiguous; on a zero-padded
+ * channel-last activation (B, T + 2p, C) with seg_rows = T, seg_stride =
+ * (T + 2p) C, row_stride = C, a row of K*C elements is the conv window.
+ *   NT: C[m,n] = sum_k A[row m][k] B[row n][k]
+ *   TN: C[m,n] = sum_k A[row k][m] B[row k][n]
+ * C rows through the same map (n contiguous).  fp32 everywhere, exact-f32
+ * MFMA products, fp32 accumulation.  n % 4 == 0; NT k % 4 == 0, TN m % 4 ==
+ * 0; 16-byte aligned pointers, strides multiples of 4 elements.  Epilogues
+ * (bf16 GEMM's not reused: fp32 out): + bias[n]; ReLU; ReLU backward
+ * (C = result where aux[row m][n] > 0, else 0); beta: C = result + beta C.
+ * ------------------------------------------------------------------------ */
+#define MTTS_CONVGEMM_BIAS 1
+#define MTTS_CONVGEMM_RELU 2
+#define MTTS_CONVGEMM_DRELU 4
+typedef struct {
+  const void* ptr;
+  int64_t seg_rows, seg_stride, row_stride;
+} MttsRowMap;
+typedef struct {
+  int layout;                /* MTTS_GEMM_NT / MTTS_GEMM_TN */
+  int m, n, k;
+  MttsRowMap a, b, c, aux;   /* aux: the ReLU output for MTTS_CONVGEMM_DRELU */
+  const float* bias;
+  int epilogue;              /* MTTS_CONVGEMM_* bits */
+  float beta;
+  int splits;                /* > 1: K split over workgroups, fp32 partial slabs summed in fixed order */
+  void* workspace;           /* splits > 1: mtts_convgemm_workspace() bytes */
+} MttsConvGemmArgs;
+int64_t mtts_convgemm_workspace(const MttsConvGemmArgs* a);
+int mtts_convgemm(const MttsConvGemmArgs* a, void* stream);
 
 /* ------------------------------------------------------------------------
  * Skinny bf16 GEMMs of the Mamba mixer's inner projections (csrc/skinny.hip).

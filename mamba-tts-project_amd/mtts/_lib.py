@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -89,6 +89,16 @@ class GemmArgs(C.Structure):
                 ("a", vp), ("b", vp), ("c", vp), ("bias", vp), ("aux", vp), ("workspace", vp), ("beta", f32)]
 
 
+class RowMap(C.Structure):
+    _fields_ = [("ptr", vp), ("seg_rows", i64), ("seg_stride", i64), ("row_stride", i64)]
+
+
+class ConvGemmArgs(C.Structure):
+    _fields_ = [("layout", i32), ("m", i32), ("n", i32), ("k", i32), ("a", RowMap), ("b", RowMap), ("c", RowMap),
+                ("aux", RowMap), ("bias", vp), ("epilogue", i32), ("beta", f32), ("splits", i32),
+                ("workspace", vp)]
+
+
 class SkinnyArgs(C.Structure):
     _fields_ = [("mode", i32), ("m", i32), ("n", i32), ("k", i32), ("c_dtype", i32), ("beta", f32),
                 ("lda", i64), ("ldb", i64), ("ldc", i64), ("a", vp), ("b", vp), ("c", vp), ("workspace", vp),
@@ -156,6 +166,8 @@ _SIGS = {
     "mtts_gemm_workspace": ([C.POINTER(GemmArgs)], i64),
     "mtts_gemm": ([C.POINTER(GemmArgs), vp], i32),
     "mtts_gemm_grouped": ([C.POINTER(GemmArgs), i32, vp], i32),
+    "mtts_convgemm": ([C.POINTER(ConvGemmArgs), vp], i32),
+    "mtts_convgemm_workspace": ([C.POINTER(ConvGemmArgs)], i64),
     "mtts_gemm_skinny": ([C.POINTER(SkinnyArgs), vp], i32),
     "mtts_gemm_skinny_workspace": ([C.POINTER(SkinnyArgs)], i64),
     "mtts_layernorm_bwd_workspace": ([i32, i32, i32], i64),

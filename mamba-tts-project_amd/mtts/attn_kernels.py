@@ -114,13 +114,14 @@ def attention_fwd(q, k, v, n_heads, kpm=None, want_lse=False):
     return out, lse
 
 
-def attention_bwd(q, k, v, n_heads, kpm, out, lse, dout, dk=None, dv=None):
-    """Returns (dq, dk, dv); dk/dv may be given as (strided) output views."""
+def attention_bwd(q, k, v, n_heads, kpm, out, lse, dout, dk=None, dv=None, dq=None):
+    """Returns (dq, dk, dv); dq/dk/dv may be given as (strided) output views."""
     B, T, d = q.shape
     S = k.shape[1]
     dout = _prep(dout.to(q.dtype))
     m = _mask_u8(kpm, B, S)
-    dq = torch.empty_like(q, memory_format=torch.contiguous_format)
+    if dq is None:
+        dq = torch.empty_like(q, memory_format=torch.contiguous_format)
     if dk is None:
         dk = torch.empty(B, S, d, device=q.device, dtype=q.dtype)
     if dv is None:
@@ -179,6 +180,42 @@ class AttentionKVFn(torch.autograd.Function):
         dq, _, _ = attention_bwd(q, kv[..., :d], kv[..., d:], ctx.n_heads, kpm, out, lse, dout,
                                  dk=dkv[..., :d], dv=dkv[..., d:])
         return dq, dkv, None, None
+
+
+class AttentionQKVFn(torch.autograd.Function):
+    """Self-attention on one fused projection output qkv (B, T, 3d): q, k, v
+    are its thirds and the gradient is written straight into one (B, T, 3d)
+    tensor (no slice-backward copies or adds)."""
+
+    @staticmethod
+    def forward(ctx, qkv, n_heads, kpm):
+        d = qkv.shape[-1] // 3
+        if not all(_aligned(qkv[..., i * d:(i + 1) * d]) for i in range(3)):
+            qkv = qkv.contiguous()
+        q, k, v = qkv[..., :d], qkv[..., d:2 * d], qkv[..., 2 * d:]
+        out, lse = attention_fwd(q, k, v, n_heads, kpm, want_lse=True)
+        ctx.save_for_backward(qkv, out, lse, kpm)
+        ctx.n_heads = n_heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse, kpm = ctx.saved_tensors
+        d = qkv.shape[-1] // 3
+        dqkv = torch.empty(qkv.shape, device=qkv.device, dtype=qkv.dtype)
+        attention_bwd(qkv[..., :d], qkv[..., d:2 * d], qkv[..., 2 * d:], ctx.n_heads, kpm, out, lse, dout,
+                      dq=dqkv[..., :d], dk=dqkv[..., d:2 * d], dv=dqkv[..., 2 * d:])
+        return dqkv, None, None
+
+
+def attention_qkv(qkv, n_heads, key_padding_mask=None, dropout_p=0.0):
+    """Self-attention of q, k, v = the thirds of qkv (B, T, 3d)."""
+    d = qkv.shape[-1] // 3
+    if dropout_p > 0.0:
+        return _sdpa_dropout(qkv[..., :d], qkv[..., d:2 * d], qkv[..., 2 * d:], n_heads, key_padding_mask, dropout_p)
+    if torch.is_grad_enabled() and qkv.requires_grad:
+        return AttentionQKVFn.apply(qkv, n_heads, key_padding_mask)
+    return attention_fwd(qkv[..., :d], qkv[..., d:2 * d], qkv[..., 2 * d:], n_heads, key_padding_mask)[0]
 
 
 def _sdpa_dropout(q, k, v, n_heads, key_padding_mask, dropout_p):

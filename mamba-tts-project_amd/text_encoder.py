@@ -20,11 +20,15 @@ architecture is restated:
 * ``VariancePredictor`` (model/modules.py): [Conv(k, pad (k-1)/2) -> ReLU ->
   LayerNorm -> Dropout] x 2 -> Linear(filter, 1) -> squeeze -> masked_fill.
 
-Arithmetic: the attention core is the HIP MFMA attention (mtts_attention_*,
-key_padding_mask = the pad mask, True = pad, as the reference's
-slf_attn_mask); LayerNorm(x + residual) is the fused HIP LayerNorm; the
-projections and the convolutions are GEMMs (convolutions as one GEMM over a
-strided unfold of the time axis: weight (O, C, K) -> (O, C*K)) on hipBLASLt.
+Arithmetic (fp32, as the reference): the attention core is the HIP MFMA
+attention (mtts_attention_*, key_padding_mask = the pad mask, True = pad, as
+the reference's slf_attn_mask) on ONE fused q/k/v projection;
+LayerNorm(x + residual) is the fused HIP LayerNorm; the projections and the
+convolutions run on the hand-written fp32 MFMA GEMM over windowed rows
+(mtts.convgemm, csrc/convgemm.hip): a 'same' Conv1d is a direct implicit-GEMM
+convolution over the zero-padded channel-last activation (no unfold copy),
+the FFN's ReLU is fused into conv 1's epilogue and its backward into conv 2's
+data-gradient epilogue.
 """
 from __future__ import annotations
 
@@ -34,7 +38,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mtts import attn_kernels, ops
-from mtts.linear import linear
+from mtts import convgemm as CG
 
 
 def get_sinusoid_encoding_table(n_position, d_hid, padding_idx=None):
@@ -54,17 +58,19 @@ def _ln(mod, x, res=None):
     return y
 
 
-def conv1d_same(x, weight, bias, padding):
+def conv1d_same(x, weight, bias, padding, relu=False):
     """Conv1d over the time axis of channel-last x (B, T, C) with weight
-    (O, C, K), as one GEMM: y[b, t] = W(O, C*K) . unfold(x)[b, t] + bias."""
-    O, C, K = weight.shape
-    if K == 1 and padding == 0:
-        return linear(x, weight.reshape(O, C), bias)
-    B, T, _ = x.shape
-    xp = F.pad(x, (0, 0, padding, padding))
-    Tout = T + 2 * padding - K + 1
-    cols = xp.unfold(1, K, 1).reshape(B * Tout, C * K)       # [c, k] order = weight's
-    return linear(cols, weight.reshape(O, C * K), bias).view(B, Tout, O)
+    (O, C, K) and padding (K - 1) / 2 (the reference's 'same' convolutions),
+    optionally followed by ReLU: a direct implicit-GEMM convolution
+    (mtts.convgemm.conv1d_same)."""
+    K = weight.shape[2]
+    if 2 * padding != K - 1:
+        raise ValueError(f"conv1d_same: padding {padding} with kernel {K} (only 'same' convolutions)")
+    return CG.conv1d_same(x, weight, bias, relu=relu)
+
+
+def linear(x, weight, bias=None):
+    return CG.linear(x, weight, bias)
 
 
 class Conv(nn.Module):
@@ -98,11 +104,16 @@ class MultiHeadAttention(nn.Module):
         """q/k/v (B, L, d_model); mask (B, L_k) bool, True = pad key.
         Returns (output, None): attention weights are not materialised."""
         residual = q
-        qh = linear(q, self.w_qs.weight, self.w_qs.bias)
-        kh = linear(k, self.w_ks.weight, self.w_ks.bias)
-        vh = linear(v, self.w_vs.weight, self.w_vs.bias)
         # temperature sqrt(d_k) = the kernel's 1/sqrt(head_dim) scale
-        o = attn_kernels.attention(qh, kh, vh, self.n_head, key_padding_mask=mask)
+        if q is k and k is v:   # self-attention (the encoder's use): one fused q/k/v projection
+            w = torch.cat([self.w_qs.weight, self.w_ks.weight, self.w_vs.weight])
+            b = torch.cat([self.w_qs.bias, self.w_ks.bias, self.w_vs.bias])
+            o = attn_kernels.attention_qkv(linear(q, w, b), self.n_head, key_padding_mask=mask)
+        else:
+            qh = linear(q, self.w_qs.weight, self.w_qs.bias)
+            kh = linear(k, self.w_ks.weight, self.w_ks.bias)
+            vh = linear(v, self.w_vs.weight, self.w_vs.bias)
+            o = attn_kernels.attention(qh, kh, vh, self.n_head, key_padding_mask=mask)
         o = self.dropout(linear(o, self.fc.weight, self.fc.bias))
         return _ln(self.layer_norm, o, res=residual), None
 
@@ -116,8 +127,10 @@ class PositionwiseFeedForward(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x):
-        h = F.relu(conv1d_same(x, self.w_1.weight, self.w_1.bias, self.w_1.padding[0]))
-        out = self.dropout(conv1d_same(h, self.w_2.weight, self.w_2.bias, self.w_2.padding[0]))
+        for c in (self.w_1, self.w_2):
+            if 2 * c.padding[0] != c.kernel_size[0] - 1:
+                raise ValueError("PositionwiseFeedForward: 'same' convolutions only")
+        out = self.dropout(CG.conv_ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias))
         return _ln(self.layer_norm, out, res=x)
 
 
@@ -199,9 +212,10 @@ class VariancePredictor(nn.Module):
 
     def forward(self, encoder_output, mask):
         cl = self.conv_layer
-        out = F.relu(cl.conv1d_1(encoder_output))
+        c1, c2 = cl.conv1d_1.conv, cl.conv1d_2.conv
+        out = conv1d_same(encoder_output, c1.weight, c1.bias, c1.padding[0], relu=True)
         out = cl.dropout_1(_ln(cl.layer_norm_1, out))
-        out = F.relu(cl.conv1d_2(out))
+        out = conv1d_same(out, c2.weight, c2.bias, c2.padding[0], relu=True)
         out = cl.dropout_2(_ln(cl.layer_norm_2, out))
         out = linear(out, self.linear_layer.weight, self.linear_layer.bias).squeeze(-1)
         if mask is not None:

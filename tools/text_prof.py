@@ -1,0 +1,57 @@
+"""Where the text-encoder bench leg's time goes: bench.text_bench's step
+(TextEncoder + DurationPredictor fwd+bwd, train.py width, B=8, 128 phonemes)
+under torch.profiler after warm-up; GPU kernels grouped by name with count and
+time per step, plus wall time per step.   python tools/text_prof.py"""
+import os
+import sys
+import time
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mamba-tts-project_amd")]
+import torch  # noqa: E402
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+import text_encoder as te  # noqa: E402
+
+B, T_text, d_model = 8, 128, 512
+dev = "cuda"
+torch.manual_seed(0)
+enc = te.TextEncoder(79, d_model=d_model).to(dev).train()
+dur = te.DurationPredictor(d_model=d_model).to(dev).train()
+g = torch.Generator(device=dev).manual_seed(9)
+ids = torch.randint(1, 79, (B, T_text), device=dev, generator=g)
+lens = torch.randint(T_text // 2, T_text + 1, (B,), device=dev, generator=g)
+mask = torch.arange(T_text, device=dev)[None] >= lens[:, None]
+ids = ids.masked_fill(mask, 0)
+target = torch.randint(1, 10, (B, T_text), device=dev, generator=g).float()
+
+
+def step():
+    h = enc(ids, mask=mask)
+    loss = dur.compute_loss(dur(h, mask=mask), target, mask=mask) + h.square().mean()
+    loss.backward()
+
+
+for _ in range(5):
+    step()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(20):
+    step()
+torch.cuda.synchronize()
+wall = (time.perf_counter() - t0) / 20 * 1e3
+with profile(activities=[ProfilerActivity.CUDA]) as prof:
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+agg = defaultdict(lambda: [0, 0.0])
+for ev in prof.events():
+    if ev.device_type == torch.autograd.DeviceType.CUDA:
+        a = agg[ev.name[:90]]
+        a[0] += 1
+        a[1] += ev.device_time
+tot = sum(v[1] for v in agg.values()) / 5
+print(f"wall {wall:.3f} ms/step, GPU kernel time {tot / 1e3:.3f} ms/step, "
+      f"{sum(v[0] for v in agg.values()) / 5:.0f} kernels/step")
+for name, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
+    print(f"{us / 5:9.1f} us {n / 5:5.0f}x  {name}")
