@@ -217,17 +217,25 @@ def scan_roofline(dtype, B=32, L=8192, D=2048, iters=20, rounds=5, barrier=False
     return ms, nbytes, nbytes / (ms * 1e-3)
 
 
+def pmc_source():
+    """The newest committed PMC summary of the roofline kernel
+    (profiles/rNN_scan_pmc_summary.json, made by the round's evidence script +
+    tools/pmc_summary.py)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_scan_pmc_summary.json")))
+    return paths[-1] if paths else None
+
+
 def pmc_traffic(dtype_key):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3
-    PMC passes (profiles/r04_scan_pmc_summary.json, made by tools/gpu/evidence_r04.sh
-    + tools/pmc_summary.py r04 gpurun_out/ev4/pmc):
-    2 x FETCH_SIZE (gfx950 counts half of wide coalesced streaming reads,
-    MI355X_MICROARCH.md HBM section) + WRITE_SIZE, both KB x 1024."""
-    path = os.path.join(ROOT, "profiles", "r04_scan_pmc_summary.json")
+    PMC passes (pmc_source()): 2 x FETCH_SIZE (gfx950 counts half of wide
+    coalesced streaming reads, MI355X_MICROARCH.md HBM section) + WRITE_SIZE,
+    both KB x 1024."""
+    path = pmc_source()
     try:
         with open(path) as f:
             return json.load(f)[dtype_key]["traffic_bytes"]
-    except (OSError, KeyError, ValueError):
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -582,7 +590,8 @@ def main():
                                      "reference's precision, f32 math)",
                            "bound": "hbm", "achieved": fbw / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                            "frac": fbw / HBM_PEAK, "traffic": pmc_traffic("fp32"), "ms": fms, "algorithmic_bytes": fb,
-                           "traffic_source": "profiles/r04_scan_pmc_summary.json (2*FETCH_SIZE+WRITE_SIZE)"}
+                           "traffic_source": f"{os.path.relpath(pmc_source() or 'none', ROOT)} "
+                                             "(2*FETCH_SIZE+WRITE_SIZE)"}
         if roof[1] is not None:
             (sms, sb, sbw) = roof[1]
             log(f"[bench] scan bf16 north-star {sms:.3f} ms {sbw / 1e9:.0f} GB/s")
