@@ -340,6 +340,27 @@ typedef struct {
 
 int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream);
 
+/* Single-query cross-attention with the query projection fused in
+ * (csrc/attn.hip, ABI 10; the decode step, mamba_decoder.py:72-77 ->
+ * nn.MultiheadAttention's q = LN_cross(x) Wq^T + bq): per (batch, head)
+ * q_h = bf16(LN(x_b) Wq_h^T + bq_h) with LN(x) = bf16((x - mean) rstd w + b)
+ * (two-pass statistics, as the projection kernels' LayerNorm prologue), then
+ * the single-pass decode attention of mtts_attention_fwd.  f.q is ignored;
+ * bf16, q_len 1, head_dim 64 / 128, batch <= 32, the single-pass key range;
+ * d_model <= 2048.  out and / or out_packed as mtts_attention_fwd. */
+typedef struct {
+  MttsAttnFwdArgs f;
+  const void* x;       /* (batch, d_model) bf16 residual rows, row stride x_rs */
+  int64_t x_rs;
+  const void* wq;      /* (heads * head_dim, d_model) bf16 row-major (16-byte aligned) */
+  const void* bq;      /* (heads * head_dim) bf16, or NULL */
+  const float* ln_w;   /* (d_model) */
+  const float* ln_b;
+  float eps;
+  int d_model;
+} MttsAttnQProjArgs;
+int mtts_attention_decode_qproj(const MttsAttnQProjArgs* a, void* stream);
+
 /* Backward: dout -> dq, dk, dv (same dtype as q).  f.out / f.lse must hold
  * the forward's results.  Deterministic (no atomics). */
 typedef struct {

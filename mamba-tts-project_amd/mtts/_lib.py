@@ -127,6 +127,11 @@ class AttnFwdArgs(C.Structure):
                 ("out_packed", vp), ("kv_hs", i64)]
 
 
+class AttnQProjArgs(C.Structure):
+    _fields_ = [("f", AttnFwdArgs), ("x", vp), ("x_rs", i64), ("wq", vp), ("bq", vp), ("ln_w", vp), ("ln_b", vp),
+                ("eps", f32), ("d_model", i32)]
+
+
 class AttnBwdArgs(C.Structure):
     _fields_ = [("f", AttnFwdArgs), ("dout", vp), ("do_bs", i64), ("do_ls", i64),
                 ("dq", vp), ("dq_bs", i64), ("dq_ls", i64), ("dk", vp), ("dk_bs", i64), ("dk_ls", i64),
@@ -175,6 +180,7 @@ _SIGS = {
     "mtts_colsum_workspace": ([i32, i32, i32], i64),
     "mtts_colsum": ([vp, i32, i32, i32, i64, i32, vp, i64, vp, vp], i32),
     "mtts_attention_fwd": ([C.POINTER(AttnFwdArgs), vp], i32),
+    "mtts_attention_decode_qproj": ([C.POINTER(AttnQProjArgs), vp], i32),
     "mtts_attention_bwd_workspace": ([i32, i32, i32, i32, i32, i32], i64),
     "mtts_attention_bwd": ([C.POINTER(AttnBwdArgs), vp], i32),
     "mtts_adam_chunks": ([i64], i64),

@@ -96,6 +96,38 @@ def attention_decode_packed(q, k, v, n_heads, kpm=None):
     return yp
 
 
+def attention_decode_qproj_packed(x, wq, bq, ln_w, ln_b, eps, k, v, n_heads, kpm=None):
+    """Single-query cross-attention with the query projection fused in
+    (mtts_attention_decode_qproj): q = bf16(LN(x) wq^T + bq) per (batch,
+    head) inside the decode kernel, LN(x) = bf16(LayerNorm(x) * ln_w + ln_b)
+    as the packed projections' LayerNorm prologue computes it; k / v
+    head-major (B, H, S, hd) contiguous.  Returns the output as the packed
+    activation image of the output projection (ops.PackedAct)."""
+    from .ops import PackedAct
+    B, d = x.shape
+    if k.dim() != 4 or not (k.is_contiguous() and v.is_contiguous()):
+        raise ValueError("attention_decode_qproj_packed: head-major contiguous (B, H, S, hd) k / v")
+    if x.dtype != torch.bfloat16 or x.stride(1) != 1 or wq.dtype != torch.bfloat16 or wq.stride(1) != 1 \
+            or wq.stride(0) != d:
+        raise ValueError("attention_decode_qproj_packed: bf16 x (B, d) and row-major bf16 wq (d, d)")
+    H, S, hd = k.shape[1:]
+    m = _mask_u8(kpm, B, S)
+    yp = PackedAct.empty(B, d, x.device)
+    q3 = x[:, None]
+    a = _fwd_args(q3, k.view(B, H * S, hd), v.view(B, H * S, hd), n_heads, m, q3, None)   # no row-major out
+    a.kv_len, a.k_ls, a.v_ls, a.kv_hs = S, hd, hd, S * hd
+    a.out = 0
+    a.out_packed = yp.data.data_ptr()
+    qa = L.AttnQProjArgs()
+    qa.f = a
+    qa.x, qa.x_rs = x.data_ptr(), x.stride(0)
+    qa.wq, qa.bq = wq.data_ptr(), L.ptr(bq)
+    lw, lb = ln_w.detach().float().contiguous(), ln_b.detach().float().contiguous()
+    qa.ln_w, qa.ln_b, qa.eps, qa.d_model = lw.data_ptr(), lb.data_ptr(), float(eps), d
+    L.call("mtts_attention_decode_qproj", qa)
+    return yp
+
+
 def attention_fwd(q, k, v, n_heads, kpm=None, want_lse=False):
     """Returns (out (B, T, d) in q's dtype, lse (B, H, T) fp32 or None)."""
     for t in (q, k, v):

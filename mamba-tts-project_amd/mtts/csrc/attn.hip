@@ -1552,16 +1552,93 @@ __device__ __forceinline__ float groups_max(float v, int lane) {
   return mtts::max_xor32(v);
 }
 
-template <typename T, int HD, int U>
-__global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a) {
+// The cross-attention's query projection fused into the decode kernel
+// (round 5): q = bf16(LN(x) Wq_h^T + bq_h) for the workgroup's (batch, head),
+// with LN(x) = bf16(fmaf((x - mean) rstd, w, b)) over the residual row -- the
+// values the LayerNorm prologue of the packed projection feeds its MFMAs --
+// so the step loses the q-projection launch (mamba_decoder.py:72-77 ->
+// nn.MultiheadAttention's q = in_proj(query)[:d]).  Each workgroup reads its
+// head's Wq rows (HD x d_model bf16) from L2.
+struct QProj {
+  const mtts::bf16_t* x;      // (batch, dm) bf16 residual rows
+  int64_t x_rs;
+  const mtts::bf16_t* w;      // (heads * HD, dm) bf16, row-major
+  const mtts::bf16_t* bias;   // (heads * HD) bf16 or null
+  const float* lnw;
+  const float* lnb;
+  float eps;
+  int dm;
+};
+constexpr int kQpMaxDm = 2048;
+
+template <int HD>
+__device__ __forceinline__ void qproj_head(const QProj& qp, int b, int hh, float* sx, float* sq, float* sred) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const mtts::bf16_t* xr = qp.x + (int64_t)b * qp.x_rs;
+  const int dm = qp.dm;
+  // two passes as the LayerNorm prologue: mean, then squared deviations
+  float s = 0.f;
+  for (int i = tid; i < dm; i += 256) {
+    const float v = mtts::bf2f(xr[i]);
+    sx[i] = v;
+    s += v;
+  }
+  s = mtts::wave_sum(s);
+  if (lane == 0) sred[wave] = s;
+  block_sync();
+  const float mean = ((sred[0] + sred[1]) + (sred[2] + sred[3])) / dm;
+  float s2 = 0.f;
+  for (int i = tid; i < dm; i += 256) {
+    const float d = sx[i] - mean;
+    s2 = fmaf(d, d, s2);
+  }
+  s2 = mtts::wave_sum(s2);
+  block_sync();   // every wave read sred's means
+  if (lane == 0) sred[wave] = s2;
+  block_sync();
+  const float rstd = 1.f / sqrtf(((sred[0] + sred[1]) + (sred[2] + sred[3])) / dm + qp.eps);
+  for (int i = tid; i < dm; i += 256) sx[i] = mtts::bf2f(mtts::f2bf(fmaf((sx[i] - mean) * rstd, qp.lnw[i], qp.lnb[i])));
+  block_sync();
+  // rows of the head: 16 lanes per row (16-byte chunks, stride 256 B), 4 rows per wave and pass
+  const int l16 = lane & 15;
+#pragma unroll 1
+  for (int r0 = 0; r0 < HD; r0 += 16) {
+    const int r = r0 + wave * 4 + (lane >> 4);
+    const mtts::bf16_t* wr = qp.w + (int64_t)(hh * HD + r) * dm;
+    float acc = 0.f;
+    for (int c8 = l16; c8 < dm / 8; c8 += 16) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(wr + c8 * 8);
+      const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+      const float* xs = sx + c8 * 8;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc = fmaf(__uint_as_float(wv[e] << 16), xs[2 * e], acc);
+        acc = fmaf(__uint_as_float(wv[e] & 0xffff0000u), xs[2 * e + 1], acc);
+      }
+    }
+    acc = group_sum<16>(acc, lane);
+    if (l16 == 0) sq[r] = mtts::bf2f(mtts::f2bf(acc + (qp.bias ? mtts::bf2f(qp.bias[hh * HD + r]) : 0.f)));
+  }
+  block_sync();
+}
+
+template <typename T, int HD, int U, bool QP = false>
+__global__ __launch_bounds__(256) void attn_decode1_kernel(MttsAttnFwdArgs a, QProj qp) {
   constexpr int G = HD / 8, NG = 256 / G;
   __shared__ float swm[4], swl[4], sacc[4][HD];
+  __shared__ float sx[QP ? kQpMaxDm : 1], sq[QP ? HD : 1], sred[4];
   const int bh = blockIdx.x, b = bh / a.heads, hh = bh % a.heads;
   const int g = threadIdx.x / G, gl = threadIdx.x % G, d0 = gl * 8, wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const float c = a.scale * kLog2e;
   float q[8];
-  ld8((const T*)a.q + b * a.q_bs + hh * HD + d0, q);
+  if constexpr (QP) {
+    qproj_head<HD>(qp, b, hh, sx, sq, sred);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = sq[d0 + e];
+  } else {
+    ld8((const T*)a.q + b * a.q_bs + hh * HD + d0, q);
+  }
   const int64_t hs = a.kv_hs ? a.kv_hs : HD;
   const T* kb = (const T*)a.k + b * a.k_bs + hh * hs + d0;
   const T* vb = (const T*)a.v + b * a.v_bs + hh * hs + d0;
@@ -1624,9 +1701,20 @@ template <typename T, int HD>
 void launch_decode(const MttsAttnFwdArgs* a, hipStream_t st) {
   constexpr int NG = 256 / (HD / 8);
   const dim3 grid(a->batch * a->heads);
-  if (a->kv_len <= 4 * NG) hipLaunchKernelGGL((attn_decode1_kernel<T, HD, 4>), grid, dim3(256), 0, st, *a);
-  else if (a->kv_len <= 8 * NG) hipLaunchKernelGGL((attn_decode1_kernel<T, HD, 8>), grid, dim3(256), 0, st, *a);
+  const QProj none{};
+  if (a->kv_len <= 4 * NG) hipLaunchKernelGGL((attn_decode1_kernel<T, HD, 4>), grid, dim3(256), 0, st, *a, none);
+  else if (a->kv_len <= 8 * NG) hipLaunchKernelGGL((attn_decode1_kernel<T, HD, 8>), grid, dim3(256), 0, st, *a, none);
   else hipLaunchKernelGGL((attn_decode_kernel<T, HD>), grid, dim3(256), 0, st, *a);
+}
+
+template <int HD>
+void launch_decode_qp(const MttsAttnFwdArgs* a, const QProj& qp, hipStream_t st) {
+  constexpr int NG = 256 / (HD / 8);
+  const dim3 grid(a->batch * a->heads);
+  if (a->kv_len <= 4 * NG)
+    hipLaunchKernelGGL((attn_decode1_kernel<mtts::bf16_t, HD, 4, true>), grid, dim3(256), 0, st, *a, qp);
+  else
+    hipLaunchKernelGGL((attn_decode1_kernel<mtts::bf16_t, HD, 8, true>), grid, dim3(256), 0, st, *a, qp);
 }
 
 template <typename T>
@@ -1760,6 +1848,36 @@ extern "C" int mtts_attention_fwd(const MttsAttnFwdArgs* a, void* stream) {
   else
     one ? dispatch_decode<float>(a, st) : dispatch_fwd<float>(a, st);
   MTTS_LAUNCH_CHECK("attention_fwd");
+  return MTTS_OK;
+}
+
+extern "C" int mtts_attention_decode_qproj(const MttsAttnQProjArgs* q, void* stream) {
+  MTTS_CHECK(q, "attention_decode_qproj: null args");
+  MttsAttnFwdArgs a = q->f;
+  MTTS_CHECK(a.out || a.out_packed, "attention_decode_qproj: null out and out_packed");
+  {   // check_fwd on the k / v / mask side; q is computed in the kernel, out may be packed only
+    MttsAttnFwdArgs c = a;
+    c.q = q->x;
+    c.q_bs = c.q_ls = 0;
+    if (!c.out) { c.out = c.out_packed; c.o_bs = c.o_ls = 0; }
+    int rc = check_fwd(&c, "attention_decode_qproj");
+    if (rc) return rc;
+  }
+  const int NG = 256 / (a.head_dim / 8);
+  MTTS_CHECK(a.q_len == 1 && a.dtype == MTTS_BF16 && a.kv_len <= 8 * NG && a.batch <= 32 &&
+                 (a.heads * a.head_dim) % 32 == 0 && (a.head_dim == 64 || a.head_dim == 128),
+             "attention_decode_qproj: q_len 1, bf16, head_dim 64 / 128, batch <= 32, kv_len <= %d", 8 * NG);
+  MTTS_CHECK(q->x && q->wq && q->ln_w && q->ln_b, "attention_decode_qproj: null x / wq / ln_w / ln_b");
+  MTTS_CHECK(q->d_model > 0 && q->d_model <= kQpMaxDm && q->d_model % 8 == 0 && q->x_rs >= q->d_model &&
+                 ((uintptr_t)q->wq % 16) == 0,
+             "attention_decode_qproj: d_model %d (<= %d, multiple of 8) / 16-byte aligned wq", q->d_model, kQpMaxDm);
+  if (a.batch == 0) return MTTS_OK;
+  QProj qp{(const bf16_t*)q->x, q->x_rs, (const bf16_t*)q->wq, (const bf16_t*)q->bq, q->ln_w, q->ln_b, q->eps,
+           q->d_model};
+  hipStream_t st = (hipStream_t)stream;
+  if (a.head_dim == 64) launch_decode_qp<64>(&a, qp, st);
+  else launch_decode_qp<128>(&a, qp, st);
+  MTTS_LAUNCH_CHECK("attention_decode_qproj");
   return MTTS_OK;
 }
 

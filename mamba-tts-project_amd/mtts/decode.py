@@ -33,7 +33,7 @@ import torch.nn.functional as F
 from . import _lib as L
 from . import ops
 from .embed import _err_flag
-from .attn_kernels import attention, attention_decode_packed
+from .attn_kernels import attention, attention_decode_packed, attention_decode_qproj_packed
 from .linear import cast_weight
 
 
@@ -71,7 +71,13 @@ class DecodeEngine:
                "fused": True,      # fused-epilogue step (LN prologues, residual / conv epilogues)
                "fuse_conv": True,  # conv update in in_proj's epilogue
                "packed": True,     # weights re-laid in MFMA fragment order (gemv16)
-               "xpacked": True}    # activation images packed too
+               "xpacked": True,    # activation images packed too
+               # cross-attention LN + q projection inside the decode attention kernel
+               # (mtts_attention_decode_qproj): measured 1.13 vs 0.76 ms p50 per
+               # step (profiles/r05_decode_ab_fuse_q.txt) -- every (batch, head)
+               # workgroup re-reads its head's Wq rows (256 KiB) from L2, 64 MiB
+               # per layer against 2 MiB for one projection over the 32 rows
+               "fuse_q": False}
 
     def __init__(self, model, use_graph=True, use_rows=True):
         self.m = model
@@ -94,6 +100,7 @@ class DecodeEngine:
         self._err_ev = None
         self._err_dev = None
         self.xpk = False
+        self.fuse_q = False
         self.ctx_key = None
         self.ctx_refs = None
         self.ctx_versions = None
@@ -259,6 +266,17 @@ class DecodeEngine:
                 p["beta_p"] = ops.PackedAct.pack(p["beta"])
         return True
 
+    def _fuse_q_ok(self, B):
+        """Shapes mtts_attention_decode_qproj takes (head_dim 64 / 128,
+        d_model <= 2048, <= 32 sequences, the single-pass key range)."""
+        for l, p in zip(self.m.layers, self.ctx["layers"]):
+            ca = l.cross_attn
+            hd = ca.embed_dim // ca.num_heads
+            if (hd not in (64, 128) or ca.embed_dim > 2048 or ca.embed_dim % 8 or B > 32
+                    or p["khm"].shape[2] > 8 * (256 // (hd // 8)) or p["Wq"].stride(0) != ca.embed_dim):
+                return False
+        return True
+
     def _step_xpk(self, x, states, ln):
         """_step_rows with packed activations (csrc/gemv.hip, common.h
         xpk_index): every producer writes the packed image of what the next
@@ -283,8 +301,13 @@ class DecodeEngine:
             y = ops.state_update(ssm_state, u, x_dbl[:, :r], p["A"], x_dbl[:, r:r + N], x_dbl[:, r + N:], p["D"],
                                  xz[:, di:], p["dt_bias"], True, dt_w=p["Wdt"], packed_out=True)
             x, xp = ops.gemm_rows(y, p["Wout_p"], res=x, packed_out="also")
-            q = ops.gemm_rows(xp, p["Wq_p"], p["bq"], ln=ln(l.norm_cross))
-            o = attention_decode_packed(q, p["khm"], p["vhm"], l.cross_attn.num_heads, c["kpm"])
+            if self.fuse_q:   # one launch: LN + q projection in the attention kernel's prologue
+                nc = l.norm_cross
+                o = attention_decode_qproj_packed(x, p["Wq"], p["bq"], nc.weight, nc.bias, nc.eps, p["khm"],
+                                                  p["vhm"], l.cross_attn.num_heads, c["kpm"])
+            else:
+                q = ops.gemm_rows(xp, p["Wq_p"], p["bq"], ln=ln(l.norm_cross))
+                o = attention_decode_packed(q, p["khm"], p["vhm"], l.cross_attn.num_heads, c["kpm"])
             x, xp = ops.gemm_rows(o, p["Wo_p"], p["bo"], res=x, packed_out="also")
             f = ops.gemm_rows(xp, p["W1_p"], p["b1"], "gelu", ln=ln(l.norm_ff, p["gamma_p"], p["beta_p"]),
                               packed_out="only")
@@ -377,6 +400,7 @@ class DecodeEngine:
             if self.fused and self.OPTIONS["packed"]:
                 self._pack_ctx()
             self.xpk = self.fused and self._xpk_ok()
+            self.fuse_q = self.xpk and self.OPTIONS["fuse_q"] and self._fuse_q_ok(last_token.shape[0])
             self.graph = None
             self.states = None
         B = last_token.shape[0]

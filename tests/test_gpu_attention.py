@@ -10,6 +10,7 @@ import os
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
@@ -328,3 +329,35 @@ def test_decode_head_major_kv_matches_channel_last(B, S, H, hd):
     vhm = v.reshape(B, S, H, hd).permute(0, 2, 1, 3).contiguous()
     b = attention_decode_packed(q, khm, vhm, H, kpm)
     assert torch.equal(a.unpack(), b.unpack())
+
+
+@pytest.mark.parametrize("B,S,H,hd,d", [(32, 128, 8, 128, 1024), (5, 77, 16, 64, 1024), (3, 200, 4, 64, 256)])
+def test_decode_qproj_fused_matches_projection_then_attention(B, S, H, hd, d):
+    """mtts_attention_decode_qproj (the decode step's LayerNorm + q
+    projection inside the single-query attention kernel) against the
+    unfused packed path it replaces -- ops.gemm_rows with the LayerNorm
+    prologue, then attention_decode_packed -- and against an fp32 torch
+    composition.  The q values may round differently by one bf16 ulp (a
+    different summation order): 2e-2 of the output scale."""
+    from mtts import ops
+    from mtts.attn_kernels import attention_decode_packed, attention_decode_qproj_packed
+    g = torch.Generator(device="cpu").manual_seed(B + S + H + d)
+    x = torch.randn(B, d, generator=g).to("cuda", torch.bfloat16)
+    wq = (torch.randn(H * hd, d, generator=g) / d ** 0.5).to("cuda", torch.bfloat16)
+    bq = (0.1 * torch.randn(H * hd, generator=g)).to("cuda", torch.bfloat16)
+    lnw = (1 + 0.1 * torch.randn(d, generator=g)).cuda()
+    lnb = (0.1 * torch.randn(d, generator=g)).cuda()
+    kv = torch.randn(B, S, 2 * H * hd, generator=g).to("cuda", torch.bfloat16)
+    kpm = torch.zeros(B, S, dtype=torch.bool, device="cuda")
+    kpm[:, S - 7:] = True
+    dd = H * hd
+    khm = kv[..., :dd].reshape(B, S, H, hd).permute(0, 2, 1, 3).contiguous()
+    vhm = kv[..., dd:].reshape(B, S, H, hd).permute(0, 2, 1, 3).contiguous()
+    fused = attention_decode_qproj_packed(x, wq, bq, lnw, lnb, 1e-5, khm, vhm, H, kpm).unpack().float()
+    q = ops.gemm_rows(x, wq, bq, ln=(lnw, lnb, 1e-5, None, None))
+    unfused = attention_decode_packed(q, khm, vhm, H, kpm).unpack().float()
+    xn = F.layer_norm(x.float(), (d,), lnw, lnb, 1e-5).bfloat16().float()
+    qr = (xn @ wq.float().t() + bq.float()).bfloat16()
+    ref, _ = ref_attention(qr[:, None], kv[..., :dd], kv[..., dd:], H, kpm)
+    close(fused, unfused.double(), 2e-2)
+    close(fused, ref[:, 0], 2e-2)

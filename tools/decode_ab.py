@@ -81,6 +81,8 @@ def step(modes=(True, False)):
     print({("rows" if k else "hipBLASLt"): v for k, v in res.items()}, "p50 ms", flush=True)
 
 
+DEFAULTS = dict(DecodeEngine.OPTIONS)
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["shapes", "step"]
     if "shapes" in what:
@@ -98,7 +100,7 @@ if __name__ == "__main__":
                     DecodeEngine.OPTIONS[key] = v
                     print(key, v, end=" ", flush=True)
                     step((True,))
-            DecodeEngine.OPTIONS[key] = True
+            DecodeEngine.OPTIONS[key] = DEFAULTS[key]
     if "splitk" in what:   # rows kernels with / without the cross-workgroup K split, interleaved
         for _ in range(2):
             for sk in (True, False):
