@@ -648,12 +648,15 @@ int mtts_gemm_grouped(const MttsGemmArgs* probs, int n, void* stream);
  * (T + 2p) C, row_stride = C, a row of K*C elements is the conv window.
  *   NT: C[m,n] = sum_k A[row m][k] B[row n][k]
  *   TN: C[m,n] = sum_k A[row k][m] B[row k][n]
+ *   NN: C[m,n] = sum_k A[row m][k] B[row k][n]  (MTTS_CONVGEMM_NN: the data
+ *       gradient straight from the forward's weight layout, no transpose)
  * C rows through the same map (n contiguous).  fp32 everywhere, exact-f32
  * MFMA products, fp32 accumulation.  n % 4 == 0; NT k % 4 == 0, TN m % 4 ==
  * 0; 16-byte aligned pointers, strides multiples of 4 elements.  Epilogues
  * (bf16 GEMM's not reused: fp32 out): + bias[n]; ReLU; ReLU backward
  * (C = result where aux[row m][n] > 0, else 0); beta: C = result + beta C.
  * ------------------------------------------------------------------------ */
+#define MTTS_CONVGEMM_NN 2   /* convgemm only: C[m,n] = sum_k A[row m][k] B[row k][n] */
 #define MTTS_CONVGEMM_BIAS 1
 #define MTTS_CONVGEMM_RELU 2
 #define MTTS_CONVGEMM_DRELU 4
@@ -662,7 +665,7 @@ typedef struct {
   int64_t seg_rows, seg_stride, row_stride;
 } MttsRowMap;
 typedef struct {
-  int layout;                /* MTTS_GEMM_NT / MTTS_GEMM_TN */
+  int layout;                /* MTTS_GEMM_NT / MTTS_GEMM_TN / MTTS_CONVGEMM_NN */
   int m, n, k;
   MttsRowMap a, b, c, aux;   /* aux: the ReLU output for MTTS_CONVGEMM_DRELU */
   const float* bias;

@@ -9,11 +9,14 @@ text_encoder.py:80-85 (FFT blocks), 118-122 (encoder) and 131-209 (duration
 predictor).  All fp32 as the reference runs them.
 
 A convolution over channel-last x (B, T, C) with weight (O, C, K), padding p
-(2p = K - 1, the reference's 'same' convolutions):
-  forward   y[b, t] = W(O, K*C) . x_pad[b, t .. t+K-1, :]          NT, windowed A
-  data grad dx[b, s] = Wflip(C, K*O) . dy_pad[b, s .. s+K-1, :]    NT, windowed A
-  weight    dW(O, K*C) = dy^T . window(x_pad)                       TN, windowed B
-No unfold copy: the zero-padded activation's rows overlap as GEMM rows.
+(2p = K - 1, the reference's 'same' convolutions) and Wf = W as (O, K*C)
+([o][k][c], made once by the forward and kept for the backward):
+  forward   y[b, t] = Wf . x_pad[b, t .. t+K-1, :]                 NT, windowed A
+  data grad dx[b, s] = sum_{j,o} dy_pad[b, s + j, o] Wf[o][K-1-j]   NN, windowed A,
+            B row (j, o) = Wf[o, (K-1-j) C ..] (a row map with a negative segment stride)
+  weight    dWf = dy^T . window(x_pad)                              TN, windowed B
+No unfold copy (the zero-padded activation's rows overlap as GEMM rows) and
+no transposed / flipped weight copy.
 """
 from __future__ import annotations
 
@@ -25,7 +28,7 @@ import torch.nn.functional as F
 from . import _lib as L
 from .linear import colsum
 
-NT, TN = 0, 1
+NT, TN, NN = 0, 1, 2
 EPI_BIAS, EPI_RELU, EPI_DRELU = 1, 2, 4
 
 
@@ -83,38 +86,57 @@ def _pad(x: torch.Tensor, p: int) -> torch.Tensor:
     return F.pad(x, (0, 0, p, p)) if p else x
 
 
+def _wf(weight):
+    O, C, K = weight.shape
+    return weight.view(O, C) if K == 1 else weight.permute(0, 2, 1).reshape(O, K * C).contiguous()
+
+
 def conv_forward(x, weight, bias, relu):
-    """y (B, T, O) = [relu](conv(x, weight) + bias); x (B, T, C) contiguous fp32."""
+    """y (B, T, O) = [relu](conv(x, weight) + bias); x (B, T, C) contiguous fp32.
+    Returns (y, x_pad, Wf)."""
     B, T, C = x.shape
     O, _, K = weight.shape
     p = (K - 1) // 2
     xp = _pad(x, p)
-    wf = weight.permute(0, 2, 1).reshape(O, K * C) if K > 1 else weight.view(O, C)
-    wf = wf.contiguous()
+    wf = _wf(weight)
     y = torch.empty(B, T, O, device=x.device, dtype=torch.float32)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0)
     gemm(NT, B * T, O, K * C, _window(xp, T), _plain(wf), _plain(y.view(B * T, O)), bias=bias, epilogue=epi)
-    return y, xp
+    return y, xp, wf
 
 
-def conv_backward(dy, xp, weight, need_dx, need_dw, need_db, relu_out=None):
-    """Gradients of y = conv(x) (+ bias) for dy (B, T, O); with `relu_out` (the
-    forward's ReLU output) dy is first masked by relu_out > 0 -- that mask is
-    fused into the data-gradient epilogue of the layer that PRODUCED dy when
-    the caller does it (ConvFFNFn), else applied here."""
+def _wflip_map(wf, K):
+    """B rows (j, o) = Wf[o, (K-1-j) C : (K-j) C] of the data gradient."""
+    O, KC = wf.shape
+    C = KC // K
+    base = wf[:, (K - 1) * C:] if K > 1 else wf
+    return _map(base, O, -C, KC)
+
+
+def dgrad(dy, wf, K, epilogue=0, aux=None):
+    """dx (B, T, C) of a 'same' convolution for dy (B, T, O) contiguous."""
     B, T, O = dy.shape
-    _, C, K = weight.shape
-    p = (K - 1) // 2
+    C = wf.shape[1] // K
+    dyp = _pad(dy, (K - 1) // 2)
+    dx = torch.empty(B, T, C, device=dy.device, dtype=torch.float32)
+    gemm(NN, B * T, C, K * O, _window(dyp, T), _wflip_map(wf, K), _plain(dx.view(B * T, C)), epilogue=epilogue,
+         aux=aux)
+    return dx
+
+
+def conv_backward(dy, xp, wf, K, need_dx, need_dw, need_db, relu_out=None):
+    """Gradients of y = conv(x) (+ bias) for dy (B, T, O); with `relu_out` (the
+    forward's ReLU output) dy is first masked by relu_out > 0 (ConvFFNFn fuses
+    that mask into the data-gradient epilogue of the layer that produced dy
+    instead).  Returns dx, dW (O, C, K), db."""
+    B, T, O = dy.shape
+    C = wf.shape[1] // K
     if relu_out is not None:
         dy = torch.where(relu_out > 0, dy, torch.zeros((), device=dy.device))
     dy = dy.contiguous()
     dx = dw = db = None
     if need_dx:
-        wd = weight.flip(2).permute(1, 2, 0).reshape(C, K * O).contiguous() if K > 1 else \
-            weight.view(O, C).t().contiguous()
-        dyp = _pad(dy, p)
-        dx = torch.empty(B, T, C, device=dy.device, dtype=torch.float32)
-        gemm(NT, B * T, C, K * O, _window(dyp, T), _plain(wd), _plain(dx.view(B * T, C)))
+        dx = dgrad(dy, wf, K)
     if need_dw:
         dwf = torch.empty(O, K * C, device=dy.device, dtype=torch.float32)
         gemm(TN, O, K * C, B * T, _plain(dy.view(B * T, O)), _window(xp, T), _plain(dwf))
@@ -129,16 +151,16 @@ class Conv1dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, relu):
-        y, xp = conv_forward(x, weight, bias, relu)
-        ctx.relu = relu
-        ctx.save_for_backward(xp, weight, y if relu else None)
+        y, xp, wf = conv_forward(x, weight, bias, relu)
+        ctx.relu, ctx.K = relu, weight.shape[2]
+        ctx.save_for_backward(xp, wf, y if relu else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xp, weight, y = ctx.saved_tensors
+        xp, wf, y = ctx.saved_tensors
         need = ctx.needs_input_grad
-        dx, dw, db = conv_backward(dy, xp, weight, need[0], need[1], need[2], relu_out=y if ctx.relu else None)
+        dx, dw, db = conv_backward(dy, xp, wf, ctx.K, need[0], need[1], need[2], relu_out=y if ctx.relu else None)
         return dx, dw, db, None
 
 
@@ -149,31 +171,26 @@ class ConvFFNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
-        h, xp = conv_forward(x, w1, b1, True)
-        out, hp = conv_forward(h, w2, b2, False)
-        ctx.save_for_backward(xp, w1, hp, w2)
+        h, xp, wf1 = conv_forward(x, w1, b1, True)
+        out, hp, wf2 = conv_forward(h, w2, b2, False)
+        ctx.save_for_backward(xp, wf1, hp, wf2)
+        ctx.K = (w1.shape[2], w2.shape[2])
         ctx.has_b = (b1 is not None, b2 is not None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        xp, w1, hp, w2 = ctx.saved_tensors
+        xp, wf1, hp, wf2 = ctx.saved_tensors
+        K1, K2 = ctx.K
         need = ctx.needs_input_grad
         dout = dout.contiguous()
         B, T, O = dout.shape
-        _, H, K2 = w2.shape
         p2 = (K2 - 1) // 2
-        h = hp[:, p2:p2 + T] if p2 else hp
+        h = (hp[:, p2:p2 + T] if p2 else hp).contiguous()
         # dh = (dout conv2^T) * (h > 0): conv2's data gradient with the ReLU mask in its epilogue
-        wd2 = w2.flip(2).permute(1, 2, 0).reshape(H, K2 * O).contiguous() if K2 > 1 else \
-            w2.view(O, H).t().contiguous()
-        dyp = _pad(dout, p2)
-        dh = torch.empty(B, T, H, device=dout.device, dtype=torch.float32)
-        hc = h.contiguous()
-        gemm(NT, B * T, H, K2 * O, _window(dyp, T), _plain(wd2), _plain(dh.view(B * T, H)),
-             epilogue=EPI_DRELU, aux=_plain(hc.view(B * T, H)))
-        _, dw2, db2 = conv_backward(dout, hp, w2, False, need[3], need[4] and ctx.has_b[1])
-        dx, dw1, db1 = conv_backward(dh, xp, w1, need[0], need[1], need[2] and ctx.has_b[0])
+        dh = dgrad(dout, wf2, K2, epilogue=EPI_DRELU, aux=_plain(h.view(B * T, h.shape[2])))
+        _, dw2, db2 = conv_backward(dout, hp, wf2, K2, False, need[3], need[4] and ctx.has_b[1])
+        dx, dw1, db1 = conv_backward(dh, xp, wf1, K1, need[0], need[1], need[2] and ctx.has_b[0])
         return dx, dw1, db1, dw2, db2
 
 
@@ -209,10 +226,9 @@ class LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, O).contiguous()
         need = ctx.needs_input_grad
         dx = dw = db = None
-        if need[0]:
-            wt = weight.t().contiguous()
+        if need[0]:   # NN: the weight's rows are the k-rows, no transpose copy
             dx = torch.empty(x2.shape[0], C, device=dy.device, dtype=torch.float32)
-            gemm(NT, x2.shape[0], C, O, _plain(dy2), _plain(wt), _plain(dx))
+            gemm(NN, x2.shape[0], C, O, _plain(dy2), _plain(weight), _plain(dx))
             dx = dx.view(*dy.shape[:-1], C)
         if need[1]:
             dw = torch.empty(O, C, device=dy.device, dtype=torch.float32)

@@ -150,7 +150,8 @@ struct TnLoad {
 template <int LAYOUT>
 __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
   constexpr bool NT = LAYOUT == MTTS_GEMM_NT;
-  constexpr int kTile = NT ? kNtTile : kTnTile;
+  constexpr bool NN = LAYOUT == MTTS_CONVGEMM_NN;   // A as NT, B as TN
+  constexpr int kTile = NT ? kNtTile : kTnTile;     // NN: A uses the first kNtTile floats
   __shared__ __attribute__((aligned(16))) float lds[2][2][kTile];   // [buffer][A / B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -162,31 +163,22 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
 
   NtLoad na, nb;
   TnLoad tl;
-  if constexpr (NT) {
-    na.init(p.a, m0, p.m, tid);
-    nb.init(p.b, n0, p.n, tid);
-  } else {
-    tl.init(tid);
-  }
+  if constexpr (NT || NN) na.init(p.a, m0, p.m, tid);
+  if constexpr (NT) nb.init(p.b, n0, p.n, tid);
+  if constexpr (!NT) tl.init(tid);
   f32x4 va[kLd], vb[kLd];
   auto load = [&](int kt) {
     const int k0 = kbeg + kt * kBK;
-    if constexpr (NT) {
-      na.load(va, k0, kend);
-      nb.load(vb, k0, kend);
-    } else {
-      tl.load(va, p.a, k0, kend, m0, p.m);
-      tl.load(vb, p.b, k0, kend, n0, p.n);
-    }
+    if constexpr (NT || NN) na.load(va, k0, kend);
+    else tl.load(va, p.a, k0, kend, m0, p.m);
+    if constexpr (NT) nb.load(vb, k0, kend);
+    else tl.load(vb, p.b, k0, kend, n0, p.n);
   };
   auto store = [&](int buf) {
-    if constexpr (NT) {
-      na.store(lds[buf][0], va);
-      nb.store(lds[buf][1], vb);
-    } else {
-      tl.store(lds[buf][0], va);
-      tl.store(lds[buf][1], vb);
-    }
+    if constexpr (NT || NN) na.store(lds[buf][0], va);
+    else tl.store(lds[buf][0], va);
+    if constexpr (NT) nb.store(lds[buf][1], vb);
+    else tl.store(lds[buf][1], vb);
   };
 
   f32x4 acc[4][4];
@@ -231,7 +223,12 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
         float fa[4], fb[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          fa[i] = ta[kr * kTnPitch + wr * 64 + i * 16 + r16];
+          if constexpr (NN) {   // A from the swizzled NT image, one element per lane
+            const int ra = wr * 64 + i * 16 + r16;
+            fa[i] = ta[ra * kBK + (((kr >> 2) ^ (ra & 7)) << 2) + (kr & 3)];
+          } else {
+            fa[i] = ta[kr * kTnPitch + wr * 64 + i * 16 + r16];
+          }
           fb[i] = tb[kr * kTnPitch + wc * 64 + i * 16 + r16];
         }
 #pragma unroll
@@ -286,12 +283,14 @@ using namespace mtts;
 extern "C" int mtts_convgemm(const MttsConvGemmArgs* a, void* stream) {
   MTTS_CHECK(a, "convgemm: null args");
   MTTS_CHECK(a->m > 0 && a->n > 0 && a->k > 0, "convgemm: m=%d n=%d k=%d must be positive", a->m, a->n, a->k);
-  MTTS_CHECK(a->layout == MTTS_GEMM_NT || a->layout == MTTS_GEMM_TN, "convgemm: layout must be NT (0) or TN (1)");
-  const bool nt = a->layout == MTTS_GEMM_NT;
+  MTTS_CHECK(a->layout == MTTS_GEMM_NT || a->layout == MTTS_GEMM_TN || a->layout == MTTS_CONVGEMM_NN,
+             "convgemm: layout must be NT (0), TN (1) or NN (2)");
+  const bool nt = a->layout == MTTS_GEMM_NT, nn = a->layout == MTTS_CONVGEMM_NN;
   MTTS_CHECK(map_ok(a->a) && map_ok(a->b) && map_ok(a->c),
              "convgemm: operands need a pointer, seg_rows > 0, 16-byte alignment and strides a multiple of 4");
   MTTS_CHECK(a->n % 4 == 0, "convgemm: n=%d must be a multiple of 4", a->n);
-  MTTS_CHECK(nt ? a->k % 4 == 0 : a->m % 4 == 0, "convgemm: %s must be a multiple of 4", nt ? "k" : "m");
+  MTTS_CHECK((nt || nn) ? a->k % 4 == 0 : a->m % 4 == 0, "convgemm: %s must be a multiple of 4",
+             (nt || nn) ? "k" : "m");
   MTTS_CHECK(!(a->epilogue & MTTS_CONVGEMM_BIAS) || (a->bias && (uintptr_t)a->bias % 16 == 0),
              "convgemm: bias epilogue needs a 16-byte aligned bias");
   MTTS_CHECK(!(a->epilogue & MTTS_CONVGEMM_DRELU) || map_ok(a->aux), "convgemm: ReLU-backward epilogue needs aux");
@@ -321,6 +320,7 @@ extern "C" int mtts_convgemm(const MttsConvGemmArgs* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const unsigned grid = (unsigned)(tiles * splits);
   if (nt) hipLaunchKernelGGL(convgemm_kernel<MTTS_GEMM_NT>, dim3(grid), dim3(kT), 0, st, p);
+  else if (nn) hipLaunchKernelGGL(convgemm_kernel<MTTS_CONVGEMM_NN>, dim3(grid), dim3(kT), 0, st, p);
   else hipLaunchKernelGGL(convgemm_kernel<MTTS_GEMM_TN>, dim3(grid), dim3(kT), 0, st, p);
   MTTS_LAUNCH_CHECK("convgemm");
   if (splits > 1) {

@@ -39,17 +39,24 @@ def _free_port():
     return p
 
 
-def _setup(grad_allreduce_factory=None):
+# train.py's widths (d_model 512, d_style 256, 8 heads, text encoder 4 x FFT
+# 2 x 64, conv 1024, duration filter 256) on a 2-layer bf16 decoder
+WIDE = dict(dec_layers=2, compute_dtype=torch.bfloat16, dropout=0.0, max_len=1024)
+CONFIGS = {"small": (SMALL, dict(T_text=12, T_codec=24, T_ref=16, d_style=SMALL["d_style"])),
+           "wide": (WIDE, dict(T_text=24, T_codec=64, T_ref=32))}
+
+
+def _setup(grad_allreduce_factory=None, cfg="small"):
     import train_harness as th
+    kw, bkw = CONFIGS[cfg]
     torch.manual_seed(0)
-    models = th.build_models("cuda", **SMALL)
+    models = th.build_models("cuda", **kw)
     dp = None
     if grad_allreduce_factory is not None:
         params = [p for m in models for p in m.parameters() if p.requires_grad]
         dp = grad_allreduce_factory(params)
     step = th.TrainStep(models, lr=LR, grad_allreduce=dp)
-    batch = th.synthetic_batch(WORLD * SHARD, "cuda", T_text=12, T_codec=24, T_ref=16, d_style=SMALL["d_style"],
-                               seed=5)
+    batch = th.synthetic_batch(WORLD * SHARD, "cuda", seed=5, **bkw)
     return models, step, dp, batch
 
 
@@ -64,7 +71,7 @@ def _named(models):
             if p.requires_grad}
 
 
-def _worker(rank, port, q):
+def _worker(rank, port, q, cfg="small"):
     import sys
     import traceback
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -75,7 +82,8 @@ def _worker(rank, port, q):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=WORLD)
         from mtts.dp import GradAllReduce
-        models, step, dp, batch = _setup(lambda ps: GradAllReduce(ps, bucket_mb=0.05, first_bucket_mb=0.01))
+        mb = 0.05 if cfg == "small" else 4.0
+        models, step, dp, batch = _setup(lambda ps: GradAllReduce(ps, bucket_mb=mb, first_bucket_mb=mb / 5), cfg)
         mine = _shard(batch, rank)
         grads = None
         for it in range(2):
@@ -93,11 +101,18 @@ def _worker(rank, port, q):
         raise
 
 
-def test_c5_train_step_dp_world2_matches_single_process_mean_loss():
+@pytest.mark.parametrize("cfg", ["small", "wide"])
+def test_c5_train_step_dp_world2_matches_single_process_mean_loss(cfg):
+    """small: fp32 everywhere, gradients to 1e-5.  wide (train.py's widths,
+    bf16 decoder): the decoder's gradients differ between the per-shard and
+    the joint graph by bf16 roundings of the activation gradients (as in
+    test_gpu_wgrad's world-2 test): 2e-2 of each tensor's max; the fp32
+    text encoder / duration predictor to 1e-5 (their gradients come from the
+    duration loss alone); parameters after two Adam steps within 4 lr."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, cfg)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = [q.get(timeout=150) for _ in range(WORLD)]
@@ -110,7 +125,7 @@ def test_c5_train_step_dp_world2_matches_single_process_mean_loss():
     for p in procs:
         assert p.exitcode == 0
 
-    models, step, _, batch = _setup()
+    models, step, _, batch = _setup(cfg=cfg)
     named = _named(models)
     ref_grads = None
     for _ in range(2):
@@ -133,9 +148,11 @@ def test_c5_train_step_dp_world2_matches_single_process_mean_loss():
             else:
                 assert g_ref is not None, n
                 g_err = (g - g_ref).abs().max().item()
-                assert g_err <= 1e-5 * max(g_ref.abs().max().item(), 1e-6), f"rank {rank} grad {n}: {g_err:.3e}"
+                tol = 2e-2 if (cfg == "wide" and n.startswith("dec.")) else 1e-5
+                assert g_err <= tol * max(g_ref.abs().max().item(), 1e-6), f"rank {rank} grad {n}: {g_err:.3e}"
             err = (torch.from_numpy(got[n]) - p.detach().cpu()).abs()
             # Adam normalises an update to ~lr: an element whose gradient is at
             # rounding level may flip sign on one side (<= 2 lr per step)
             assert err.max().item() <= 4 * LR, f"rank {rank} {n}: {err.max().item():.3e}"
-            assert (err > 1e-5).float().mean().item() <= 2e-3, f"rank {rank} {n}: too many differing elements"
+            if cfg == "small":
+                assert (err > 1e-5).float().mean().item() <= 2e-3, f"rank {rank} {n}: too many differing elements"

@@ -1,5 +1,5 @@
 """fp32 windowed-row MFMA GEMM (csrc/convgemm.hip, mtts.convgemm) against
-torch fp32: plain NT / TN products (one workgroup per tile and split-K) with
+torch fp32: plain NT / TN / NN products (one workgroup per tile and split-K) with
 ragged edges and every epilogue,
 'same' convolutions (k = 9 / 3 / 1) forward and backward against
 F.conv1d's autograd, the fused conv FFN against its unfused composition, and
@@ -41,6 +41,9 @@ def test_nt_tn_plain_and_epilogues(m, n, k):
     c.copy_(before)
     CG.gemm(CG.NT, m, n, k, CG._plain(a), CG._plain(b), CG._plain(c), beta=1.0)
     assert rel(c, ref + before) < 1e-5
+    bkn = torch.randn(k, n, device=dev)   # NN: C = A B with B row-major (k, n)
+    CG.gemm(CG.NN, m, n, k, CG._plain(a), CG._plain(bkn), CG._plain(c))
+    assert rel(c, a @ bkn) < 1e-5
     if m % 4 == 0:   # TN: C = A^T B over row-major (k, m) / (k, n)
         at, bt = torch.randn(k, m, device=dev), torch.randn(k, n, device=dev)
         CG.gemm(CG.TN, m, n, k, CG._plain(at), CG._plain(bt), CG._plain(c))

@@ -31,11 +31,11 @@ for (C, O, K) in [(512, 1024, 9), (1024, 512, 1), (512, 384, 1), (128, 512, 1), 
     w = torch.randn(O, C, K, device="cuda") / (C * K) ** 0.5
     b = torch.randn(O, device="cuda")
     dy = torch.randn(B, T, O, device="cuda")
-    y, xp = CG.conv_forward(x, w, b, False)
+    y, xp, wf = CG.conv_forward(x, w, b, False)
     fl = 2.0 * B * T * O * C * K
     t_f = timed(lambda: CG.conv_forward(x, w, b, False))
-    t_dx = timed(lambda: CG.conv_backward(dy, xp, w, True, False, False))
-    t_dw = timed(lambda: CG.conv_backward(dy, xp, w, False, True, False))
+    t_dx = timed(lambda: CG.conv_backward(dy, xp, wf, K, True, False, False))
+    t_dw = timed(lambda: CG.conv_backward(dy, xp, wf, K, False, True, False))
     xt = x.transpose(1, 2).contiguous()
     t_tf = timed(lambda: F.conv1d(xt, w, b, padding=(K - 1) // 2))
     print(f"C{C} O{O} K{K}: fwd {t_f:6.1f} us {fl / t_f / 1e6:5.1f} TF/s | dgrad {t_dx:6.1f} us {fl / t_dx / 1e6:5.1f} | "
