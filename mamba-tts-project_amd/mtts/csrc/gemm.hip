@@ -145,6 +145,35 @@ __device__ __forceinline__ float gelu_f(float x) {
   const float h = __builtin_amdgcn_exp2f(fmaf(x * (-0.5f * kLog2e), x, gelu_tail_s(a)));
   return x * (x >= 0.f ? 1.f - h : h);
 }
+// The same two functions on two values at once: the polynomial and the
+// argument arithmetic as packed f32 (v_pk_fma_f32 / v_pk_mul_f32, each lane's
+// fma exactly the scalar one: bit-identical results at half the VALU issues)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_tail_s2(f32x2 a) {
+  f32x2 s = f32x2{-1.7774024116e-08f, -1.7774024116e-08f};
+  const float c[10] = {5.6194854933e-07f, -7.6223902631e-06f, 5.5893204013e-05f, -2.0454518331e-04f,
+                       -1.6655060660e-04f, 7.1668288485e-03f, -5.2604280745e-02f, 2.6218665810e-01f,
+                       -1.1511125488e+00f, -9.9999981719e-01f};
+#pragma unroll
+  for (int i = 0; i < 10; ++i) s = __builtin_elementwise_fma(s, a, f32x2{c[i], c[i]});
+  return s;
+}
+__device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
+  const f32x2 a = __builtin_elementwise_min(__builtin_elementwise_abs(x), f32x2{5.5f, 5.5f});
+  const f32x2 t = __builtin_elementwise_fma(x * f32x2{-0.5f * kLog2e, -0.5f * kLog2e}, x, gelu_tail_s2(a));
+  const float h0 = __builtin_amdgcn_exp2f(t[0]), h1 = __builtin_amdgcn_exp2f(t[1]);
+  return x * f32x2{x[0] >= 0.f ? 1.f - h0 : h0, x[1] >= 0.f ? 1.f - h1 : h1};
+}
+__device__ __forceinline__ f32x2 gelu_grad_f2(f32x2 x) {
+  const f32x2 a = __builtin_elementwise_min(__builtin_elementwise_abs(x), f32x2{5.5f, 5.5f});
+  const f32x2 m = x * f32x2{-0.5f * kLog2e, -0.5f * kLog2e} * x;
+  const f32x2 u = m + gelu_tail_s2(a);
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(m[0]), __builtin_amdgcn_exp2f(m[1])};
+  const f32x2 h = f32x2{__builtin_amdgcn_exp2f(u[0]), __builtin_amdgcn_exp2f(u[1])};
+  return __builtin_elementwise_fma(x * f32x2{0.3989422804014327f, 0.3989422804014327f}, e,
+                                   f32x2{x[0] >= 0.f ? 1.f - h[0] : h[0], x[1] >= 0.f ? 1.f - h[1] : h[1]});
+}
+
 // torch's GeluBackward: Phi(x) + x exp(-x^2/2) / sqrt(2 pi)
 __device__ __forceinline__ float gelu_grad_f(float x) {
   const float a = fminf(fabsf(x), 5.5f);
@@ -689,9 +718,12 @@ __device__ __forceinline__ void store_tile_buf(const GemmParams& p, f32x4 (&acc)
         if constexpr ((EPI & MTTS_GEMM_EPI_GELU) != 0) {
           bf16_t hpre[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            hpre[j] = f2bf(v[j]);
-            o[j] = f2bf(gelu_f(bf2f(hpre[j])));
+          for (int j = 0; j < 4; ++j) hpre[j] = f2bf(v[j]);
+#pragma unroll
+          for (int j = 0; j < 4; j += 2) {
+            const f32x2 g = gelu_f2(f32x2{bf2f(hpre[j]), bf2f(hpre[j + 1])});
+            o[j] = f2bf(g[0]);
+            o[j + 1] = f2bf(g[1]);
           }
           h2[NB][0] = hpre[0] | ((uint32_t)hpre[1] << 16);
           h2[NB][1] = hpre[2] | ((uint32_t)hpre[3] << 16);
@@ -700,7 +732,11 @@ __device__ __forceinline__ void store_tile_buf(const GemmParams& p, f32x4 (&acc)
           const float h[4] = {__uint_as_float(x << 16), __uint_as_float(x & 0xffff0000u), __uint_as_float(y << 16),
                               __uint_as_float(y & 0xffff0000u)};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = f2bf(bf2f(f2bf(v[j])) * gelu_grad_f(h[j]));
+          for (int j = 0; j < 4; j += 2) {
+            const f32x2 gg = gelu_grad_f2(f32x2{h[j], h[j + 1]});
+            o[j] = f2bf(bf2f(f2bf(v[j])) * gg[0]);
+            o[j + 1] = f2bf(bf2f(f2bf(v[j + 1])) * gg[1]);
+          }
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
