@@ -627,7 +627,7 @@ typedef struct {
 int64_t mtts_gemm_workspace(const MttsGemmArgs* a);
 int mtts_gemm(const MttsGemmArgs* a, void* stream);
 
-/* Grouped weight gradients (ABI 9): `n` (1..16) TN problems, each C_i =
+/* Grouped weight gradients (ABI 9; 24 problems since ABI 10): `n` (1..24) TN problems, each C_i =
  * A_i^T B_i (+ C_i when beta_i = 1) with fp32 out, no epilogue, no split-K,
  * in ONE launch; every output tile reduces its problem's whole K in one
  * workgroup (no partial slabs, no reduce pass).  Put the longest-K problems

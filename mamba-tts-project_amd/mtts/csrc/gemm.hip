@@ -970,7 +970,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_pp_kernel(GemmParams p) {
 // launch, each tile over the problem's WHOLE K (no split-K slabs, no
 // split_reduce pass).  The host orders the problems longest-K first; tiles of
 // a problem are consecutive work ids (an XCD walks one problem's tiles).
-constexpr int kGroupMax = 16;
+constexpr int kGroupMax = 24;   // 24 x 128-byte problems: kernel arguments stay under 4 KiB
 struct GroupParams {
   GemmParams p[kGroupMax];
   int tile_end[kGroupMax];   // exclusive prefix sums of the problems' tile counts

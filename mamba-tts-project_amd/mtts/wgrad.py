@@ -43,7 +43,12 @@ from . import _lib as L
 from . import gemm as G
 
 GROUP_TILES = 192       # flush once the queue holds this many 256x256 output tiles
-MAX_PROBLEMS = 16       # mtts_gemm_grouped's problem limit
+MAX_PROBLEMS = 24       # mtts_gemm_grouped's problem limit
+# a flush with fewer tiles than this leaves most CUs idle for its whole-K
+# tiles (C5's d_model 512 layers: ~68 tiles of 640 K-tiles each): its jobs
+# run one by one on the split-K TN path instead (tools/c5_once.py trace:
+# grouped 5.4 vs split-K 4.0 ms of weight gradients per step at 100 tiles)
+MIN_GROUP_TILES = 128
 # run the grouped launches on a side stream (the layer's long tiles leave some
 # CUs idle for the next layer's data-gradient kernels); the end-of-backward
 # callback joins the streams
@@ -219,8 +224,12 @@ def _flush(jobs, side=None):
             out, beta = tmp, 0.0
         probs.append((j.dy, j.x, out, beta))
     probs.sort(key=lambda t: -t[0].shape[0])   # longest reduction first (tail balance)
-    for s in range(0, len(probs), MAX_PROBLEMS):
-        _launch(probs[s:s + MAX_PROBLEMS])
+    if sum(-(-dy.shape[1] // G.TILE) * -(-x.shape[1] // G.TILE) for dy, x, _, _ in probs) < MIN_GROUP_TILES:
+        for dy, x, out, beta in probs:
+            G.mm_tn(dy, x, out=out, beta=beta)
+    else:
+        for s in range(0, len(probs), MAX_PROBLEMS):
+            _launch(probs[s:s + MAX_PROBLEMS])
     for out, tmp, beta in fixups:
         if beta:
             out.add_(tmp)

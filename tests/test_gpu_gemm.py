@@ -167,7 +167,7 @@ def test_tn_grouped_rejects_bad_problems():
     out = torch.empty(256, 256, device=dev)
     assert _grouped([(dy, x, out, 0.5)]) != 0          # beta must be 0 or 1
     assert _grouped([(rnd(100, 256), rnd(100, 256), out, 0.0)]) != 0   # k % 64
-    assert _grouped([(dy, x, out, 0.0)] * 17) != 0     # at most 16 problems
+    assert _grouped([(dy, x, out, 0.0)] * 25) != 0     # at most 24 problems
 
 
 def test_default_splits_fill_the_chip():

@@ -55,6 +55,34 @@ def _check(a, b, tol=1e-4):
         assert err <= tol * scale, f"{n}: {err:.3e} > {tol} * {scale:.3e}"
 
 
+@pytest.fixture(autouse=True)
+def _grouped_always(monkeypatch):
+    """These small models' flushes hold few tiles: force the grouped launch
+    (test_small_group_falls_back_to_split_k covers the fallback)."""
+    from mtts import wgrad
+    monkeypatch.setattr(wgrad, "MIN_GROUP_TILES", 0)
+
+
+def test_small_group_falls_back_to_split_k(monkeypatch):
+    """A flush with fewer than MIN_GROUP_TILES output tiles runs its jobs one
+    by one on the split-K TN path (no grouped launch) with the same result."""
+    from mtts import wgrad
+    m = _model()
+    batch = _batch()
+    launches = []
+    real = wgrad._launch
+    monkeypatch.setattr(wgrad, "_launch", lambda probs: launches.append(len(probs)) or real(probs))
+    out = {}
+    for defer, min_tiles in ((False, 0), (True, 10 ** 6)):
+        monkeypatch.setattr(wgrad, "MIN_GROUP_TILES", min_tiles)
+        m.zero_grad(set_to_none=True)
+        with wgrad.deferred(defer):
+            _loss(m, *batch).backward()
+        out[defer] = _grads(m)
+    assert not launches
+    _check(out[True], out[False])
+
+
 def test_deferred_grouped_equals_immediate(monkeypatch):
     from mtts import wgrad
     m = _model()
@@ -127,6 +155,7 @@ def _worker(rank, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=2)
     from mtts import wgrad
     from mtts.dp import GradAllReduce
+    wgrad.MIN_GROUP_TILES = 0   # the grouped launch writing into the bucket views
     m = _model()
     dp = GradAllReduce(list(m.parameters()), bucket_mb=1.0)
     tok, text, z, mask = _batch(2 * B)
