@@ -51,11 +51,22 @@ def _window(xp: torch.Tensor, T: int) -> L.RowMap:
 TILE, BK = 128, 32
 
 
+FORCE_SPLITS = None    # measurement hook (tools/convgemm_bench.py SPLITS=...)
+WG_TARGET = 1024       # workgroups to aim for: 2 resident per CU, 2 rounds
+
+
 def splits_for(m, n, k):
-    """K split: ~512 workgroups (two per CU) when the output has fewer
-    128 x 128 tiles, each split keeping >= 8 K-steps of 32."""
+    """K split: one workgroup per 128 x 128 tile is latency-bound (one
+    workgroup per CU overlaps nothing: the k = 9 conv forward runs 370 us
+    unsplit, 133 us in 8 splits, tools/convgemm_bench.py SPLITS sweep,
+    profiles/r05_convgemm_splits.txt), so aim for ~1024 workgroups (two
+    resident per CU and fine-grained enough to balance), up to 16 splits of
+    >= 4 K-steps each.  The slab sum moves 8 bytes per output element per
+    split, so wide outputs stop at max(4, 8M / (m n)) splits (k = 9 forward,
+    1M outputs: 8 splits 133 us vs 16 splits 144 us)."""
     tiles = -(-m // TILE) * -(-n // TILE)
-    return max(1, min(512 // tiles, (-(-k // BK)) // 8, 16))
+    nk = -(-k // BK)
+    return max(1, min(16, -(-WG_TARGET // tiles), nk // 4, max(4, (8 << 20) // (m * n))))
 
 
 def gemm(layout, m, n, k, a, b, c, bias=None, epilogue=0, aux=None, beta=0.0, device="cuda"):
@@ -68,7 +79,7 @@ def gemm(layout, m, n, k, a, b, c, bias=None, epilogue=0, aux=None, beta=0.0, de
         args.aux = aux
     args.bias = 0 if bias is None else bias.data_ptr()
     args.epilogue, args.beta = epilogue, beta
-    args.splits = splits_for(m, n, k)
+    args.splits = splits_for(m, n, k) if FORCE_SPLITS is None else FORCE_SPLITS
     ws = None
     if args.splits > 1:
         ws = torch.empty(L.lib().mtts_convgemm_workspace(C.byref(args)), device=device, dtype=torch.uint8)

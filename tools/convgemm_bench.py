@@ -26,6 +26,9 @@ def timed(fn, it=20):
 
 
 B, T = 8, 128
+if os.environ.get("SPLITS"):   # fixed split count for every GEMM (heuristic check)
+    CG.FORCE_SPLITS = int(os.environ["SPLITS"])
+    print("splits", CG.FORCE_SPLITS, flush=True)
 for (C, O, K) in [(512, 1024, 9), (1024, 512, 1), (512, 384, 1), (128, 512, 1), (512, 256, 3), (256, 256, 3)]:
     x = torch.randn(B, T, C, device="cuda")
     w = torch.randn(O, C, K, device="cuda") / (C * K) ** 0.5
