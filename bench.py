@@ -380,19 +380,39 @@ def text_bench(B=8, T_text=128, d_model=512, iters=10):
     ids = ids.masked_fill(mask, 0)
     target = torch.randint(1, 10, (B, T_text), device=dev, generator=g).float()
 
+    params = list(enc.parameters()) + list(dur.parameters())
+
     def step():
+        for p in params:
+            p.grad = None
         h = enc(ids, mask=mask)
         loss = dur.compute_loss(dur(h, mask=mask), target, mask=mask) + h.square().mean()
         loss.backward()
-    for _ in range(3):
+
+    def clock(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / iters * 1e3
+
+    side = torch.cuda.Stream()      # eager warm-up on a side stream (torch's capture recipe)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    eager_ms = clock(step)
+    # the same fwd + bwd (dropout included: its RNG offsets advance per
+    # replay) captured once as a hipGraph: ~400 launches of 2-15 us each, so
+    # an eager step is bound by host launch work on a slow host core
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
         step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        step()
-    torch.cuda.synchronize()
+    graph_ms = clock(graph.replay)
     return {"B": B, "T_text": T_text, "d_model": d_model, "dtype": "fp32",
-            "fwd_bwd_ms": (time.perf_counter() - t0) / iters * 1e3}
+            "fwd_bwd_ms": graph_ms, "mode": "hipGraph replay", "fwd_bwd_eager_ms": eager_ms}
 
 
 def cpu_baseline_scan(L=8192, D=2048):

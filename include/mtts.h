@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 10
+#define MTTS_ABI_VERSION 11
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -663,6 +663,13 @@ int mtts_gemm_grouped(const MttsGemmArgs* probs, int n, void* stream);
 typedef struct {
   const void* ptr;
   int64_t seg_rows, seg_stride, row_stride;
+  /* halo_c > 0 (a 'same' convolution's window over the UNPADDED activation,
+   * (B, T, C) with seg_rows = T, seg_stride = T C, row_stride = C, halo_c = C,
+   * halo_p = p): row r = (b, t) starts at ptr + b seg_stride + (t - p) C and
+   * its element e reads 0 where tap t - p + e / C falls outside [0, T) -- the
+   * zero padding without a padded copy.  Only on NT / NN operand A and TN
+   * operand B, halo_c % 32 == 0. */
+  int32_t halo_c, halo_p;
 } MttsRowMap;
 typedef struct {
   int layout;                /* MTTS_GEMM_NT / MTTS_GEMM_TN / MTTS_CONVGEMM_NN */

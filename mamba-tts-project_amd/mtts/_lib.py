@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -90,7 +90,8 @@ class GemmArgs(C.Structure):
 
 
 class RowMap(C.Structure):
-    _fields_ = [("ptr", vp), ("seg_rows", i64), ("seg_stride", i64), ("row_stride", i64)]
+    _fields_ = [("ptr", vp), ("seg_rows", i64), ("seg_stride", i64), ("row_stride", i64), ("halo_c", i32),
+                ("halo_p", i32)]
 
 
 class ConvGemmArgs(C.Structure):

@@ -16,7 +16,9 @@ A convolution over channel-last x (B, T, C) with weight (O, C, K), padding p
             B row (j, o) = Wf[o, (K-1-j) C ..] (a row map with a negative segment stride)
   weight    dWf = dy^T . window(x_pad)                              TN, windowed B
 No unfold copy (the zero-padded activation's rows overlap as GEMM rows) and
-no transposed / flipped weight copy.
+no transposed / flipped weight copy.  With C % 32 == 0 (every text-encoder
+convolution) there is no padded copy either: x_pad is virtual, a halo row map
+over x whose out-of-sequence taps the kernel reads as zeros.
 """
 from __future__ import annotations
 
@@ -46,6 +48,29 @@ def _window(xp: torch.Tensor, T: int) -> L.RowMap:
     """Rows b*T + t of the windows xp[b, t .. t+K-1, :] of a contiguous (B, T + K - 1, C) tensor."""
     _, Tp, C = xp.shape
     return _map(xp, T, Tp * C, C)
+
+
+def _halo_window(x: torch.Tensor, p: int) -> L.RowMap:
+    """The same windows over the UNPADDED (B, T, C) x: a halo map (mtts.h
+    MttsRowMap), taps outside [0, T) read 0 in the kernel -- no padded copy."""
+    _, T, C = x.shape
+    m = _map(x, T, T * C, C)
+    m.halo_c, m.halo_p = C, p
+    return m
+
+
+def _halo_ok(C, p):
+    return p > 0 and C % 32 == 0
+
+
+def _win(x: torch.Tensor, T: int, K: int) -> L.RowMap:
+    """Conv windows of x: padded (B, T + K - 1, C) or unpadded (halo)."""
+    return _window(x, T) if x.shape[1] != T or K == 1 else _halo_window(x, (K - 1) // 2)
+
+
+def _pad_for(x: torch.Tensor, p: int) -> torch.Tensor:
+    """x itself where the kernel zero-pads (halo), else a padded copy."""
+    return x if (p == 0 or _halo_ok(x.shape[2], p)) else F.pad(x, (0, 0, p, p))
 
 
 TILE, BK = 128, 32
@@ -93,10 +118,6 @@ def _f32c(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
-def _pad(x: torch.Tensor, p: int) -> torch.Tensor:
-    return F.pad(x, (0, 0, p, p)) if p else x
-
-
 def _wf(weight):
     O, C, K = weight.shape
     return weight.view(O, C) if K == 1 else weight.permute(0, 2, 1).reshape(O, K * C).contiguous()
@@ -108,11 +129,11 @@ def conv_forward(x, weight, bias, relu):
     B, T, C = x.shape
     O, _, K = weight.shape
     p = (K - 1) // 2
-    xp = _pad(x, p)
+    xp = _pad_for(x, p)
     wf = _wf(weight)
     y = torch.empty(B, T, O, device=x.device, dtype=torch.float32)
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0)
-    gemm(NT, B * T, O, K * C, _window(xp, T), _plain(wf), _plain(y.view(B * T, O)), bias=bias, epilogue=epi)
+    gemm(NT, B * T, O, K * C, _win(xp, T, K), _plain(wf), _plain(y.view(B * T, O)), bias=bias, epilogue=epi)
     return y, xp, wf
 
 
@@ -128,9 +149,9 @@ def dgrad(dy, wf, K, epilogue=0, aux=None):
     """dx (B, T, C) of a 'same' convolution for dy (B, T, O) contiguous."""
     B, T, O = dy.shape
     C = wf.shape[1] // K
-    dyp = _pad(dy, (K - 1) // 2)
+    dyp = _pad_for(dy, (K - 1) // 2)
     dx = torch.empty(B, T, C, device=dy.device, dtype=torch.float32)
-    gemm(NN, B * T, C, K * O, _window(dyp, T), _wflip_map(wf, K), _plain(dx.view(B * T, C)), epilogue=epilogue,
+    gemm(NN, B * T, C, K * O, _win(dyp, T, K), _wflip_map(wf, K), _plain(dx.view(B * T, C)), epilogue=epilogue,
          aux=aux)
     return dx
 
@@ -150,7 +171,7 @@ def conv_backward(dy, xp, wf, K, need_dx, need_dw, need_db, relu_out=None):
         dx = dgrad(dy, wf, K)
     if need_dw:
         dwf = torch.empty(O, K * C, device=dy.device, dtype=torch.float32)
-        gemm(TN, O, K * C, B * T, _plain(dy.view(B * T, O)), _window(xp, T), _plain(dwf))
+        gemm(TN, O, K * C, B * T, _plain(dy.view(B * T, O)), _win(xp, T, K), _plain(dwf))
         dw = dwf.view(O, K, C).permute(0, 2, 1).contiguous() if K > 1 else dwf.view(O, C, 1)
     if need_db:
         db = colsum(dy.view(B * T, O))
@@ -197,7 +218,7 @@ class ConvFFNFn(torch.autograd.Function):
         dout = dout.contiguous()
         B, T, O = dout.shape
         p2 = (K2 - 1) // 2
-        h = (hp[:, p2:p2 + T] if p2 else hp).contiguous()
+        h = (hp[:, p2:p2 + T] if hp.shape[1] != T else hp).contiguous()
         # dh = (dout conv2^T) * (h > 0): conv2's data gradient with the ReLU mask in its epilogue
         dh = dgrad(dout, wf2, K2, epilogue=EPI_DRELU, aux=_plain(h.view(B * T, h.shape[2])))
         _, dw2, db2 = conv_backward(dout, hp, wf2, K2, False, need[3], need[4] and ctx.has_b[1])

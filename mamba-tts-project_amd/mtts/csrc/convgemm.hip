@@ -34,6 +34,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <climits>
 
 namespace mtts {
 namespace {
@@ -48,13 +49,15 @@ constexpr int kTnPitch = kBM + 16;          // floats per k-row of a TN tile
 constexpr int kTnTile = kBK * kTnPitch;
 
 struct RowMap {
-  const float* p;
+  const float* p;        // halo maps: already moved back by halo_p rows (host)
   int64_t seg_stride, row_stride;
   uint32_t seg_rows;     // host-checked < 2^31 (32-bit division on the device)
+  int halo_c, halo_p;    // halo_c > 0: taps outside the segment read 0 (mtts.h)
   __device__ __forceinline__ const float* row(int r) const {
     const uint32_t s = (uint32_t)r / seg_rows;
     return p + (int64_t)s * seg_stride + (int64_t)((uint32_t)r - s * seg_rows) * row_stride;
   }
+  __device__ __forceinline__ int pos(int r) const { return (int)((uint32_t)r % seg_rows); }
 };
 
 struct Params {
@@ -95,7 +98,7 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // holds float4 t + 256 i (i < kLd) of the 128 x 32 tile
 struct NtLoad {
   const float* rp[kLd];
-  int chunk[kLd], lrow[kLd];
+  int chunk[kLd], lrow[kLd], tpos[kLd];
   bool rok[kLd];
   __device__ void init(const RowMap& mp, int r0, int rows, int tid) {
 #pragma unroll
@@ -106,13 +109,23 @@ struct NtLoad {
       const int r = r0 + lrow[i];
       rok[i] = r < rows;
       rp[i] = mp.row(rok[i] ? r : 0);
+      tpos[i] = mp.pos(rok[i] ? r : 0);
     }
   }
-  __device__ __forceinline__ void load(f32x4 (&v)[kLd], int k0, int K) const {
+  // halo: the K-step's 32 columns are one tap j = k0 / halo_c (halo_c % 32 ==
+  // 0, K-steps 32-aligned), valid on rows with 0 <= t - p + j < T
+  __device__ __forceinline__ void load(f32x4 (&v)[kLd], int k0, int K, const RowMap& mp) const {
+    int lo = INT_MIN, hi = INT_MAX;
+    if (mp.halo_c > 0) {
+      const int j = __builtin_amdgcn_readfirstlane(k0 / mp.halo_c);   // uniform: scalar division
+      lo = mp.halo_p - j;
+      hi = (int)mp.seg_rows + mp.halo_p - j;
+    }
 #pragma unroll
     for (int i = 0; i < kLd; ++i) {
       const int kk = k0 + chunk[i] * 4;
-      v[i] = (rok[i] && kk < K) ? *(const f32x4*)(rp[i] + kk) : f32x4{0.f, 0.f, 0.f, 0.f};
+      v[i] = (rok[i] && kk < K && tpos[i] >= lo && tpos[i] < hi) ? *(const f32x4*)(rp[i] + kk)
+                                                                : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   __device__ __forceinline__ void store(float* tile, const f32x4 (&v)[kLd]) const {
@@ -126,19 +139,27 @@ struct NtLoad {
 // contiguously, columns c0..c0+127): thread t holds float4 t + 256 i
 struct TnLoad {
   int krow[kLd], col[kLd];
-  __device__ void init(int tid) {
+  int tap[kLd];          // halo: the column's tap - p (fixed per thread: c0 is per workgroup)
+  __device__ void init(int tid, const RowMap& mp, int c0) {
 #pragma unroll
     for (int i = 0; i < kLd; ++i) {
       const int idx = tid + i * kT;
       krow[i] = idx >> 5;
       col[i] = (idx & 31) * 4;
+      tap[i] = mp.halo_c > 0 ? (c0 + col[i]) / mp.halo_c - mp.halo_p : 0;
     }
   }
+  // halo (operand B of TN: rows = tokens, column cc = tap * C + channel):
+  // token t contributes to tap j only where 0 <= t - p + j < T
   __device__ __forceinline__ void load(f32x4 (&v)[kLd], const RowMap& mp, int k0, int K, int c0, int cols) const {
 #pragma unroll
     for (int i = 0; i < kLd; ++i) {
       const int kr = k0 + krow[i], cc = c0 + col[i];
-      v[i] = (kr < K && cc < cols) ? *(const f32x4*)(mp.row(kr) + cc) : f32x4{0.f, 0.f, 0.f, 0.f};
+      bool ok = kr < K && cc < cols;
+      const uint32_t sg = (uint32_t)kr / mp.seg_rows, t = (uint32_t)kr - sg * mp.seg_rows;
+      if (mp.halo_c > 0) ok = ok && (uint32_t)((int)t + tap[i]) < mp.seg_rows;   // 0 <= t + tap < T
+      v[i] = ok ? *(const f32x4*)(mp.p + (int64_t)sg * mp.seg_stride + (int64_t)t * mp.row_stride + cc)
+                : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   __device__ __forceinline__ void store(float* tile, const f32x4 (&v)[kLd]) const {
@@ -162,16 +183,16 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
   const int nk = (kend - kbeg + kBK - 1) / kBK;
 
   NtLoad na, nb;
-  TnLoad tl;
+  TnLoad tl;   // TN / NN operand B (TN operand A shares its row / column layout; no halo there)
   if constexpr (NT || NN) na.init(p.a, m0, p.m, tid);
   if constexpr (NT) nb.init(p.b, n0, p.n, tid);
-  if constexpr (!NT) tl.init(tid);
+  if constexpr (!NT) tl.init(tid, p.b, n0);
   f32x4 va[kLd], vb[kLd];
   auto load = [&](int kt) {
     const int k0 = kbeg + kt * kBK;
-    if constexpr (NT || NN) na.load(va, k0, kend);
+    if constexpr (NT || NN) na.load(va, k0, kend, p.a);
     else tl.load(va, p.a, k0, kend, m0, p.m);
-    if constexpr (NT) nb.load(vb, k0, kend);
+    if constexpr (NT) nb.load(vb, k0, kend, p.b);
     else tl.load(vb, p.b, k0, kend, n0, p.n);
   };
   auto store = [&](int buf) {
@@ -270,7 +291,9 @@ __global__ __launch_bounds__(256) void convgemm_reduce_kernel(Params p) {
   }
 }
 
-bool map_ok(const MttsRowMap& r) {
+bool map_ok(const MttsRowMap& r, bool halo_ok = false) {
+  if (r.halo_c != 0 && !(halo_ok && r.halo_c > 0 && r.halo_c % 32 == 0 && r.halo_p >= 0))
+    return false;
   return r.ptr && r.seg_rows > 0 && r.seg_rows < (1ll << 31) && r.seg_stride % 4 == 0 && r.row_stride % 4 == 0 &&
          (uintptr_t)r.ptr % 16 == 0;
 }
@@ -286,18 +309,23 @@ extern "C" int mtts_convgemm(const MttsConvGemmArgs* a, void* stream) {
   MTTS_CHECK(a->layout == MTTS_GEMM_NT || a->layout == MTTS_GEMM_TN || a->layout == MTTS_CONVGEMM_NN,
              "convgemm: layout must be NT (0), TN (1) or NN (2)");
   const bool nt = a->layout == MTTS_GEMM_NT, nn = a->layout == MTTS_CONVGEMM_NN;
-  MTTS_CHECK(map_ok(a->a) && map_ok(a->b) && map_ok(a->c),
-             "convgemm: operands need a pointer, seg_rows > 0, 16-byte alignment and strides a multiple of 4");
+  MTTS_CHECK(map_ok(a->a, nt || nn) && map_ok(a->b, !nt && !nn) && map_ok(a->c),
+             "convgemm: operands need a pointer, seg_rows > 0, 16-byte alignment and strides a multiple of 4 "
+             "(halo maps: NT / NN operand A or TN operand B only, halo_c %% 32 == 0, halo_p >= 0)");
   MTTS_CHECK(a->n % 4 == 0, "convgemm: n=%d must be a multiple of 4", a->n);
   MTTS_CHECK((nt || nn) ? a->k % 4 == 0 : a->m % 4 == 0, "convgemm: %s must be a multiple of 4",
              (nt || nn) ? "k" : "m");
   MTTS_CHECK(!(a->epilogue & MTTS_CONVGEMM_BIAS) || (a->bias && (uintptr_t)a->bias % 16 == 0),
              "convgemm: bias epilogue needs a 16-byte aligned bias");
   MTTS_CHECK(!(a->epilogue & MTTS_CONVGEMM_DRELU) || map_ok(a->aux), "convgemm: ReLU-backward epilogue needs aux");
+  MTTS_CHECK(a->k % 32 == 0 || a->a.halo_c == 0, "convgemm: a halo operand A needs k %% 32 == 0");
   MTTS_CHECK(!((a->epilogue & MTTS_CONVGEMM_RELU) && (a->epilogue & MTTS_CONVGEMM_DRELU)),
              "convgemm: RELU and DRELU are exclusive");
   Params p{};
-  auto rm = [](const MttsRowMap& r) { return RowMap{(const float*)r.ptr, r.seg_stride, r.row_stride, (uint32_t)r.seg_rows}; };
+  auto rm = [](const MttsRowMap& r) {   // a halo map's rows start halo_p rows before t (never read there)
+    return RowMap{(const float*)r.ptr - (int64_t)r.halo_p * r.row_stride, r.seg_stride, r.row_stride,
+                  (uint32_t)r.seg_rows, r.halo_c, r.halo_p};
+  };
   p.a = rm(a->a);
   p.b = rm(a->b);
   if (a->epilogue & MTTS_CONVGEMM_DRELU) p.aux = rm(a->aux);

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void colsum_rows_kernel(const T* __restrict__ 
 }  // namespace mtts
 
 extern "C" int64_t mtts_colsum_workspace(int rows, int cols, int rows_per_group) {
-  if (rows_per_group <= 1024 && !(rows_per_group >= rows && rows > 1024)) return 0;
+  if (rows_per_group <= 1024 && !(rows_per_group >= rows && rows >= 256)) return 0;
   const int64_t chunks = (int64_t)(rows + 15) / 16;     // the single-group path's chunks (>= 16 rows each)
   return chunks * cols * 4 + 256;
 }
@@ -162,13 +162,20 @@ extern "C" int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_
     return MTTS_OK;
   }
   const int es = dtype == MTTS_F32 ? 4 : 2;
-  if (rows_per_group >= rows && rows > 1024 && cols % (16 / es) == 0 && row_stride % (16 / es) == 0 &&
+  if (rows_per_group >= rows && rows >= 256 && cols % (16 / es) == 0 && row_stride % (16 / es) == 0 &&
       (uintptr_t)in % 16 == 0) {
     // one group over many rows (bias gradients): 16-byte row pieces, 128-row
     // chunks -> fp32 partial slab -> sum of the chunks
     MTTS_CHECK(workspace, "colsum: workspace required (mtts_colsum_workspace)");
-    // 128-row chunks (tools/bench_colsum.py: 64 / 32 measured equal at 1024 columns, slower at 2048+)
-    const int rchunk = 128;
+    // 128-row chunks (tools/bench_colsum.py: 64 / 32 measured equal at 1024 columns, slower at 2048+);
+    // up to 1024 rows (the text encoder's 1024 x 1024 fp32 bias gradients: 16
+    // blocks took 13 us) the chunks shrink to 16 rows until ~256 blocks run
+    int rchunk = 128;
+    if (rows <= 1024) {
+      const int cblocks = (cols + 64 * (16 / es) - 1) / (64 * (16 / es));
+      const int want = (256 + cblocks - 1) / cblocks;
+      rchunk = std::min(128, std::max(16, ((rows + want - 1) / want + 15) / 16 * 16));
+    }
     const int chunks = (rows + rchunk - 1) / rchunk;
     float* part = (float*)workspace;
     if (dtype == MTTS_F32)

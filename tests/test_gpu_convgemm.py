@@ -121,3 +121,25 @@ def test_refuses_bad_arguments():
         CG.gemm(CG.NT, 8, 8, 8, CG._plain(a), CG._plain(a), CG._plain(c), epilogue=CG.EPI_BIAS)
     with pytest.raises(TypeError):
         CG.conv1d_same(torch.randn(1, 4, 8, device=dev, dtype=torch.bfloat16), torch.randn(8, 8, 3, device=dev))
+
+
+@pytest.mark.parametrize("B,T,C,K", [(3, 40, 64, 9), (2, 3, 32, 9), (4, 17, 96, 3)])
+def test_halo_windows_equal_padded_copy(B, T, C, K, monkeypatch):
+    """The halo row map (taps outside [0, T) read as zeros in the kernel) gives
+    bit-identical forward / dx / dW to the explicitly zero-padded windows,
+    including T < p (every tap of a row but a few reads the halo)."""
+    torch.manual_seed(B * T * K)
+    x = torch.randn(B, T, C, device=dev)
+    w = torch.randn(64, C, K, device=dev) / (C * K) ** 0.5
+    b = torch.randn(64, device=dev)
+    g = torch.randn(B, T, 64, device=dev)
+    outs = []
+    for halo in (True, False):
+        if not halo:
+            monkeypatch.setattr(CG, "_halo_ok", lambda C_, p: False)
+        ts = [t.clone().requires_grad_(True) for t in (x, w, b)]
+        y = CG.conv1d_same(*ts)
+        (y * g).sum().backward()
+        outs.append([y.detach()] + [t.grad for t in ts])
+    for a, r in zip(*outs):
+        assert torch.equal(a, r)

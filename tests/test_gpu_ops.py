@@ -503,7 +503,7 @@ def test_upstream_signature_ops(golden):
         close(t.grad, g["d" + k], name="d" + k)
 
 
-@pytest.mark.parametrize("rows,cols", [(1, 5), (300, 64), (16384, 1024), (4097, 96), (20000, 2050)])
+@pytest.mark.parametrize("rows,cols", [(1, 5), (300, 64), (16384, 1024), (4097, 96), (20000, 2050), (1024, 1024), (256, 512), (777, 384)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_colsum(rows, cols, dtype):
     from mtts.linear import colsum

@@ -29,6 +29,9 @@ B, T = 8, 128
 if os.environ.get("SPLITS"):   # fixed split count for every GEMM (heuristic check)
     CG.FORCE_SPLITS = int(os.environ["SPLITS"])
     print("splits", CG.FORCE_SPLITS, flush=True)
+if os.environ.get("HALO") == "0":   # explicit zero-padded copies instead of halo row maps (A/B)
+    CG._halo_ok = lambda C_, p: False
+    print("halo off", flush=True)
 for (C, O, K) in [(512, 1024, 9), (1024, 512, 1), (512, 384, 1), (128, 512, 1), (512, 256, 3), (256, 256, 3)]:
     x = torch.randn(B, T, C, device="cuda")
     w = torch.randn(O, C, K, device="cuda") / (C * K) ** 0.5

@@ -13,6 +13,9 @@ import torch  # noqa: E402
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 import text_encoder as te  # noqa: E402
 
+if os.environ.get("HALO") == "0":   # explicit zero-padded conv inputs instead of halo row maps (A/B)
+    from mtts import convgemm as CG
+    CG._halo_ok = lambda C_, p: False
 B, T_text, d_model = 8, 128, 512
 dev = "cuda"
 torch.manual_seed(0)
@@ -26,7 +29,12 @@ ids = ids.masked_fill(mask, 0)
 target = torch.randint(1, 10, (B, T_text), device=dev, generator=g).float()
 
 
-def step():
+params = list(enc.parameters()) + list(dur.parameters())
+
+
+def step():   # as bench.text_bench: gradients set to None first (zero_grad(set_to_none=True))
+    for p in params:
+        p.grad = None
     h = enc(ids, mask=mask)
     loss = dur.compute_loss(dur(h, mask=mask), target, mask=mask) + h.square().mean()
     loss.backward()
@@ -40,13 +48,13 @@ for _ in range(20):
     step()
 torch.cuda.synchronize()
 wall = (time.perf_counter() - t0) / 20 * 1e3
-with profile(activities=[ProfilerActivity.CUDA]) as prof:
+with profile(activities=[ProfilerActivity.CUDA, ProfilerActivity.CPU]) as prof:
     for _ in range(5):
         step()
     torch.cuda.synchronize()
 agg = defaultdict(lambda: [0, 0.0])
 for ev in prof.events():
-    if ev.device_type == torch.autograd.DeviceType.CUDA:
+    if ev.device_type == torch.autograd.DeviceType.CUDA and ev.device_time > 0:
         a = agg[ev.name[:90]]
         a[0] += 1
         a[1] += ev.device_time
@@ -55,3 +63,10 @@ print(f"wall {wall:.3f} ms/step, GPU kernel time {tot / 1e3:.3f} ms/step, "
       f"{sum(v[0] for v in agg.values()) / 5:.0f} kernels/step")
 for name, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
     print(f"{us / 5:9.1f} us {n / 5:5.0f}x  {name}")
+ops = defaultdict(int)
+for ev in prof.events():
+    if ev.device_type == torch.autograd.DeviceType.CPU and ev.name.startswith("aten::") and \
+            ev.name in ("aten::add", "aten::add_", "aten::copy_", "aten::fill_", "aten::zero_", "aten::where",
+                        "aten::masked_fill", "aten::cat", "aten::constant_pad_nd", "aten::mul", "aten::clone"):
+        ops[ev.name] += 1
+print("aten ops per step:", ", ".join(f"{k} {v / 5:.0f}" for k, v in sorted(ops.items(), key=lambda kv: -kv[1])))
