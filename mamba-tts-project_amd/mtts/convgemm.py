@@ -172,7 +172,10 @@ def conv_backward(dy, xp, wf, K, need_dx, need_dw, need_db, relu_out=None):
     if need_dw:
         dwf = torch.empty(O, K * C, device=dy.device, dtype=torch.float32)
         gemm(TN, O, K * C, B * T, _plain(dy.view(B * T, O)), _win(xp, T, K), _plain(dwf))
-        dw = dwf.view(O, K, C).permute(0, 2, 1).contiguous() if K > 1 else dwf.view(O, C, 1)
+        # (O, C, K) over the [o][k][c] result, no transposing copy: a weight
+        # kept [O][K][C] (text_encoder.kc_major) takes it as its gradient as is;
+        # autograd re-lays it out for a contiguous weight
+        dw = dwf.view(O, K, C).permute(0, 2, 1) if K > 1 else dwf.view(O, C, 1)
     if need_db:
         db = colsum(dy.view(B * T, O))
     return dx, dw, db

@@ -62,7 +62,10 @@ class GradAllReduce:
             if p.dtype != dtype or dtype not in (torch.float32, torch.float64):
                 raise TypeError("GradAllReduce expects fp32 (or, for tests, fp64) master parameters of one dtype")
             n = p.numel()
-            self.views[p] = self.flat[off:off + n].view_as(p)
+            # the bucket view takes p's own (dense) strides: a gradient of p's
+            # layout folds into it with a straight copy and the fused optimizer
+            # sees p, grad and moments in one storage order
+            self.views[p] = self.flat[off:off + n].as_strided(p.shape, p.stride())
             p.grad = self.views[p]
             self.bucket_of[p] = len(self.buckets)
             off += pad(n)

@@ -435,6 +435,7 @@ class LayerNormFn(torch.autograd.Function):
             gamma, beta = film[:, :n], film[:, n:]
         y, mean, rstd, x_sum = layernorm_fwd(x, w, b, eps, res, gamma, beta, rows_per_group)
         xn = x_sum if res is not None else x
+        ctx.set_materialize_grads(False)   # an unused x_sum: no zero-filled gradient, no dx_acc pass
         ctx.eps, ctx.rpg = eps, rows_per_group
         ctx.has_res = res is not None
         ctx.has_film = film is not None
@@ -451,6 +452,8 @@ class LayerNormFn(torch.autograd.Function):
         xn, w, b, gamma, beta, mean, rstd = ctx.saved_tensors
         if dsum is not None and dsum.numel() == 0:
             dsum = None
+        if dy is None:   # only x_sum was used
+            dy = torch.zeros_like(xn)
         n = xn.shape[-1]
         dgb = None
         if ctx.has_film:

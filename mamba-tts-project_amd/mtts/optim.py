@@ -21,6 +21,20 @@ import torch
 from . import _lib as L
 
 
+def dense(t: torch.Tensor) -> bool:
+    """t covers its storage span without gaps or overlap (a permutation of a
+    contiguous tensor)."""
+    if t.is_contiguous():
+        return True
+    order = sorted(range(t.dim()), key=lambda d: -t.stride(d))
+    return t.permute(order).is_contiguous()
+
+
+def same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Equal shapes and strides (a size-1 dimension's stride does not matter)."""
+    return a.shape == b.shape and all(n == 1 or sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()))
+
+
 class FusedClipAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_grad_norm=None):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
@@ -103,8 +117,10 @@ class FusedClipAdam(torch.optim.Optimizer):
             for p in ps:
                 if p.dtype != torch.float32 or not p.is_cuda or p.grad.dtype != torch.float32:
                     raise TypeError("FusedClipAdam takes fp32 CUDA (HIP) parameters and gradients")
-                if p.grad.is_sparse or not p.grad.is_contiguous() or not p.is_contiguous():
-                    raise ValueError("FusedClipAdam needs dense contiguous parameters and gradients")
+                # the kernel walks storage order: p, grad and moments need one
+                # dense layout (contiguous, or e.g. a conv weight kept [O][K][C])
+                if p.grad.is_sparse or not dense(p) or not same_layout(p.grad, p):
+                    raise ValueError("FusedClipAdam needs dense parameters and gradients of the same strides")
                 st = self.state[p]
                 if not st:
                     st["step"] = torch.tensor(0.0)

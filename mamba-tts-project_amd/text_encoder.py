@@ -73,6 +73,19 @@ def linear(x, weight, bias=None):
     return CG.linear(x, weight, bias)
 
 
+def kc_major(conv: nn.Conv1d) -> nn.Conv1d:
+    """Keep a Conv1d weight's storage as [O][K][C] behind its (O, C, K) shape
+    (a permuted dense view: state_dict keys, shapes and values unchanged).
+    The implicit-GEMM convolution reads the weight as (O, K*C) rows, so its
+    forward and weight gradient then need no transposing copies; the fused
+    optimizer and the DP buckets follow the parameter's strides."""
+    w = conv.weight
+    if w.shape[2] > 1 and not w.permute(0, 2, 1).is_contiguous():
+        conv.weight = nn.Parameter(w.detach().permute(0, 2, 1).contiguous().permute(0, 2, 1),
+                                   requires_grad=w.requires_grad)
+    return conv
+
+
 class Conv(nn.Module):
     """FastSpeech2 model/modules.py Conv: Conv1d on (B, T, C) inputs."""
 
@@ -81,7 +94,7 @@ class Conv(nn.Module):
         super().__init__()
         if stride != 1 or dilation != 1:
             raise ValueError("Conv: stride / dilation 1 only (the text encoder's use)")
-        self.conv = nn.Conv1d(in_channels, out_channels, kernel_size=kernel_size, padding=padding, bias=bias)
+        self.conv = kc_major(nn.Conv1d(in_channels, out_channels, kernel_size=kernel_size, padding=padding, bias=bias))
 
     def forward(self, x):
         return conv1d_same(x, self.conv.weight, self.conv.bias, self.conv.padding[0])
@@ -121,8 +134,8 @@ class MultiHeadAttention(nn.Module):
 class PositionwiseFeedForward(nn.Module):
     def __init__(self, d_in, d_hid, kernel_size, dropout=0.1):
         super().__init__()
-        self.w_1 = nn.Conv1d(d_in, d_hid, kernel_size=kernel_size[0], padding=(kernel_size[0] - 1) // 2)
-        self.w_2 = nn.Conv1d(d_hid, d_in, kernel_size=kernel_size[1], padding=(kernel_size[1] - 1) // 2)
+        self.w_1 = kc_major(nn.Conv1d(d_in, d_hid, kernel_size=kernel_size[0], padding=(kernel_size[0] - 1) // 2))
+        self.w_2 = kc_major(nn.Conv1d(d_hid, d_in, kernel_size=kernel_size[1], padding=(kernel_size[1] - 1) // 2))
         self.layer_norm = nn.LayerNorm(d_in)
         self.dropout = nn.Dropout(dropout)
 
@@ -143,9 +156,12 @@ class FFTBlock(nn.Module):
     def forward(self, enc_input, mask=None, slf_attn_mask=None):
         keypad = mask                      # slf_attn_mask = mask expanded over queries: the key pad mask
         enc_output, attn = self.slf_attn(enc_input, enc_input, enc_input, mask=keypad)
-        enc_output = enc_output.masked_fill(mask.unsqueeze(-1), 0)
+        # masked_fill(mask, 0) as a product with the keep mask: one kernel each
+        # way instead of a clone + fill (padded rows become +-0)
+        keep = (~mask).unsqueeze(-1).to(enc_output.dtype)
+        enc_output = enc_output * keep
         enc_output = self.pos_ffn(enc_output)
-        enc_output = enc_output.masked_fill(mask.unsqueeze(-1), 0)
+        enc_output = enc_output * keep
         return enc_output, attn
 
 

@@ -61,3 +61,33 @@ def test_fused_clip_adam_rejects_mixed_steps():
     b.grad = torch.randn(8, device=DEV)
     with pytest.raises(ValueError, match="step count"):
         opt.step()
+
+
+def test_fused_clip_adam_permuted_dense_parameter():
+    """A conv weight kept [O][K][C] behind its (O, C, K) shape (text_encoder.
+    kc_major): the step walks storage order, so p, grad and moments must share
+    the layout -- result equal to the contiguous parameter's step; a gradient
+    of another layout is refused."""
+    from mtts.optim import FusedClipAdam
+    torch.manual_seed(1)
+    w0 = torch.randn(64, 32, 9, device=DEV)
+    g0 = torch.randn(64, 32, 9, device=DEV)
+    a = torch.nn.Parameter(w0.permute(0, 2, 1).contiguous().permute(0, 2, 1))
+    b = torch.nn.Parameter(w0.clone())
+    assert not a.is_contiguous()
+    for p in (a, b):
+        p.grad = torch.empty_like(p).copy_(g0)          # empty_like keeps the parameter's strides
+    oa, ob = FusedClipAdam([a], lr=1e-2, max_grad_norm=1.0), FusedClipAdam([b], lr=1e-2, max_grad_norm=1.0)
+    for _ in range(2):
+        oa.step()
+        ob.step()
+    assert torch.equal(a.detach(), b.detach())
+    assert opt_state_strides_match(oa, a)
+    a.grad = g0.clone()                                  # contiguous gradient on the permuted parameter
+    with pytest.raises(ValueError, match="same strides"):
+        oa.step()
+
+
+def opt_state_strides_match(opt, p):
+    st = opt.state[p]
+    return st["exp_avg"].stride() == p.stride() and st["exp_avg_sq"].stride() == p.stride()

@@ -67,6 +67,9 @@ def test_text_encoder_vs_oracle(d_model, n_head, d_k, d_inner):
     assert torch.count_nonzero(m.phoneme_emb.weight.grad[0]) == 0
     assert m.position_enc.grad is None
     close(m.position_enc.detach()[0], R.sinusoid_table_ref(101, d_model, 0), rtol=1e-6, name="position_enc")
+    for blk in m.layer_stack:   # the k = 9 weights stay [O][K][C] in storage and so do their gradients
+        wk = blk.pos_ffn.w_1.weight
+        assert wk.permute(0, 2, 1).is_contiguous() and wk.grad.stride() == wk.stride()
 
 
 def test_duration_predictor_and_loss_vs_oracle():

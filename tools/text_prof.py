@@ -70,3 +70,11 @@ for ev in prof.events():
                         "aten::masked_fill", "aten::cat", "aten::constant_pad_nd", "aten::mul", "aten::clone"):
         ops[ev.name] += 1
 print("aten ops per step:", ", ".join(f"{k} {v / 5:.0f}" for k, v in sorted(ops.items(), key=lambda kv: -kv[1])))
+if os.environ.get("STACKS"):   # where the copies / clones / fills come from
+    with profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=True) as prof2:
+        step()
+        torch.cuda.synchronize()
+    for row in prof2.key_averages(group_by_stack_n=6, group_by_input_shape=True):
+        if row.key in ("aten::copy_", "aten::clone", "aten::fill_", "aten::add_", "aten::add", "aten::mul"):
+            st = [f for f in row.stack if "mamba-tts-project_amd" in f or "tools/" in f][:3]
+            print(f"{row.key:12s} x{row.count:3d} {str(row.input_shapes)[:70]:70s} {' <- '.join(st)}")
