@@ -211,7 +211,11 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
 }
 
 static int ln_rb(const MttsLNArgs* a) {
-  if (!a->gamma) return 64;
+  if (!a->gamma) {   // 64 rows per block; short inputs (the text encoder's 1024 rows: 16 blocks) down to 8
+    int rb = 64;
+    while (rb > 8 && (a->rows + rb - 1) / rb < 256) rb >>= 1;
+    return rb;
+  }
   for (int rb = 64; rb > 1; rb >>= 1)
     if (a->rows_per_group % rb == 0) return rb;
   return 1;
@@ -315,6 +319,7 @@ extern "C" int64_t mtts_layernorm_bwd_workspace(int rows, int cols, int rows_per
   MttsLNArgs t{};
   t.gamma = rows_per_group > 0 ? (const void*)1 : nullptr;
   t.rows_per_group = rows_per_group;
+  t.rows = rows;
   const int rb = ln_rb(&t);
   const int64_t nblk = (rows + rb - 1) / rb;
   return 5 * nblk * cols * 4 + 256;

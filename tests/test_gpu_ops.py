@@ -412,6 +412,7 @@ def test_state_update_vs_golden(golden):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cols,rows,film", [(64, 6, False), (1024, 64, True), (512, 40, True), (2048, 17, False),
+                                            (512, 1024, False), (256, 3001, False),
                                             (96 * 2, 5, False)])
 def test_layernorm_res_film_fwd_bwd(dtype, cols, rows, film):
     from mtts import ops

@@ -76,5 +76,5 @@ if os.environ.get("STACKS"):   # where the copies / clones / fills come from
         torch.cuda.synchronize()
     for row in prof2.key_averages(group_by_stack_n=6, group_by_input_shape=True):
         if row.key in ("aten::copy_", "aten::clone", "aten::fill_", "aten::add_", "aten::add", "aten::mul"):
-            st = [f for f in row.stack if "mamba-tts-project_amd" in f or "tools/" in f][:3]
+            st = [f for f in row.stack if "site-packages" not in f and "dist-packages" not in f][:3]
             print(f"{row.key:12s} x{row.count:3d} {str(row.input_shapes)[:70]:70s} {' <- '.join(st)}")
