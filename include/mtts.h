@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 11
+#define MTTS_ABI_VERSION 12
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -680,6 +680,8 @@ typedef struct {
   float beta;
   int splits;                /* > 1: K split over workgroups, fp32 partial slabs summed in fixed order */
   void* workspace;           /* splits > 1: mtts_convgemm_workspace() bytes */
+  float* colsum_a;           /* TN only, optional (ABI 12): colsum_a[m] = sum_k A[row k][m] -- with A = dy,
+                                the bias gradient, summed by the weight-gradient kernel from its own A tiles */
 } MttsConvGemmArgs;
 int64_t mtts_convgemm_workspace(const MttsConvGemmArgs* a);
 int mtts_convgemm(const MttsConvGemmArgs* a, void* stream);

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -97,7 +97,7 @@ class RowMap(C.Structure):
 class ConvGemmArgs(C.Structure):
     _fields_ = [("layout", i32), ("m", i32), ("n", i32), ("k", i32), ("a", RowMap), ("b", RowMap), ("c", RowMap),
                 ("aux", RowMap), ("bias", vp), ("epilogue", i32), ("beta", f32), ("splits", i32),
-                ("workspace", vp)]
+                ("workspace", vp), ("colsum_a", vp)]
 
 
 class SkinnyArgs(C.Structure):

@@ -94,9 +94,10 @@ def splits_for(m, n, k):
     return max(1, min(16, -(-WG_TARGET // tiles), nk // 4, max(4, (8 << 20) // (m * n))))
 
 
-def gemm(layout, m, n, k, a, b, c, bias=None, epilogue=0, aux=None, beta=0.0, device="cuda"):
+def gemm(layout, m, n, k, a, b, c, bias=None, epilogue=0, aux=None, beta=0.0, device="cuda", colsum_a=None):
     """One mtts_convgemm call on the current stream (the tensors the maps
-    point into are kept alive by the caller until it returns)."""
+    point into are kept alive by the caller until it returns).  colsum_a (TN,
+    fp32 (m,)): receives the column sums of A over the k rows."""
     args = L.ConvGemmArgs()
     args.layout, args.m, args.n, args.k = layout, m, n, k
     args.a, args.b, args.c = a, b, c
@@ -105,6 +106,8 @@ def gemm(layout, m, n, k, a, b, c, bias=None, epilogue=0, aux=None, beta=0.0, de
     args.bias = 0 if bias is None else bias.data_ptr()
     args.epilogue, args.beta = epilogue, beta
     args.splits = splits_for(m, n, k) if FORCE_SPLITS is None else FORCE_SPLITS
+    if colsum_a is not None:
+        args.colsum_a = colsum_a.data_ptr()
     ws = None
     if args.splits > 1:
         ws = torch.empty(L.lib().mtts_convgemm_workspace(C.byref(args)), device=device, dtype=torch.uint8)
@@ -171,12 +174,14 @@ def conv_backward(dy, xp, wf, K, need_dx, need_dw, need_db, relu_out=None):
         dx = dgrad(dy, wf, K)
     if need_dw:
         dwf = torch.empty(O, K * C, device=dy.device, dtype=torch.float32)
-        gemm(TN, O, K * C, B * T, _plain(dy.view(B * T, O)), _win(xp, T, K), _plain(dwf))
+        if need_db:   # the bias gradient from the weight-gradient kernel's own dy tiles
+            db = torch.empty(O, device=dy.device, dtype=torch.float32)
+        gemm(TN, O, K * C, B * T, _plain(dy.view(B * T, O)), _win(xp, T, K), _plain(dwf), colsum_a=db)
         # (O, C, K) over the [o][k][c] result, no transposing copy: a weight
         # kept [O][K][C] (text_encoder.kc_major) takes it as its gradient as is;
         # autograd re-lays it out for a contiguous weight
         dw = dwf.view(O, K, C).permute(0, 2, 1) if K > 1 else dwf.view(O, C, 1)
-    if need_db:
+    if need_db and db is None:
         db = colsum(dy.view(B * T, O))
     return dx, dw, db
 
@@ -267,8 +272,10 @@ class LinearFn(torch.autograd.Function):
             dx = dx.view(*dy.shape[:-1], C)
         if need[1]:
             dw = torch.empty(O, C, device=dy.device, dtype=torch.float32)
-            gemm(TN, O, C, x2.shape[0], _plain(dy2), _plain(x2), _plain(dw))
-        if need[2] and ctx.has_b:
+            if need[2] and ctx.has_b:   # from the weight-gradient kernel's own dy tiles
+                db = torch.empty(O, device=dy.device, dtype=torch.float32)
+            gemm(TN, O, C, x2.shape[0], _plain(dy2), _plain(x2), _plain(dw), colsum_a=db)
+        if need[2] and ctx.has_b and db is None:
             db = colsum(dy2)
         return dx, dw, db
 

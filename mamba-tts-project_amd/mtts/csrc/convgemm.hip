@@ -66,7 +66,8 @@ struct Params {
   int64_t c_seg_stride, c_row_stride;
   uint32_t c_seg_rows;
   const float* bias;
-  float* slabs;          // splits > 1: (splits, m, n) fp32 partials
+  float* slabs;          // splits > 1: (splits, m, n) fp32 partials, then (splits, m) column-sum partials
+  float* colsum;         // TN: sum over k of A's columns (n-tile 0's workgroups sum their A tiles)
   int m, n, k, tiles_n, tiles, splits, kper;
   int layout, epi;
   float beta;
@@ -207,6 +208,12 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // TN column sums of A (the bias gradient when A = dy): the first n-tile's
+  // workgroups add up the A tiles they stage anyway, thread t column t & 127
+  // over k-rows 16 (t >> 7) .. +15 of each step (~16 LDS reads against 128
+  // MFMAs per wave and step)
+  const bool do_cs = !NT && !NN && p.colsum != nullptr && tile % p.tiles_n == 0;
+  float cs = 0.f;
 
   load(0);
   store(0);
@@ -238,6 +245,10 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
             for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(fb[j][s], fa[i][s], acc[i][j]);
       }
     } else {
+      if (do_cs) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cs += ta[((tid >> 7) * 16 + r) * kTnPitch + (tid & 127)];
+      }
 #pragma unroll
       for (int s = 0; s < kBK / 4; ++s) {
         const int kr = s * 4 + q;
@@ -259,6 +270,18 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
       }
     }
     block_sync();
+  }
+
+  if (do_cs) {   // halves of the k-rows -> one sum per column (fixed order), then the split's slab or colsum
+    float* red = lds[0][0];   // free: every step's reads precede the loop's last barrier
+    if (tid >= 128) red[tid - 128] = cs;
+    block_sync();
+    const int m = m0 + tid;
+    if (tid < 128 && m < p.m) {
+      const float v = cs + red[tid];
+      if (p.splits > 1) p.slabs[(int64_t)p.splits * p.m * p.n + (int64_t)split * p.m + m] = v;
+      else p.colsum[m] = v;
+    }
   }
 
   // lane holds C[m][n .. n+3], m = .. + (lane & 15), n = .. + 4 (lane >> 4)
@@ -288,6 +311,14 @@ __global__ __launch_bounds__(256) void convgemm_reduce_kernel(Params p) {
     f32x4 v = *(const f32x4*)sp;
     for (int s = 1; s < p.splits; ++s) v += *(const f32x4*)(sp + (int64_t)s * p.m * p.n);
     epi_store(p, m, n, v);
+  }
+  if (p.colsum) {   // the column-sum partials, in split order
+    const float* cp = p.slabs + (int64_t)p.splits * p.m * p.n;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < p.m; i += gridDim.x * blockDim.x) {
+      float v = cp[i];
+      for (int s = 1; s < p.splits; ++s) v += cp[(int64_t)s * p.m + i];
+      p.colsum[i] = v;
+    }
   }
 }
 
@@ -345,6 +376,8 @@ extern "C" int mtts_convgemm(const MttsConvGemmArgs* a, void* stream) {
   p.splits = splits;
   p.kper = (int)(((int64_t)(a->k + splits - 1) / splits + kBK - 1) / kBK * kBK);
   p.slabs = (float*)a->workspace;
+  MTTS_CHECK(!a->colsum_a || a->layout == MTTS_GEMM_TN, "convgemm: colsum_a is a TN option (A = dy)");
+  p.colsum = a->colsum_a;
   hipStream_t st = (hipStream_t)stream;
   const unsigned grid = (unsigned)(tiles * splits);
   if (nt) hipLaunchKernelGGL(convgemm_kernel<MTTS_GEMM_NT>, dim3(grid), dim3(kT), 0, st, p);
@@ -362,5 +395,5 @@ extern "C" int mtts_convgemm(const MttsConvGemmArgs* a, void* stream) {
 
 extern "C" int64_t mtts_convgemm_workspace(const MttsConvGemmArgs* a) {
   if (!a || a->splits <= 1) return 0;
-  return (int64_t)a->splits * a->m * a->n * 4;
+  return (int64_t)a->splits * a->m * (a->n + (a->colsum_a ? 1 : 0)) * 4;
 }

@@ -48,6 +48,11 @@ def test_nt_tn_plain_and_epilogues(m, n, k):
         at, bt = torch.randn(k, m, device=dev), torch.randn(k, n, device=dev)
         CG.gemm(CG.TN, m, n, k, CG._plain(at), CG._plain(bt), CG._plain(c))
         assert rel(c, at.t() @ bt) < 1e-5
+        # the column sums of A (the bias gradient when A = dy) from the same launch(es)
+        cs = torch.full((m,), float("nan"), device=dev)
+        c.zero_()
+        CG.gemm(CG.TN, m, n, k, CG._plain(at), CG._plain(bt), CG._plain(c), colsum_a=cs)
+        assert rel(c, at.t() @ bt) < 1e-5 and rel(cs, at.sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("B,T,C,O,K", [(8, 128, 512, 1024, 9), (2, 13, 64, 128, 9), (3, 40, 256, 256, 3),
@@ -119,6 +124,8 @@ def test_refuses_bad_arguments():
         CG.gemm(CG.NT, 8, 6, 8, CG._plain(a), CG._plain(a), CG._plain(c))
     with pytest.raises(RuntimeError, match="bias"):
         CG.gemm(CG.NT, 8, 8, 8, CG._plain(a), CG._plain(a), CG._plain(c), epilogue=CG.EPI_BIAS)
+    with pytest.raises(RuntimeError, match="colsum_a"):
+        CG.gemm(CG.NT, 8, 8, 8, CG._plain(a), CG._plain(a), CG._plain(c), colsum_a=torch.empty(8, device=dev))
     with pytest.raises(TypeError):
         CG.conv1d_same(torch.randn(1, 4, 8, device=dev, dtype=torch.bfloat16), torch.randn(8, 8, 3, device=dev))
 
