@@ -137,35 +137,53 @@ struct NtLoad {
 };
 
 // TN operand tile (k-rows k0.. of a matrix whose rows hold the m / n index
-// contiguously, columns c0..c0+127): thread t holds float4 t + 256 i
+// contiguously, columns c0..c0+127): thread t holds float4 t + 256 i.  The
+// row pointers walk the map incrementally (K-steps are consecutive within a
+// split), so there is no 32-bit division per load and step.
 struct TnLoad {
-  int krow[kLd], col[kLd];
+  int krow[kLd];
+  bool cok[kLd];
   int tap[kLd];          // halo: the column's tap - p (fixed per thread: c0 is per workgroup)
-  __device__ void init(int tid, const RowMap& mp, int c0) {
+  const float* rp[kLd];  // row k0 + krow[i] of the current step, at the thread's column
+  uint32_t t[kLd];       // that row's position in its segment
+  __device__ void init(int tid, const RowMap& mp, int c0, int cols, int k0) {
 #pragma unroll
     for (int i = 0; i < kLd; ++i) {
       const int idx = tid + i * kT;
       krow[i] = idx >> 5;
-      col[i] = (idx & 31) * 4;
-      tap[i] = mp.halo_c > 0 ? (c0 + col[i]) / mp.halo_c - mp.halo_p : 0;
+      const int cc = c0 + (idx & 31) * 4;
+      cok[i] = cc < cols;
+      tap[i] = mp.halo_c > 0 ? cc / mp.halo_c - mp.halo_p : 0;
+      const uint32_t kr = (uint32_t)(k0 + krow[i]);
+      const uint32_t sg = kr / mp.seg_rows;
+      t[i] = kr - sg * mp.seg_rows;
+      rp[i] = mp.p + (int64_t)sg * mp.seg_stride + (int64_t)t[i] * mp.row_stride + cc;
     }
   }
   // halo (operand B of TN: rows = tokens, column cc = tap * C + channel):
   // token t contributes to tap j only where 0 <= t - p + j < T
-  __device__ __forceinline__ void load(f32x4 (&v)[kLd], const RowMap& mp, int k0, int K, int c0, int cols) const {
+  __device__ __forceinline__ void load(f32x4 (&v)[kLd], const RowMap& mp, int k0, int K) const {
 #pragma unroll
     for (int i = 0; i < kLd; ++i) {
-      const int kr = k0 + krow[i], cc = c0 + col[i];
-      bool ok = kr < K && cc < cols;
-      const uint32_t sg = (uint32_t)kr / mp.seg_rows, t = (uint32_t)kr - sg * mp.seg_rows;
-      if (mp.halo_c > 0) ok = ok && (uint32_t)((int)t + tap[i]) < mp.seg_rows;   // 0 <= t + tap < T
-      v[i] = ok ? *(const f32x4*)(mp.p + (int64_t)sg * mp.seg_stride + (int64_t)t * mp.row_stride + cc)
-                : f32x4{0.f, 0.f, 0.f, 0.f};
+      bool ok = k0 + krow[i] < K && cok[i];
+      if (mp.halo_c > 0) ok = ok && (uint32_t)((int)t[i] + tap[i]) < mp.seg_rows;
+      v[i] = ok ? *(const f32x4*)rp[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ __forceinline__ void advance(const RowMap& mp) {   // to the next K-step's rows
+#pragma unroll
+    for (int i = 0; i < kLd; ++i) {
+      t[i] += kBK;
+      rp[i] += kBK * mp.row_stride;
+      while (t[i] >= mp.seg_rows) {
+        t[i] -= mp.seg_rows;
+        rp[i] += mp.seg_stride - (int64_t)mp.seg_rows * mp.row_stride;
+      }
     }
   }
   __device__ __forceinline__ void store(float* tile, const f32x4 (&v)[kLd]) const {
 #pragma unroll
-    for (int i = 0; i < kLd; ++i) *(f32x4*)(tile + krow[i] * kTnPitch + col[i]) = v[i];
+    for (int i = 0; i < kLd; ++i) *(f32x4*)(tile + krow[i] * kTnPitch + ((threadIdx.x + i * kT) & 31) * 4) = v[i];
   }
 };
 
@@ -184,23 +202,24 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
   const int nk = (kend - kbeg + kBK - 1) / kBK;
 
   NtLoad na, nb;
-  TnLoad tl;   // TN / NN operand B (TN operand A shares its row / column layout; no halo there)
+  TnLoad ta_l, tb_l;   // TN operand A, TN / NN operand B
   if constexpr (NT || NN) na.init(p.a, m0, p.m, tid);
   if constexpr (NT) nb.init(p.b, n0, p.n, tid);
-  if constexpr (!NT) tl.init(tid, p.b, n0);
+  if constexpr (!NT && !NN) ta_l.init(tid, p.a, m0, p.m, kbeg);
+  if constexpr (!NT) tb_l.init(tid, p.b, n0, p.n, kbeg);
   f32x4 va[kLd], vb[kLd];
-  auto load = [&](int kt) {
+  auto load = [&](int kt) {   // called for kt = 0, 1, 2, ... in order (the TN row walk)
     const int k0 = kbeg + kt * kBK;
     if constexpr (NT || NN) na.load(va, k0, kend, p.a);
-    else tl.load(va, p.a, k0, kend, m0, p.m);
+    else { ta_l.load(va, p.a, k0, kend); ta_l.advance(p.a); }
     if constexpr (NT) nb.load(vb, k0, kend, p.b);
-    else tl.load(vb, p.b, k0, kend, n0, p.n);
+    else { tb_l.load(vb, p.b, k0, kend); tb_l.advance(p.b); }
   };
   auto store = [&](int buf) {
     if constexpr (NT || NN) na.store(lds[buf][0], va);
-    else tl.store(lds[buf][0], va);
+    else ta_l.store(lds[buf][0], va);
     if constexpr (NT) nb.store(lds[buf][1], vb);
-    else tl.store(lds[buf][1], vb);
+    else tb_l.store(lds[buf][1], vb);
   };
 
   f32x4 acc[4][4];
@@ -244,6 +263,28 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(fb[j][s], fa[i][s], acc[i][j]);
       }
+    } else if constexpr (NN) {
+      // A from the swizzled NT image by float4 (as NT: lane group q's element
+      // s is k = 16h + 4q + s), B from the TN image at those k-rows
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 fa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ra = wr * 64 + i * 16 + r16;
+          fa[i] = *(const f32x4*)(ta + ra * kBK + (((h * 4 + q) ^ (ra & 7)) << 2));
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float fb[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[j] = tb[(16 * h + 4 * q + s) * kTnPitch + wc * 64 + j * 16 + r16];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma4(fb[j], fa[i][s], acc[i][j]);
+        }
+      }
     } else {
       if (do_cs) {
 #pragma unroll
@@ -255,12 +296,7 @@ __global__ __launch_bounds__(kT, 2) void convgemm_kernel(Params p) {
         float fa[4], fb[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          if constexpr (NN) {   // A from the swizzled NT image, one element per lane
-            const int ra = wr * 64 + i * 16 + r16;
-            fa[i] = ta[ra * kBK + (((kr >> 2) ^ (ra & 7)) << 2) + (kr & 3)];
-          } else {
-            fa[i] = ta[kr * kTnPitch + wr * 64 + i * 16 + r16];
-          }
+          fa[i] = ta[kr * kTnPitch + wr * 64 + i * 16 + r16];
           fb[i] = tb[kr * kTnPitch + wc * 64 + i * 16 + r16];
         }
 #pragma unroll

@@ -28,6 +28,13 @@ for k, c in rows[:25]:
                  f" valu_insts/wave {c['SQ_INSTS_VALU'] / max(c['SQ_WAVES'], 1):8.0f}")
     if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
         g = c.get("GRBM_GUI_ACTIVE", 0)
-        line += (f" | mfma_busy/gui {c['SQ_VALU_MFMA_BUSY_CYCLES'] / max(g, 1):7.3f} mops_bf16 {c['SQ_INSTS_VALU_MFMA_MOPS_BF16']:.3g}"
-                 f" lds {c['SQ_INSTS_LDS']:.3g} vmem {c['SQ_INSTS_VMEM']:.3g}")
+        line += (f" | mfma_busy/gui {c['SQ_VALU_MFMA_BUSY_CYCLES'] / max(g, 1):7.3f}"
+                 f" mops_bf16 {c.get('SQ_INSTS_VALU_MFMA_MOPS_BF16', 0):.3g}"
+                 f" mops_f32 {c.get('SQ_INSTS_VALU_MFMA_MOPS_F32', 0):.3g}"
+                 f" lds {c.get('SQ_INSTS_LDS', 0):.3g} vmem {c.get('SQ_INSTS_VMEM', 0):.3g}")
+    if wc and "SQ_WAIT_INST_LDS" in c:
+        line += (f" | wait_inst_lds {c['SQ_WAIT_INST_LDS'] / wc:5.2f}"
+                 f" lds_active {c.get('SQ_ACTIVE_INST_LDS', 0) / wc:5.2f}"
+                 f" bank_conf/lds_active {c.get('SQ_LDS_BANK_CONFLICT', 0) / max(c.get('SQ_ACTIVE_INST_LDS', 1), 1):5.2f}"
+                 f" busy/gui {c.get('SQ_BUSY_CYCLES', 0) / max(c.get('GRBM_GUI_ACTIVE', 1), 1):5.2f}")
     print(line)
