@@ -53,6 +53,36 @@ def get_sinusoid_encoding_table(n_position, d_hid, padding_idx=None):
     return torch.FloatTensor(table)
 
 
+class EmbeddingFn(torch.autograd.Function):
+    """F.embedding(ids, weight, padding_idx) with the weight gradient as one
+    fp32 TN GEMM, dW = onehot(ids)^T dy (mtts.convgemm; padding ids land in a
+    discarded column), deterministic, instead of torch's sort-based dense
+    embedding backward (49 us at B=8 x 128 phonemes)."""
+
+    @staticmethod
+    def forward(ctx, ids, weight, padding_idx):
+        ctx.save_for_backward(ids)
+        ctx.V, ctx.pad = weight.shape[0], padding_idx
+        return F.embedding(ids, weight, padding_idx=padding_idx)
+
+    @staticmethod
+    def backward(ctx, dy):
+        ids, = ctx.saved_tensors
+        V, pad = ctx.V, ctx.pad
+        d = dy.shape[-1]
+        dy2 = dy.reshape(-1, d).contiguous()
+        n = dy2.shape[0]
+        Vp = (V + 1 + 3) // 4 * 4                 # + one discard column, a multiple of 4
+        cols = ids.reshape(-1)
+        if pad is not None:
+            cols = torch.where(cols == pad, torch.full_like(cols, V), cols)
+        onehot = torch.zeros(n, Vp, device=dy.device, dtype=torch.float32)
+        onehot.scatter_(1, cols[:, None], 1.0)
+        dw = torch.empty(Vp, d, device=dy.device, dtype=torch.float32)
+        CG.gemm(CG.TN, Vp, d, n, CG._plain(onehot), CG._plain(dy2), CG._plain(dw))
+        return None, dw[:V], None
+
+
 def _ln(mod, x, res=None):
     y, _ = ops.layer_norm(x, mod.weight, mod.bias, mod.eps, res=res)
     return y
@@ -100,6 +130,40 @@ class Conv(nn.Module):
         return conv1d_same(x, self.conv.weight, self.conv.bias, self.conv.padding[0])
 
 
+def _adjacent(ts):
+    """Contiguous tensors laid end to end in one storage, in order."""
+    t0 = ts[0]
+    off = t0.storage_offset()
+    for t in ts:
+        if not t.is_contiguous() or t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr() or \
+                t.storage_offset() != off:
+            return False
+        off += t.numel()
+    return True
+
+
+class PackedRowsFn(torch.autograd.Function):
+    """cat(ts) along dim 0 for parameters stored end to end (MultiHeadAttention
+    packs w_qs / w_ks / w_vs so): a view of their storage, no copy; the
+    gradient comes back as row-slice views."""
+
+    @staticmethod
+    def forward(ctx, *ts):
+        ctx.rows = [t.shape[0] for t in ts]
+        t0 = ts[0]
+        shape = (sum(ctx.rows),) + tuple(t0.shape[1:])
+        return t0.new_empty(0).set_(t0.untyped_storage(), t0.storage_offset(), shape,
+                                    torch.empty(shape, device="meta").stride())
+
+    @staticmethod
+    def backward(ctx, g):
+        return tuple(g.split(ctx.rows, 0))
+
+
+def _packed_rows(ts):
+    return PackedRowsFn.apply(*ts) if _adjacent(ts) else torch.cat(ts)
+
+
 class MultiHeadAttention(nn.Module):
     def __init__(self, n_head, d_model, d_k, d_v, dropout=0.1):
         super().__init__()
@@ -112,6 +176,27 @@ class MultiHeadAttention(nn.Module):
         self.layer_norm = nn.LayerNorm(d_model)
         self.fc = nn.Linear(n_head * d_v, d_model)
         self.dropout = nn.Dropout(dropout)
+        self._pack()
+
+    def _pack(self):
+        """Store the q / k / v weights (and biases) end to end so the fused
+        projection reads them in place (state_dict keys and shapes unchanged;
+        re-packed after .to() / .cuda(), which move each parameter alone)."""
+        lins = (self.w_qs, self.w_ks, self.w_vs)
+        for name in ("weight", "bias"):
+            ps = [getattr(m, name) for m in lins]
+            if _adjacent(ps):
+                continue
+            packed = torch.cat([p.detach() for p in ps])
+            off = 0
+            for p in ps:
+                p.data = packed[off:off + p.shape[0]]
+                off += p.shape[0]
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._pack()
+        return out
 
     def forward(self, q, k, v, mask=None):
         """q/k/v (B, L, d_model); mask (B, L_k) bool, True = pad key.
@@ -119,8 +204,8 @@ class MultiHeadAttention(nn.Module):
         residual = q
         # temperature sqrt(d_k) = the kernel's 1/sqrt(head_dim) scale
         if q is k and k is v:   # self-attention (the encoder's use): one fused q/k/v projection
-            w = torch.cat([self.w_qs.weight, self.w_ks.weight, self.w_vs.weight])
-            b = torch.cat([self.w_qs.bias, self.w_ks.bias, self.w_vs.bias])
+            w = _packed_rows([self.w_qs.weight, self.w_ks.weight, self.w_vs.weight])
+            b = _packed_rows([self.w_qs.bias, self.w_ks.bias, self.w_vs.bias])
             o = attn_kernels.attention_qkv(linear(q, w, b), self.n_head, key_padding_mask=mask)
         else:
             qh = linear(q, self.w_qs.weight, self.w_qs.bias)
@@ -153,12 +238,15 @@ class FFTBlock(nn.Module):
         self.slf_attn = MultiHeadAttention(n_head, d_model, d_k, d_v, dropout=dropout)
         self.pos_ffn = PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout=dropout)
 
-    def forward(self, enc_input, mask=None, slf_attn_mask=None):
+    def forward(self, enc_input, mask=None, slf_attn_mask=None, keep=None):
+        """keep (optional): (~mask)[..., None] in the activation dtype, made
+        once by TextEncoder for all its blocks."""
         keypad = mask                      # slf_attn_mask = mask expanded over queries: the key pad mask
         enc_output, attn = self.slf_attn(enc_input, enc_input, enc_input, mask=keypad)
         # masked_fill(mask, 0) as a product with the keep mask: one kernel each
         # way instead of a clone + fill (padded rows become +-0)
-        keep = (~mask).unsqueeze(-1).to(enc_output.dtype)
+        if keep is None:
+            keep = (~mask).unsqueeze(-1).to(enc_output.dtype)
         enc_output = enc_output * keep
         enc_output = self.pos_ffn(enc_output)
         enc_output = enc_output * keep
@@ -188,15 +276,20 @@ class TextEncoder(nn.Module):
         B, L = phoneme_ids.shape
         if mask is None:
             mask = torch.zeros(B, L, dtype=torch.bool, device=phoneme_ids.device)
-        emb = F.embedding(phoneme_ids, self.phoneme_emb.weight, padding_idx=self.padding_idx)
+        w = self.phoneme_emb.weight
+        if w.dtype == torch.float32 and w.is_cuda and w.shape[1] % 4 == 0:
+            emb = EmbeddingFn.apply(phoneme_ids, w, self.padding_idx)
+        else:
+            emb = F.embedding(phoneme_ids, w, padding_idx=self.padding_idx)
         if not self.training and L > self.max_seq_len:
             pos = get_sinusoid_encoding_table(L, self.d_model)[:L].to(emb.device, emb.dtype)
         else:
             pos = self.position_enc[0, :L].to(emb.dtype)
         x = emb + pos[None]
         attns = []
+        keep = (~mask).unsqueeze(-1).to(x.dtype)
         for layer in self.layer_stack:
-            x, a = layer(x, mask=mask, slf_attn_mask=None)
+            x, a = layer(x, mask=mask, slf_attn_mask=None, keep=keep)
             if return_attns:
                 attns.append(a)
         return (x, attns) if return_attns else x
