@@ -7,11 +7,11 @@
 
 namespace mtts {
 
-template <typename T>
-__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ part, int nparts, int ppg,
-                                                     int64_t pstride, int ncols, float* __restrict__ out,
-                                                     int64_t out_gstride) {
-  __shared__ float red[4][64];
+template <typename T, int W = 4>
+__global__ __launch_bounds__(64 * W) void colsum_kernel(const T* __restrict__ part, int nparts, int ppg,
+                                                        int64_t pstride, int ncols, float* __restrict__ out,
+                                                        int64_t out_gstride) {
+  __shared__ float red[W][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const int g = blockIdx.y;
@@ -21,22 +21,35 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ part,
   for (int q = 0; q < 8; ++q) acc[q] = 0.f;
   if (c < ncols) {
     int p = p0 + w;
-    for (; p + 28 < p1; p += 32) {
+    for (; p + 7 * W < p1; p += 8 * W) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] += ldf(part + (int64_t)(p + 4 * q) * pstride + c);
+      for (int q = 0; q < 8; ++q) acc[q] += ldf(part + (int64_t)(p + W * q) * pstride + c);
     }
-    for (; p < p1; p += 4) acc[0] += ldf(part + (int64_t)p * pstride + c);
+    for (; p < p1; p += W) acc[0] += ldf(part + (int64_t)p * pstride + c);
   }
   float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   red[w][lane] = s;
   block_sync();
-  if (w == 0 && c < ncols) out[(int64_t)g * out_gstride + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (w == 0 && c < ncols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < W; i += 4) t += (red[i][lane] + red[i + 1][lane]) + (red[i + 2][lane] + red[i + 3][lane]);
+    out[(int64_t)g * out_gstride + c] = t;
+  }
 }
 
 void colsum(const float* part, int nparts, int ppg, int64_t pstride, int ncols, float* out, int64_t out_gstride,
             hipStream_t st) {
   const int ngroups = (nparts + ppg - 1) / ppg;
-  hipLaunchKernelGGL(colsum_kernel<float>, dim3((ncols + 63) / 64, ngroups), dim3(256), 0, st, part, nparts, ppg,
+  if (ngroups * ((ncols + 63) / 64) < 128 && ppg >= 64) {
+    // few blocks over many partials (a chunked column sum's second stage: 16
+    // blocks x 128 partials took ~11 us on 4 waves): 16 waves, one batch of
+    // 8 loads each
+    hipLaunchKernelGGL((colsum_kernel<float, 16>), dim3((ncols + 63) / 64, ngroups), dim3(1024), 0, st, part, nparts,
+                       ppg, pstride, ncols, out, out_gstride);
+    return;
+  }
+  hipLaunchKernelGGL((colsum_kernel<float, 4>), dim3((ncols + 63) / 64, ngroups), dim3(256), 0, st, part, nparts, ppg,
                      pstride, ncols, out, out_gstride);
 }
 
@@ -47,12 +60,13 @@ struct ColsumJobs {
   int ncols;
   int64_t pstride;
 };
-__global__ __launch_bounds__(256) void colsum_multi_kernel(const ColsumJobs J) {
+template <int W>
+__global__ __launch_bounds__(64 * W) void colsum_multi_kernel(const ColsumJobs J) {
   const ColsumJob& jb = J.j[blockIdx.z];
   const int g = blockIdx.y;
   const int p0 = g * jb.ppg;
   if (p0 >= jb.nparts) return;   // block-uniform: before any barrier
-  __shared__ float red[4][64];
+  __shared__ float red[W][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const int p1 = min(jb.nparts, p0 + jb.ppg);
@@ -61,29 +75,38 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(const ColsumJobs J) {
   for (int q = 0; q < 8; ++q) acc[q] = 0.f;
   if (c < J.ncols) {
     int p = p0 + w;
-    for (; p + 28 < p1; p += 32) {
+    for (; p + 7 * W < p1; p += 8 * W) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] += jb.part[(int64_t)(p + 4 * q) * J.pstride + c];
+      for (int q = 0; q < 8; ++q) acc[q] += jb.part[(int64_t)(p + W * q) * J.pstride + c];
     }
-    for (; p < p1; p += 4) acc[0] += jb.part[(int64_t)p * J.pstride + c];
+    for (; p < p1; p += W) acc[0] += jb.part[(int64_t)p * J.pstride + c];
   }
   const float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   red[w][lane] = s;
   block_sync();
-  if (w == 0 && c < J.ncols)
-    jb.out[(int64_t)g * jb.out_gstride + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (w == 0 && c < J.ncols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < W; i += 4) t += (red[i][lane] + red[i + 1][lane]) + (red[i + 2][lane] + red[i + 3][lane]);
+    jb.out[(int64_t)g * jb.out_gstride + c] = t;
+  }
 }
 
 void colsum_multi(const ColsumJob* jobs, int n, int ncols, int64_t pstride, hipStream_t st) {
   ColsumJobs J{};
-  int gmax = 1;
+  int gmax = 1, pmax = 0;
   for (int i = 0; i < n; ++i) {
     J.j[i] = jobs[i];
     gmax = std::max(gmax, (jobs[i].nparts + jobs[i].ppg - 1) / jobs[i].ppg);
+    pmax = std::max(pmax, std::min(jobs[i].ppg, jobs[i].nparts));
   }
   J.ncols = ncols;
   J.pstride = pstride;
-  hipLaunchKernelGGL(colsum_multi_kernel, dim3((ncols + 63) / 64, gmax, n), dim3(256), 0, st, J);
+  const dim3 grid((ncols + 63) / 64, gmax, n);
+  if ((int)(grid.x * grid.y * grid.z) < 128 && pmax >= 64)   // few blocks over many partials: 16 waves
+    hipLaunchKernelGGL(colsum_multi_kernel<16>, grid, dim3(1024), 0, st, J);
+  else
+    hipLaunchKernelGGL(colsum_multi_kernel<4>, grid, dim3(256), 0, st, J);
 }
 
 // Stage 1 of a long column sum (bias gradients: rows = tokens): a block owns
@@ -197,10 +220,10 @@ extern "C" int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_
     float* part = (float*)workspace;
     dim3 g1((cols + 63) / 64, chunks);
     if (dtype == MTTS_F32)
-      hipLaunchKernelGGL(colsum_kernel<float>, g1, dim3(256), 0, st, (const float*)in, rows, 256, row_stride, cols,
+      hipLaunchKernelGGL((colsum_kernel<float, 4>), g1, dim3(256), 0, st, (const float*)in, rows, 256, row_stride, cols,
                          part, (int64_t)cols);
     else
-      hipLaunchKernelGGL(colsum_kernel<bf16_t>, g1, dim3(256), 0, st, (const bf16_t*)in, rows, 256, row_stride,
+      hipLaunchKernelGGL((colsum_kernel<bf16_t, 4>), g1, dim3(256), 0, st, (const bf16_t*)in, rows, 256, row_stride,
                          cols, part, (int64_t)cols);
     MTTS_LAUNCH_CHECK("colsum stage 1");
     const int cpg = rows_per_group >= rows ? chunks : rows_per_group / 256;
@@ -211,10 +234,10 @@ extern "C" int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_
   const int ngroups = (rows + rows_per_group - 1) / rows_per_group;
   dim3 grid((cols + 63) / 64, ngroups);
   if (dtype == MTTS_F32)
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)in, rows, rows_per_group,
+    hipLaunchKernelGGL((colsum_kernel<float, 4>), grid, dim3(256), 0, st, (const float*)in, rows, rows_per_group,
                        row_stride, cols, out, out_gstride);
   else
-    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)in, rows, rows_per_group,
+    hipLaunchKernelGGL((colsum_kernel<bf16_t, 4>), grid, dim3(256), 0, st, (const bf16_t*)in, rows, rows_per_group,
                        row_stride, cols, out, out_gstride);
   MTTS_LAUNCH_CHECK("colsum");
   return MTTS_OK;
