@@ -287,7 +287,9 @@ class TextEncoder(nn.Module):
             pos = self.position_enc[0, :L].to(emb.dtype)
         x = emb + pos[None]
         attns = []
-        keep = (~mask).unsqueeze(-1).to(x.dtype)
+        # full-width keep mask: the 8 masking products per direction then run
+        # as vectorised same-shape kernels instead of broadcasting ones
+        keep = (~mask).unsqueeze(-1).to(x.dtype).expand(x.shape).contiguous()
         for layer in self.layer_stack:
             x, a = layer(x, mask=mask, slf_attn_mask=None, keep=keep)
             if return_attns:
