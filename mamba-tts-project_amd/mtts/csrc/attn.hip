@@ -86,6 +86,24 @@ __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >
 
 __device__ __forceinline__ float exp2_raw(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// XCD-aware block coordinates: dispatch hands linear workgroup id i to XCD
+// i % 8, so the workgroups that share a (batch, head)'s K / V (forward, dQ)
+// or a query chunk's Q / dO slices (dK / dV) -- consecutive x -- would land on
+// all eight L2s.  Re-number so each XCD holds a contiguous 1/8 of the grid
+// (x fastest): those workgroups then meet in one L2.  A bijection, so a
+// kernel's work set is unchanged.  Off (plain order) for short key sides,
+// where there is nothing to share and C2's forward measured 0.8 us slower.
+struct Blk { int x, y, z; };
+__device__ __forceinline__ Blk xcd_block(bool on = true) {
+  if (!on) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int n = gx * gy * gridDim.z;
+  const int bid = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int q8 = n / 8, r8 = n % 8, xcd = bid % 8;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  return {id % gx, (id / gx) % gy, id / (gx * gy)};
+}
+
 // LDS pitch (elements) of a bf16 [rows][hd] image read with tr_read:
 // row pitch = 16 or 48 dwords mod 64 makes the 4 rows x 32 columns of a
 // 32-lane half hit 64 distinct banks.
@@ -372,8 +390,9 @@ __global__ __launch_bounds__(256, 4) void attn_fwd_db_kernel(MttsAttnFwdArgs a) 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int b = blockIdx.z, hh = blockIdx.y;
-  const int qw = (blockIdx.x * 4 + wave) * 32 * QT + r;   // query of tile u: qw + 32 u
+  const Blk bk = xcd_block(a.kv_len >= 1024);
+  const int b = bk.z, hh = bk.y;
+  const int qw = (bk.x * 4 + wave) * 32 * QT + r;   // query of tile u: qw + 32 u
   const bf16_t* kbase = (const bf16_t*)a.k + b * a.k_bs + hh * HD;
   const bf16_t* vbase = (const bf16_t*)a.v + b * a.v_bs + hh * HD;
   const uint8_t* mb = a.key_padding_mask ? a.key_padding_mask + b * a.mask_bs : nullptr;
@@ -1016,8 +1035,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
-  const int b = blockIdx.z, hh = blockIdx.y;
-  const int q0 = blockIdx.x * 128 + wave * 32;           // this wave's queries
+  const Blk bk = xcd_block(f.kv_len >= 1024);
+  const int b = bk.z, hh = bk.y;
+  const int q0 = bk.x * 128 + wave * 32;           // this wave's queries
   const float c = f.scale * kLog2e, inv_scale = 1.f / f.scale;
   const uint8_t* mb = f.key_padding_mask ? f.key_padding_mask + b * f.mask_bs : nullptr;
   const bf16_t* qb = (const bf16_t*)f.q + b * f.q_bs + hh * HD;
@@ -1201,10 +1221,11 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
-  const int b = blockIdx.z, hh = blockIdx.y;
+  const Blk bk = xcd_block();
+  const int b = bk.z, hh = bk.y;
   const int d = f.heads * HD;
   const int nkg = (f.kv_len + KG - 1) / KG;
-  const int kg = blockIdx.x % nkg, qc = blockIdx.x / nkg;
+  const int kg = bk.x % nkg, qc = bk.x / nkg;
   const int qbeg = qc * p.qchunk, qend = min(f.q_len, qbeg + p.qchunk);
   const float c = f.scale * kLog2e, inv_scale = 1.f / f.scale;
   const uint8_t* mb = f.key_padding_mask ? f.key_padding_mask + b * f.mask_bs : nullptr;

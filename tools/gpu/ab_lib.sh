@@ -13,9 +13,9 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/ab
 mkdir -p $O
 cd $R
-TOOL=$1; K=${2:+-k "$2"}
-eval timeout -k 10 600 python -u -m pytest -q --timeout 120 --timeout-method thread \
-  tests/test_gpu_ops.py tests/test_gpu_configs.py tests/test_gpu_attention.py -x $K > $O/tests.log 2>&1
+TOOL=$1; KARGS=(); [ -n "$2" ] && KARGS=(-k "$2")
+timeout -k 10 600 python -u -m pytest -q --timeout 120 --timeout-method thread \
+  tests/test_gpu_ops.py tests/test_gpu_configs.py tests/test_gpu_attention.py -x "${KARGS[@]}" > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 $O/tests.log
 [ $rc -eq 0 ] || exit 1
 for i in 1 2 3; do
