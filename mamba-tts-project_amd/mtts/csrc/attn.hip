@@ -422,20 +422,29 @@ __global__ __launch_bounds__(256, 4) void attn_fwd_db_kernel(MttsAttnFwdArgs a) 
   const __amdgpu_buffer_rsrc_t rk = brsrc(kbase, (uint32_t)(((int64_t)(a.kv_len - 1) * a.k_ls + HD) * 2));
   const __amdgpu_buffer_rsrc_t rv = brsrc(vbase, (uint32_t)(((int64_t)(a.kv_len - 1) * a.k_ls + HD) * 2));
   const __amdgpu_buffer_rsrc_t rm = brsrc(mb ? mb : (const uint8_t*)kbase, mb ? (uint32_t)a.kv_len : 0u);
-  uint32_t ok_[NPF];   // K and V share the row stride (host)
+  // K and V share the row stride (host).  hd 64: chunk i of a thread lies
+  // 256 / (HD / CH) rows below chunk 0, so one lane offset serves all chunks
+  // and the rest rides in the scalar offset -- one VGPR fewer, which at 4
+  // waves per SIMD removes the spill whose in-loop reload made every block
+  // wait (vmcnt(0)) for the next block's prefetch (C5m 609 -> 598 us,
+  // profiles/r05_attn_ab_fwd_spill.txt; hd 128 measured 0.8 % slower so, keeps
+  // per-chunk lane offsets)
+  constexpr bool kOneOff = HD == 64;
+  uint32_t ok_[kOneOff ? 1 : NPF];
 #pragma unroll
-  for (int i = 0; i < NPF; ++i) {
+  for (int i = 0; i < (kOneOff ? 1 : NPF); ++i) {
     const int idx = tid + 256 * i;
     const int row = idx / (HD / CH), cc = (idx % (HD / CH)) * CH;
     ok_[i] = (uint32_t)((row * a.k_ls + cc) * 2);
   }
   auto fetch = [&](int k0) __attribute__((always_inline)) {
     pk0 = k0;
-    const int sk = (int)(k0 * a.k_ls * 2);
 #pragma unroll
     for (int i = 0; i < NPF; ++i) {
-      pk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, ok_[i], sk, 0));
-      pv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, ok_[i], sk, 0));
+      const int sk = (int)((k0 + (kOneOff ? i * (256 / (HD / CH)) : 0)) * a.k_ls * 2);
+      const uint32_t oi = ok_[kOneOff ? 0 : i];
+      pk[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rk, oi, sk, 0));
+      pv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rv, oi, sk, 0));
     }
     praw = __builtin_amdgcn_raw_buffer_load_b8(rm, (uint32_t)lane, k0, 0);
   };
