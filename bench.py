@@ -164,12 +164,17 @@ def train_bench(args, rank, world, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     assert torch.isfinite(loss).item(), "non-finite loss"
+    dpinfo = None
+    if dp is not None:
+        dpinfo = dp_breakdown(lambda: cross_entropy(model(tokens, text, z, text_mask=mask).view(-1, c["vocab"]),
+                                                    tokens.view(-1), ignore_index=0), dp, dev)
+        log(f"[bench] data parallel: {dpinfo}")
     ms = dt / args.steps * 1e3
     tokens_per_s = world * c["B"] * c["T"] * args.steps / dt
     ups = sum(p["uploads"] for p in opt._plans.values())
     log(f"[bench] optimizer descriptor uploads over {args.warmup + args.steps} steps: {ups}")
     del model, opt
-    return c, ms, tokens_per_s, (first_loss, float(loss.item()))
+    return c, ms, tokens_per_s, (first_loss, float(loss.item())), dpinfo
 
 
 def scan_roofline(dtype, B=32, L=8192, D=2048, iters=20, rounds=5, barrier=False):
@@ -497,6 +502,51 @@ def _max_over_ranks(v, world, dev):
     return float(t.item())
 
 
+def dp_breakdown(forward_loss, dp, dev, steps=3):
+    """N > 1: why a scaling record looks the way it does.  Runs
+    `steps` extra data-parallel steps after the timed region and reports, per
+    rank, the backward time (loss.backward() with the bucketed all-reduces
+    overlapping it) and the all-reduce time left EXPOSED after it (backward
+    end -> GradAllReduce.finish() return: the stream waits for the buckets
+    still in flight), medians over the steps, max over ranks; plus the bucket
+    layout.  HIP events on the compute stream on GPU, wall clock on CPU."""
+    import statistics
+    from mtts import wgrad
+    cuda = torch.device(dev).type == "cuda"
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    bwd, exposed = [], []
+    for _ in range(steps):
+        loss = forward_loss()
+        dp.zero_grad()
+        if cuda:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record()
+        t0 = time.perf_counter()
+        with wgrad.deferred():
+            loss.backward()
+        if cuda:
+            ev[1].record()
+        t1 = time.perf_counter()
+        dp.finish()
+        if cuda:
+            ev[2].record()
+            torch.cuda.synchronize()
+            bwd.append(ev[0].elapsed_time(ev[1]))
+            exposed.append(ev[1].elapsed_time(ev[2]))
+        else:
+            t2 = time.perf_counter()
+            bwd.append((t1 - t0) * 1e3)
+            exposed.append((t2 - t1) * 1e3)
+    rec = {"backward_ms": _max_over_ranks(statistics.median(bwd), world, dev),
+           "allreduce_exposed_ms": _max_over_ranks(statistics.median(exposed), world, dev),
+           "steps": steps,
+           "timing": ("median over steps of per-rank " + ("HIP-event" if cuda else "wall-clock") +
+                      " times on the compute stream, max over ranks; exposed = backward end -> "
+                      "GradAllReduce.finish() return")}
+    rec.update(dp.describe())
+    return rec
+
+
 def launch_check(args, world):
     """The N-rank plumbing without GPU work (CPU, gloo): process group,
     barrier-bracketed 'timed region', max-over-ranks time, rank-0 JSON."""
@@ -510,9 +560,19 @@ def launch_check(args, world):
         dist.all_reduce(x)
         dist.barrier()
     dt = _max_over_ranks(time.perf_counter() - t0, world, "cpu")
+    rec = {"metric": "launch-check", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "allreduce_ok": bool(x[0].item() == world * (world + 1) / 2), "seconds": dt}
+    if world > 1:
+        # the N > 1 line's data-parallel breakdown on a small CPU model (gloo)
+        from mtts.dp import GradAllReduce
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.GELU(), torch.nn.Linear(512, 256))
+        dp = GradAllReduce(list(model.parameters()), bucket_mb=0.25, first_bucket_mb=0.125)
+        xin = torch.randn(64, 256)
+        rec["dp"] = dp_breakdown(lambda: model(xin).square().mean(), dp, "cpu", steps=args.steps)
+        dp.remove()
     if rank == 0:
-        print(json.dumps({"metric": "launch-check", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "allreduce_ok": bool(x[0].item() == world * (world + 1) / 2), "seconds": dt}), flush=True)
+        print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -578,7 +638,7 @@ def main():
     roof = None
     if rank == 0 and world == 1 and not args.skip_extras:
         roof = (scan_roofline(torch.float32), scan_roofline(torch.bfloat16))
-    c, ms, tps, loss = train_bench(args, rank, world, dev)
+    c, ms, tps, loss, dpinfo = train_bench(args, rank, world, dev)
     scaling_leg = scan_scaling(rank, world, dev)
     log(f"[bench] step {ms:.2f} ms  {tps:.0f} tok/s  loss first warmup step {loss[0]} -> last timed step {loss[1]:.3e} "
         f"(one fixed batch; the decoder's unshifted targets, SURVEY quirk 4, make it learn the identity fast)")
@@ -597,6 +657,8 @@ def main():
     rec["step_mfma"] = {"bound": "mfma", "achieved": fl / (ms * 1e-3) / 1e12, "peak": BF16_PEAK / 1e12,
                         "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / BF16_PEAK, "flops_per_step": fl}
     rec["scan_scaling"] = scaling_leg
+    if dpinfo is not None:
+        rec["dp"] = dpinfo
     if roof is None:
         # N > 1 (or --skip-extras): the roofline kernel's per-GPU figure from the
         # weak leg (each rank ran the full north-star batch; slowest rank)

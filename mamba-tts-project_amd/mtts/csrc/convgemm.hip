@@ -20,8 +20,10 @@
 // (4096 cycles) per wave against 8 fragment reads, and fp32 operands cost
 // 32 flop per byte staged (a 64 x 64 tile: 16, which L2 cannot feed at the
 // fp32 MFMA rate).  Operands are register-staged (four float4 per thread and
-// operand, loaded one K-step ahead) into a double-buffered LDS image (64 KiB:
-// two workgroups per CU): NT tiles [row][32 k] with 16-B chunk c of row r at
+// operand, loaded one K-step ahead) into a double-buffered LDS image sized
+// for the TN tile (2 x 2 x 32 x 144 floats = 72 KiB per workgroup; two
+// workgroups per CU fit gfx950's 160 KiB of LDS -- above the 64 KiB per
+// workgroup of gfx942-class parts, a gfx950-only tile): NT tiles [row][32 k] with 16-B chunk c of row r at
 // c ^ (r & 7) (conflict-free ds_read_b128: a lane group's 16 rows hit 16
 // distinct slots), TN tiles [k][128 + 16] floats (the pad puts k-rows 0 / 1
 // on disjoint banks for ds_read_b32).  MFMA operands are swapped (B fragment
@@ -47,6 +49,10 @@ constexpr int kLd = 4;                      // float4 loads per thread and opera
 constexpr int kNtTile = kBM * kBK;          // floats per NT operand tile
 constexpr int kTnPitch = kBM + 16;          // floats per k-row of a TN tile
 constexpr int kTnTile = kBK * kTnPitch;
+// the double-buffered A / B image of convgemm_kernel, two workgroups per CU
+// (__launch_bounds__(kT, 2)) within gfx950's 160 KiB LDS
+static_assert(2 * 2 * std::max(kNtTile, kTnTile) * sizeof(float) * 2 <= 160 * 1024,
+              "convgemm: two workgroups' LDS images exceed gfx950's 160 KiB");
 
 struct RowMap {
   const float* p;        // halo maps: already moved back by halo_p rows (host)

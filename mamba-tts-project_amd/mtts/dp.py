@@ -32,12 +32,15 @@ import torch.distributed as dist
 
 from . import wgrad
 
+DEFER_LISTENER_LAUNCH = True
+
 
 class GradAllReduce:
     def __init__(self, params, bucket_mb: float = 128.0, group=None, first_bucket_mb: float = 8.0,
                  comm_dtype: torch.dtype = None):
         self.group = group
         self.world = dist.get_world_size(group)
+        self.bucket_mb, self.first_bucket_mb = bucket_mb, first_bucket_mb
         self.params = [p for p in params if p.requires_grad]
         order = list(reversed(self.params))
         dev = order[0].device
@@ -79,6 +82,8 @@ class GradAllReduce:
         self.cbuf = None if self.comm_dtype is None else torch.empty(total, device=dev, dtype=self.comm_dtype)
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
+        self.counted = set()     # ids of the parameters counted into their bucket this step
+        self.ready = []          # buckets completed inside a deferred flush, launched at the next hook
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
         # deferred weight gradients (mtts.wgrad) are written straight into the
         # bucket views and announced through the engine's listener
@@ -88,7 +93,7 @@ class GradAllReduce:
 
     def _deferred_ready(self, p):
         if p in self.views:
-            self._hook(p)
+            self._hook(p, from_listener=True)
 
     def zero_grad(self):
         """Start a step: drop the gradients (p.grad = None).  Autograd then
@@ -100,13 +105,20 @@ class GradAllReduce:
             p.grad = None
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
+        self.counted = set()
 
-    def _hook(self, p):
+    def _hook(self, p, from_listener=False):
         if p.grad is None:
             # autograd runs post-accumulate hooks even when a backward returned
             # no gradient for p -- the deferred weight gradients (mtts.wgrad)
             # do exactly that and announce p through the engine's listener
             return
+        if id(p) in self.counted:
+            # counted once per step: a deferred gradient flushed inside p's own
+            # backward (mtts.wgrad's mid-backward flush) is announced by the
+            # engine's listener AND then seen here by autograd's hook
+            return
+        self.counted.add(id(p))
         v = self.views[p]
         if p.grad is not v and p.grad.data_ptr() != v.data_ptr():
             # autograd allocated a fresh gradient (the optimizer's zero_grad
@@ -118,7 +130,17 @@ class GradAllReduce:
         b = self.bucket_of[p]
         self.pending[b] += 1
         if self.pending[b] == self.buckets[b][2]:
-            self._launch(b)
+            if from_listener and DEFER_LISTENER_LAUNCH:
+                self.ready.append(b)
+            else:
+                self._launch_ready()
+                self._launch(b)
+        elif not from_listener:
+            self._launch_ready()
+
+    def _launch_ready(self):
+        while self.ready:
+            self._launch(self.ready.pop(0))
 
     def _avg_op(self):
         """RCCL averages in the collective (ReduceOp.AVG: no separate 1/world
@@ -146,6 +168,7 @@ class GradAllReduce:
     def finish(self):
         """Wait for every bucket (launching any whose hooks did not all fire,
         e.g. unused parameters) and average over ranks."""
+        self._launch_ready()
         for p, v in self.views.items():   # no gradient this step: contributes zeros
             if p.grad is None:
                 v.zero_()
@@ -166,6 +189,16 @@ class GradAllReduce:
             self.flat.mul_(1.0 / self.world)
         self.handles = [None] * len(self.buckets)
         self.pending = [0] * len(self.buckets)
+        self.counted = set()
+
+    def describe(self) -> dict:
+        """Bucket layout, for the bench line (bench.py dp_breakdown)."""
+        es = self.flat.element_size()
+        return {"buckets": len(self.buckets), "bucket_mb": self.bucket_mb, "first_bucket_mb": self.first_bucket_mb,
+                "grad_MB": self.flat.numel() * es / 2 ** 20,
+                "bucket_MB": [round((e - s) * es / 2 ** 20, 3) for s, e, _ in self.buckets],
+                "comm_dtype": str(self.comm_dtype or self.flat.dtype).replace("torch.", ""),
+                "reduce_op": "avg" if self._avg_op() else "sum+scale"}
 
     def remove(self):
         for h in self.hooks:

@@ -23,8 +23,15 @@ the end-of-backward callback makes the caller's stream wait for it.
 Gradient semantics are autograd's: a parameter whose .grad is None gets a
 fresh gradient (or its data-parallel bucket view, mtts.dp), one whose .grad
 exists is accumulated into (beta = 1).  Listeners (mtts.dp.GradAllReduce)
-are told when a parameter's gradient is complete, so bucketed all-reduces
-still overlap the rest of the backward.
+are told ONCE per backward when a parameter's gradient is complete, so
+bucketed all-reduces still overlap the rest of the backward: at the flush
+that completes the union of its row slices (a parameter reached by several
+row-sliced projections, e.g. CrossAttention's separate q / k / v
+in-projections, is complete only when every slice has run), or at the end of
+the backward for one whose slices never cover it (the single-key path's
+value rows) or overlap (a weight used twice).  A parameter submitted again
+after it was announced would reach its all-reduce with a stale gradient:
+that raises.
 
 Opt-in per backward pass:  `with mtts.wgrad.deferred(): loss.backward()`
 (bench.py and train_harness.py do).  Outside it, or when a shape does not
@@ -58,10 +65,10 @@ _depth = 0
 
 
 class _Job:
-    __slots__ = ("dy", "x", "param", "rows", "last")
+    __slots__ = ("dy", "x", "param", "rows")
 
-    def __init__(self, dy, x, param, rows, last):
-        self.dy, self.x, self.param, self.rows, self.last = dy, x, param, rows, last
+    def __init__(self, dy, x, param, rows):
+        self.dy, self.x, self.param, self.rows = dy, x, param, rows
 
     def tiles(self):
         m, n = self.dy.shape[1], self.x.shape[1]
@@ -73,7 +80,8 @@ class _Engine:
         self.jobs = []
         self.tiles = 0
         self.callback_queued = False
-        self.done = set()        # ids of params whose gradient is complete this backward
+        self.done = set()        # ids of params announced complete this backward
+        self.covered = {}        # id(param) -> (param, [(r0, r1), ...] rows flushed this backward, overlapped)
         self.listeners = []
         self.side = {}           # device index -> side stream
         self.used_side = None    # (main, side) streams of this backward
@@ -81,6 +89,7 @@ class _Engine:
     def reset_pass(self):
         self.callback_queued = False
         self.done = set()
+        self.covered = {}
         self.used_side = None
 
 
@@ -128,7 +137,30 @@ def _end_of_backward():
     if _E.used_side is not None:   # gradients complete before anything after the backward
         main, side = _E.used_side
         main.wait_stream(side)
+    # parameters whose flushed slices never covered them or overlapped
+    for key, (p, _, _) in list(_E.covered.items()):
+        if key not in _E.done:
+            _announce(p)
     _E.reset_pass()
+
+
+def _announce(p):
+    _E.done.add(id(p))
+    for fn in _E.listeners:
+        fn(p)
+
+
+def _cover(p, rows):
+    """Record rows (r0, r1) of p as flushed; True once their union is all of p
+    and no two slices overlapped."""
+    r0, r1 = rows if rows is not None else (0, p.shape[0])
+    _, ivs, overlap = _E.covered.get(id(p), (p, [], False))
+    overlap = overlap or any(a < r1 and r0 < b for a, b in ivs)
+    ivs = ivs + [(r0, r1)]
+    _E.covered[id(p)] = (p, ivs, overlap)
+    if overlap:
+        return False
+    return sum(b - a for a, b in ivs) >= p.shape[0]
 
 
 def _side_stream(dev):
@@ -153,13 +185,17 @@ def submit(jobs, narrow=False) -> bool:
         r0, r1 = rows if rows is not None else (0, p.shape[0])
         if p is not param or p.shape[1] != x.shape[1] or r1 - r0 != dy.shape[1]:
             return False
+    if id(param) in _E.done and _E.listeners:
+        raise RuntimeError("wgrad: a parameter's weight gradient was submitted after its gradient was announced "
+                           "complete to a listener (a weight used again later in the backward under GradAllReduce); "
+                           "run this backward outside mtts.wgrad.deferred()")
     if any(j.param is param for j in _E.jobs):   # e.g. a weight shared by two modules: keep the order
         flush()
     if not _E.callback_queued:
         torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
         _E.callback_queued = True
-    for i, (dy, x, p, rows) in enumerate(jobs):
-        j = _Job(dy, x, p, rows, i == len(jobs) - 1)
+    for dy, x, p, rows in jobs:
+        j = _Job(dy, x, p, rows)
         _E.jobs.append(j)
         _E.tiles += j.tiles()
     if _E.tiles >= GROUP_TILES or len(_E.jobs) >= MAX_PROBLEMS - 2:
@@ -239,11 +275,12 @@ def _flush(jobs, side=None):
         g, _, fresh = dest[id(j.param)]
         if fresh and j.param.grad is None:
             j.param.grad = g
+    complete = {}
     for j in jobs:
-        if j.last and id(j.param) not in _E.done:
-            _E.done.add(id(j.param))
-            for fn in _E.listeners:
-                fn(j.param)
+        if _cover(j.param, j.rows) and id(j.param) not in _E.done:
+            complete[id(j.param)] = j.param
+    for p in complete.values():
+        _announce(p)
 
 
 def _addressable(out):

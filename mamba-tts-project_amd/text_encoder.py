@@ -73,7 +73,7 @@ class EmbeddingFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, d).contiguous()
         n = dy2.shape[0]
         Vp = (V + 1 + 3) // 4 * 4                 # + one discard column, a multiple of 4
-        cols = ids.reshape(-1)
+        cols = ids.reshape(-1).long()      # scatter_ takes int64 indices (int32 ids are valid input)
         if pad is not None:
             cols = torch.where(cols == pad, torch.full_like(cols, V), cols)
         onehot = torch.zeros(n, Vp, device=dy.device, dtype=torch.float32)
@@ -239,17 +239,19 @@ class FFTBlock(nn.Module):
         self.pos_ffn = PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout=dropout)
 
     def forward(self, enc_input, mask=None, slf_attn_mask=None, keep=None):
-        """keep (optional): (~mask)[..., None] in the activation dtype, made
-        once by TextEncoder for all its blocks."""
+        """keep (optional): (~mask)[..., None] as bool, expanded to the
+        activation's shape, made once by TextEncoder for all its blocks."""
         keypad = mask                      # slf_attn_mask = mask expanded over queries: the key pad mask
         enc_output, attn = self.slf_attn(enc_input, enc_input, enc_input, mask=keypad)
-        # masked_fill(mask, 0) as a product with the keep mask: one kernel each
-        # way instead of a clone + fill (padded rows become +-0)
+        # masked_fill(mask, 0) as torch.where over the keep mask: one kernel
+        # each way instead of a clone + fill; like masked_fill it zeroes the NaN
+        # rows a zero-length sequence's all-masked softmax leaves
         if keep is None:
-            keep = (~mask).unsqueeze(-1).to(enc_output.dtype)
-        enc_output = enc_output * keep
+            keep = (~mask).unsqueeze(-1)
+        zero = enc_output.new_zeros(())
+        enc_output = torch.where(keep, enc_output, zero)
         enc_output = self.pos_ffn(enc_output)
-        enc_output = enc_output * keep
+        enc_output = torch.where(keep, enc_output, zero)
         return enc_output, attn
 
 
@@ -287,9 +289,9 @@ class TextEncoder(nn.Module):
             pos = self.position_enc[0, :L].to(emb.dtype)
         x = emb + pos[None]
         attns = []
-        # full-width keep mask: the 8 masking products per direction then run
+        # full-width keep mask: the 8 masking selects per direction then run
         # as vectorised same-shape kernels instead of broadcasting ones
-        keep = (~mask).unsqueeze(-1).to(x.dtype).expand(x.shape).contiguous()
+        keep = (~mask).unsqueeze(-1).expand(x.shape).contiguous()
         for layer in self.layer_stack:
             x, a = layer(x, mask=mask, slf_attn_mask=None, keep=keep)
             if return_attns:

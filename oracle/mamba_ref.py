@@ -18,7 +18,11 @@ vectors produced in the build container from
   * the reference ``mamba_decoder.py`` / ``style_cross_attention.py`` imported
     with a ``mamba_ssm`` shim that wraps HF's mixer and honours the documented
     ``out, state = mamba(x[, state])`` contract (``mamba_decoder.py:10-15``).
-See tests/golden/make_golden.py.
+The text-encoder / duration-predictor restatements (text_encoder_ref,
+duration_predictor_ref, duration_loss_ref, sinusoid_table_ref) are pinned
+against the reference ``text_encoder.py`` itself, imported behind a
+``lib.FastSpeech2`` shim that restates the three FastSpeech2 names it imports
+(tests/golden/text.npz).  See tests/golden/make_golden.py.
 
 Layouts follow upstream mamba-ssm: u/delta/z are (B, D, L), B/C are (B, N, L).
 Everything runs in the dtype and on the device of the inputs (tests use
@@ -195,15 +199,26 @@ def _conv_ref(x, w, b, pad):
     return F.conv1d(x.transpose(1, 2), w, b, padding=pad).transpose(1, 2)
 
 
-def text_encoder_ref(p, ids, mask, n_layers, n_head, d_k, kernel=(9, 1)):
+def text_encoder_ref(p, ids, mask, n_layers, n_head, d_k, kernel=(9, 1), training=True, relu=torch.relu,
+                     padding_idx=0):
     """Restates text_encoder.py:87-128 with FastSpeech2's FFTBlock /
     MultiHeadAttention / ScaledDotProductAttention / PositionwiseFeedForward
     (transformer/Layers.py, SubLayers.py, Modules.py; ming024, unpinned):
     x = emb + pos; per layer: attn = softmax(q k^T / sqrt(d_k), pad keys -inf)
     v -> fc -> LN(+res) -> masked_fill(pad, 0) -> conv FFN -> LN(+res) ->
-    masked_fill(pad, 0).  Dropout off."""
+    masked_fill(pad, 0).  Dropout off.  Positions: position_enc[:, :L]
+    (padding row 0 zeroed), or -- eval mode with L > max_seq_len
+    (text_encoder.py:107-112) -- a fresh fp32 table of L rows with row 0 NOT
+    zeroed.  The embedding's padding_idx row receives no gradient
+    (nn.Embedding(padding_idx), :69-71).  `relu` (tests): the FFN's activation, e.g. one that applies a
+    recorded mask so the comparison follows the kernel's side of the kink."""
     B, L = ids.shape
-    x = p["phoneme_emb.weight"][ids] + p["position_enc"][0, :L][None]
+    n_pos = p["position_enc"].shape[1]
+    if not training and L > n_pos - 1:
+        pos = sinusoid_table_ref(L, p["position_enc"].shape[2]).float().to(p["phoneme_emb.weight"].dtype)
+    else:
+        pos = p["position_enc"][0, :L]
+    x = F.embedding(ids, p["phoneme_emb.weight"], padding_idx=padding_idx) + pos[None]
     for i in range(n_layers):
         pre = f"layer_stack.{i}."
         res = x
@@ -220,21 +235,21 @@ def text_encoder_ref(p, ids, mask, n_layers, n_head, d_k, kernel=(9, 1)):
         x = layer_norm_ref(o + res, p[pre + "slf_attn.layer_norm.weight"], p[pre + "slf_attn.layer_norm.bias"])
         x = x.masked_fill(mask[..., None], 0.0)
         res = x
-        h = torch.relu(_conv_ref(x, p[pre + "pos_ffn.w_1.weight"], p[pre + "pos_ffn.w_1.bias"], (kernel[0] - 1) // 2))
+        h = relu(_conv_ref(x, p[pre + "pos_ffn.w_1.weight"], p[pre + "pos_ffn.w_1.bias"], (kernel[0] - 1) // 2))
         h = _conv_ref(h, p[pre + "pos_ffn.w_2.weight"], p[pre + "pos_ffn.w_2.bias"], (kernel[1] - 1) // 2)
         x = layer_norm_ref(h + res, p[pre + "pos_ffn.layer_norm.weight"], p[pre + "pos_ffn.layer_norm.bias"])
         x = x.masked_fill(mask[..., None], 0.0)
     return x
 
 
-def duration_predictor_ref(p, x, mask, kernel=3):
+def duration_predictor_ref(p, x, mask, kernel=3, relu=torch.relu):
     """Restates text_encoder.py:131-181 -> FastSpeech2 model/modules.py
     VariancePredictor: [conv(k, pad (k-1)/2) -> relu -> LN] x 2 (the second
     conv's padding is 1) -> linear -> squeeze -> masked_fill(pad, 0)."""
     c = "predictor.conv_layer."
-    h = torch.relu(_conv_ref(x, p[c + "conv1d_1.conv.weight"], p[c + "conv1d_1.conv.bias"], (kernel - 1) // 2))
+    h = relu(_conv_ref(x, p[c + "conv1d_1.conv.weight"], p[c + "conv1d_1.conv.bias"], (kernel - 1) // 2))
     h = layer_norm_ref(h, p[c + "layer_norm_1.weight"], p[c + "layer_norm_1.bias"])
-    h = torch.relu(_conv_ref(h, p[c + "conv1d_2.conv.weight"], p[c + "conv1d_2.conv.bias"], 1))
+    h = relu(_conv_ref(h, p[c + "conv1d_2.conv.weight"], p[c + "conv1d_2.conv.bias"], 1))
     h = layer_norm_ref(h, p[c + "layer_norm_2.weight"], p[c + "layer_norm_2.bias"])
     out = (h @ p["predictor.linear_layer.weight"].T + p["predictor.linear_layer.bias"]).squeeze(-1)
     return out.masked_fill(mask, 0.0) if mask is not None else out
@@ -412,14 +427,15 @@ def heuristic_durations_ref(text_mask, target_frames):
 def duration_loss_ref(log_duration_pred, duration_target, mask=None):
     """Restates DurationPredictor.compute_loss (text_encoder.py:183-209): MSE in
     the log domain, masked mean over non-pad phonemes."""
-    log_t = torch.log(duration_target.to(log_duration_pred.dtype) + 1e-8)
+    log_t = torch.log(duration_target.float() + 1e-8).to(log_duration_pred.dtype)   # target built in fp32 (:196)
     loss = F.mse_loss(log_duration_pred, log_t, reduction="none")
     if mask is not None:
         return loss.masked_fill(mask, 0.0).sum() / (~mask).sum().to(loss.dtype)
     return loss.mean()
 
 
-def train_step_losses_ref(p_te, p_dur, p_dec, batch, te_cfg, dec_cfg, w_codec=1.0, w_dur=0.1, w_smsd=0.5):
+def train_step_losses_ref(p_te, p_dur, p_dec, batch, te_cfg, dec_cfg, w_codec=1.0, w_dur=0.1, w_smsd=0.5,
+                          relu=torch.relu):
     """Restates the loss of one train.py step (train.py:168-230) on a synthetic
     batch, dropout off, SMSD absent (spk_embs None -> loss_smsd = 0, :192;
     z_style = the batch's fixed style vector in place of smsd(style_prompts)):
@@ -433,8 +449,8 @@ def train_step_losses_ref(p_te, p_dur, p_dec, batch, te_cfg, dec_cfg, w_codec=1.
     audio_tokens = codec.permute(0, 2, 1).reshape(B, -1)                          # :181-182
     ids, tmask = batch["phoneme_ids"], batch["text_mask"]
     text_hidden = text_encoder_ref(p_te, ids, tmask, te_cfg["n_layers"], te_cfg["n_head"], te_cfg["d_k"],
-                                   te_cfg.get("kernel", (9, 1)))                   # :188
-    log_dur = duration_predictor_ref(p_dur, text_hidden, tmask)                    # :198
+                                   te_cfg.get("kernel", (9, 1)), relu=relu)        # :188
+    log_dur = duration_predictor_ref(p_dur, text_hidden, tmask, relu=relu)         # :198
     dur_t = heuristic_durations_ref(tmask, audio_tokens.shape[1])                  # :201
     loss_dur = duration_loss_ref(log_dur, dur_t, tmask)                            # :202
     v3 = batch["voice_codec"].permute(0, 2, 1)                                     # :216

@@ -91,6 +91,165 @@ def import_reference():
     return mamba_decoder, style_cross_attention
 
 
+# ---------------------------------------------------------------------------
+# lib.FastSpeech2 shim: the three names /root/reference/text_encoder.py:16-18
+# imports from ming024/FastSpeech2 (cloned unpinned by setup.sh, absent here),
+# restated from that repository's published code -- transformer/Models.py
+# get_sinusoid_encoding_table, transformer/Layers.py FFTBlock,
+# transformer/SubLayers.py MultiHeadAttention + PositionwiseFeedForward,
+# transformer/Modules.py ScaledDotProductAttention, model/modules.py
+# VariancePredictor + Conv.  Written against torch directly (independent of
+# the product's text_encoder.py); the reference's OWN code around them
+# (TextEncoder.forward's embedding, position_enc slice and eval branch,
+# DurationPredictor.compute_loss, TextProcessor) runs unmodified.
+# ---------------------------------------------------------------------------
+def fs2_sinusoid_table(n_position, d_hid, padding_idx=None):
+    def angle(pos, j):
+        return pos / np.power(10000, 2 * (j // 2) / d_hid)
+
+    table = np.array([[angle(p, j) for j in range(d_hid)] for p in range(n_position)])
+    table[:, 0::2] = np.sin(table[:, 0::2])
+    table[:, 1::2] = np.cos(table[:, 1::2])
+    if padding_idx is not None:
+        table[padding_idx] = 0.0
+    return torch.FloatTensor(table)
+
+
+class FS2ScaledDotProductAttention(nn.Module):
+    def __init__(self, temperature):
+        super().__init__()
+        self.temperature = temperature
+        self.softmax = nn.Softmax(dim=2)
+
+    def forward(self, q, k, v, mask=None):
+        attn = torch.bmm(q, k.transpose(1, 2)) / self.temperature
+        if mask is not None:
+            attn = attn.masked_fill(mask, -np.inf)
+        attn = self.softmax(attn)
+        return torch.bmm(attn, v), attn
+
+
+class FS2MultiHeadAttention(nn.Module):
+    def __init__(self, n_head, d_model, d_k, d_v, dropout=0.1):
+        super().__init__()
+        self.n_head, self.d_k, self.d_v = n_head, d_k, d_v
+        self.w_qs = nn.Linear(d_model, n_head * d_k)
+        self.w_ks = nn.Linear(d_model, n_head * d_k)
+        self.w_vs = nn.Linear(d_model, n_head * d_v)
+        self.attention = FS2ScaledDotProductAttention(temperature=np.power(d_k, 0.5))
+        self.layer_norm = nn.LayerNorm(d_model)
+        self.fc = nn.Linear(n_head * d_v, d_model)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, q, k, v, mask=None):
+        d_k, d_v, n_head = self.d_k, self.d_v, self.n_head
+        sz_b, len_q, _ = q.size()
+        _, len_k, _ = k.size()
+        _, len_v, _ = v.size()
+        residual = q
+        q = self.w_qs(q).view(sz_b, len_q, n_head, d_k)
+        k = self.w_ks(k).view(sz_b, len_k, n_head, d_k)
+        v = self.w_vs(v).view(sz_b, len_v, n_head, d_v)
+        q = q.permute(2, 0, 1, 3).contiguous().view(-1, len_q, d_k)
+        k = k.permute(2, 0, 1, 3).contiguous().view(-1, len_k, d_k)
+        v = v.permute(2, 0, 1, 3).contiguous().view(-1, len_v, d_v)
+        mask = mask.repeat(n_head, 1, 1)
+        output, attn = self.attention(q, k, v, mask=mask)
+        output = output.view(n_head, sz_b, len_q, d_v)
+        output = output.permute(1, 2, 0, 3).contiguous().view(sz_b, len_q, -1)
+        output = self.dropout(self.fc(output))
+        return self.layer_norm(output + residual), attn
+
+
+class FS2PositionwiseFeedForward(nn.Module):
+    def __init__(self, d_in, d_hid, kernel_size, dropout=0.1):
+        super().__init__()
+        self.w_1 = nn.Conv1d(d_in, d_hid, kernel_size=kernel_size[0], padding=(kernel_size[0] - 1) // 2)
+        self.w_2 = nn.Conv1d(d_hid, d_in, kernel_size=kernel_size[1], padding=(kernel_size[1] - 1) // 2)
+        self.layer_norm = nn.LayerNorm(d_in)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x):
+        residual = x
+        output = self.w_2(torch.relu(self.w_1(x.transpose(1, 2)))).transpose(1, 2)
+        return self.layer_norm(self.dropout(output) + residual)
+
+
+class FS2FFTBlock(nn.Module):
+    def __init__(self, d_model, n_head, d_k, d_v, d_inner, kernel_size, dropout=0.1):
+        super().__init__()
+        self.slf_attn = FS2MultiHeadAttention(n_head, d_model, d_k, d_v, dropout=dropout)
+        self.pos_ffn = FS2PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout=dropout)
+
+    def forward(self, enc_input, mask=None, slf_attn_mask=None):
+        enc_output, enc_slf_attn = self.slf_attn(enc_input, enc_input, enc_input, mask=slf_attn_mask)
+        enc_output = enc_output.masked_fill(mask.unsqueeze(-1), 0)
+        enc_output = self.pos_ffn(enc_output)
+        enc_output = enc_output.masked_fill(mask.unsqueeze(-1), 0)
+        return enc_output, enc_slf_attn
+
+
+class FS2Conv(nn.Module):
+    def __init__(self, in_channels, out_channels, kernel_size=1, stride=1, padding=0, dilation=1, bias=True,
+                 w_init="linear"):
+        super().__init__()
+        self.conv = nn.Conv1d(in_channels, out_channels, kernel_size=kernel_size, stride=stride, padding=padding,
+                              dilation=dilation, bias=bias)
+
+    def forward(self, x):
+        return self.conv(x.contiguous().transpose(1, 2)).contiguous().transpose(1, 2)
+
+
+class FS2VariancePredictor(nn.Module):
+    def __init__(self, model_config):
+        super().__init__()
+        from collections import OrderedDict
+        self.input_size = model_config["transformer"]["encoder_hidden"]
+        self.filter_size = model_config["variance_predictor"]["filter_size"]
+        self.kernel = model_config["variance_predictor"]["kernel_size"]
+        self.conv_output_size = model_config["variance_predictor"]["filter_size"]
+        self.dropout = model_config["variance_predictor"]["dropout"]
+        self.conv_layer = nn.Sequential(OrderedDict([
+            ("conv1d_1", FS2Conv(self.input_size, self.filter_size, kernel_size=self.kernel,
+                                 padding=(self.kernel - 1) // 2)),
+            ("relu_1", nn.ReLU()),
+            ("layer_norm_1", nn.LayerNorm(self.filter_size)),
+            ("dropout_1", nn.Dropout(self.dropout)),
+            ("conv1d_2", FS2Conv(self.filter_size, self.filter_size, kernel_size=self.kernel, padding=1)),
+            ("relu_2", nn.ReLU()),
+            ("layer_norm_2", nn.LayerNorm(self.filter_size)),
+            ("dropout_2", nn.Dropout(self.dropout)),
+        ]))
+        self.linear_layer = nn.Linear(self.conv_output_size, 1)
+
+    def forward(self, encoder_output, mask):
+        out = self.linear_layer(self.conv_layer(encoder_output)).squeeze(-1)
+        if mask is not None:
+            out = out.masked_fill(mask, 0.0)
+        return out
+
+
+def import_reference_text_encoder():
+    """/root/reference/text_encoder.py itself, behind the lib.FastSpeech2 shim."""
+    import importlib.util
+    names = {
+        "lib": {}, "lib.FastSpeech2": {}, "lib.FastSpeech2.transformer": {}, "lib.FastSpeech2.model": {},
+        "lib.FastSpeech2.transformer.Models": {"get_sinusoid_encoding_table": fs2_sinusoid_table},
+        "lib.FastSpeech2.transformer.Layers": {"FFTBlock": FS2FFTBlock},
+        "lib.FastSpeech2.model.modules": {"VariancePredictor": FS2VariancePredictor},
+    }
+    for name, attrs in names.items():
+        mod = types.ModuleType(name)
+        mod.__path__ = []
+        for k, v in attrs.items():
+            setattr(mod, k, v)
+        sys.modules[name] = mod
+    spec = importlib.util.spec_from_file_location("ref_text_encoder", os.path.join(REF, "text_encoder.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def f32(t):
     return t.detach().to(torch.float32).cpu().numpy()
 
@@ -311,8 +470,180 @@ def gen_regulator(msca, seed=7):
     save("regulator.npz", **arrays)
 
 
+# ---------------------------------------------------------------------------
+# 5. text encoder / duration predictor / text processor through the REFERENCE
+#    text_encoder.py (behind the lib.FastSpeech2 shim)
+# ---------------------------------------------------------------------------
+TEXT = dict(vocab_size=40, d_model=64, n_layers=2, n_head=2, d_k=32, d_v=32, d_inner=128, kernel_size=(9, 1),
+            dropout=0.0, max_seq_len=48, padding_idx=0)
+DUR = dict(d_model=64, filter_size=128, kernel_size=3, dropout=0.0)
+RELU_MARGIN = 2e-5    # every ReLU pre-activation at least this far from 0 (fp32 rounding cannot flip one)
+
+
+def _pad_batch(g, lengths, V, L):
+    ids = torch.randint(1, V, (len(lengths), L), generator=g)
+    mask = torch.arange(L)[None] >= torch.tensor(lengths)[:, None]   # True = pad (text_encoder.py:93)
+    ids[mask] = 0
+    return ids, mask
+
+
+def _relu_margin(model, run):
+    """min |pre-activation| over every ReLU input the reference computes in run()."""
+    pres = []
+    hooks = []
+    for name, mod in model.named_modules():
+        if name.endswith("pos_ffn.w_1") or name.endswith("conv1d_1") or name.endswith("conv1d_2"):
+            hooks.append(mod.register_forward_hook(lambda m, i, o: pres.append(o.detach().abs().min().item())))
+    try:
+        run()
+    finally:
+        for h in hooks:
+            h.remove()
+    return min(pres)
+
+
+def gen_text(mte, seed=11):
+    arrays = {}
+    for attempt in range(50):
+        s = seed + 1000 * attempt
+        torch.manual_seed(s)
+        g = torch.Generator().manual_seed(s + 1)
+        enc = mte.TextEncoder(**TEXT).double()
+        perturb_norms(enc, g)
+        with torch.no_grad():
+            for n, p in enc.named_parameters():
+                if n.endswith("bias"):
+                    p.copy_(0.1 * torch.randn(p.shape, generator=g, dtype=p.dtype))
+        sd = {k: f32(v) for k, v in enc.state_dict().items()}
+        enc.load_state_dict({k: torch.from_numpy(v).double() for k, v in sd.items()})
+        ids_t, mask_t = _pad_batch(g, [37, 20, 29], TEXT["vocab_size"], 37)
+        ids_t[0, 5] = 0          # the padding id inside a valid span: zero embedding row, no gradient
+        ids_e, mask_e = _pad_batch(g, [60, 45], TEXT["vocab_size"], 60)   # eval branch: L > max_seq_len
+        ids_z, mask_z = _pad_batch(g, [52, 0, 17], TEXT["vocab_size"], 52)  # a zero-length row (forward only)
+        enc.train()
+        m_train = _relu_margin(enc, lambda: enc(ids_t, mask=mask_t))
+        enc.eval()
+        m_eval = _relu_margin(enc, lambda: enc(ids_e, mask=mask_e))
+        if min(m_train, m_eval) > RELU_MARGIN:
+            break
+    print(f"text encoder seed {s}: relu margins train {m_train:.2e} eval {m_eval:.2e}")
+    arrays.update({f"enc/sd/{k}": v for k, v in sd.items()})
+    arrays["enc/seed"] = np.array(s)
+    for tag, ids, mask, train in (("train", ids_t, mask_t, True), ("eval", ids_e, mask_e, False)):
+        enc.train(train)
+        enc.zero_grad()
+        out = enc(ids, mask=mask)
+        w = rnd(g, *out.shape)
+        (out * w).sum().backward()
+        arrays.update({f"{tag}/ids": ids.numpy(), f"{tag}/mask": mask.numpy(), f"{tag}/out": f32(out),
+                       f"{tag}/w": f32(w)})
+        for n, p in enc.named_parameters():
+            if p.requires_grad:
+                arrays[f"{tag}/grad/{n}"] = f32(p.grad)
+    enc.eval()
+    with torch.no_grad():
+        out_z = enc(ids_z, mask=mask_z)
+    assert torch.isfinite(out_z).all()
+    arrays.update({"empty/ids": ids_z.numpy(), "empty/mask": mask_z.numpy(), "empty/out": f32(out_z)})
+
+    # DurationPredictor (text_encoder.py:131-209): forward + compute_loss, masked and not
+    for attempt in range(50):
+        s = seed + 7 + 1000 * attempt
+        torch.manual_seed(s)
+        g = torch.Generator().manual_seed(s + 1)
+        dp = mte.DurationPredictor(**DUR).double()
+        perturb_norms(dp, g)
+        with torch.no_grad():
+            for n, p in dp.named_parameters():
+                if n.endswith("bias"):
+                    p.copy_(0.1 * torch.randn(p.shape, generator=g, dtype=p.dtype))
+        sd = {k: f32(v) for k, v in dp.state_dict().items()}
+        dp.load_state_dict({k: torch.from_numpy(v).double() for k, v in sd.items()})
+        x = rnd(g, 3, 29, DUR["d_model"])
+        _, dmask = _pad_batch(g, [29, 11, 23], 10, 29)
+        if _relu_margin(dp, lambda: dp(x, mask=dmask)) > RELU_MARGIN:
+            break
+    dp.train()
+    target = torch.randint(1, 9, (3, 29), generator=g).double()
+    target[dmask] = 0.0
+    target[0, 3] = 0.0           # a zero duration inside a valid span: log(1e-8)
+    xr = x.clone().requires_grad_(True)
+    pred = dp(xr, mask=dmask)
+    # compute_loss builds its target in float32 (duration_target.float(),
+    # text_encoder.py:196) as it runs in train.py on fp32 predictions: the loss
+    # stage runs on the fp32-rounded prediction and its gradient is carried back
+    # through the float64 predictor
+    pred32 = pred.detach().float().requires_grad_(True)
+    loss = dp.compute_loss(pred32, target, mask=dmask)
+    loss.backward()
+    pred.backward(pred32.grad.double())
+    with torch.no_grad():
+        loss_nomask = dp.compute_loss(dp(x, mask=None).float(), target.clamp(min=1.0))
+    arrays.update({f"dur/sd/{k}": v for k, v in sd.items()})
+    arrays.update({"dur/x": f32(x), "dur/mask": dmask.numpy(), "dur/target": f32(target), "dur/pred": f32(pred),
+                   "dur/loss": f32(loss), "dur/loss_nomask": f32(loss_nomask), "dur/dx": f32(xr.grad)})
+    for n, p in dp.named_parameters():
+        arrays[f"dur/grad/{n}"] = f32(p.grad)
+    # the positional table the reference builds (FastSpeech2's, padding row zeroed) and the eval-branch one
+    arrays["table/pad"] = f32(mte.TextProcessor(vocab_list=["<PAD>", "a"]).create_positional_encoding(10, 8))
+    arrays["table/eval"] = f32(fs2_sinusoid_table(60, TEXT["d_model"]))
+    save("text.npz", **arrays)
+
+
+G2P = {"dict": lambda t: {"ph": t}, "str": lambda t: " ".join(reversed(t.split())), "list": lambda t: t.split()[1:]}
+
+
+def gen_text_processor(mte):
+    """TextProcessor (text_encoder.py:212-428) on the reference's own
+    phoneme_vocab.json and two list vocabularies -> text_processor.json
+    (inputs and the reference's outputs; ints, strings and bools only)."""
+    import json
+    vocabs = {"file": None,
+              "unk_custom_pad": ["<UNK>", "AA0", "B", "<SIL>", "K"],
+              "no_specials": ["x", "y", "z"]}
+    texts = ["HH AH0 L OW1 , W ER1 L D .", "", "K AE1 T QQ S AE1 T", "B IY1 | XX YY ZZ", "  AA0   B  ",
+             "x y z w", "<PAD> <UNK> <SIL>"]
+    cases = []
+    for vname, vlist in vocabs.items():
+        kw = {"vocab_path": os.path.join(REF, "phoneme_vocab.json")} if vlist is None else {"vocab_list": vlist}
+        if vname == "unk_custom_pad":
+            kw["padding_token"] = "<SIL>"
+        tp = mte.TextProcessor(**kw)
+        case = {"vocab": vname, "kwargs": {k: v for k, v in kw.items() if k != "vocab_path"},
+                "vocab_size": tp.vocab_size, "padding_id": tp.padding_id, "unk_id": tp.unk_id, "batches": [],
+                "process": [], "ids_to_phonemes": []}
+        for max_length in (None, 3, 0):
+            for pad in (True, False):
+                ids, lengths, masks = tp.batch_process(texts, max_length=max_length, pad_to_max=pad)
+                case["batches"].append({
+                    "max_length": max_length, "pad_to_max": pad, "lengths": lengths,
+                    "ids": ids.tolist() if pad else [t.tolist() for t in ids],
+                    "masks": None if masks is None else masks.tolist(),
+                    "ids_shape": list(ids.shape) if pad else None})
+        ids, lengths, masks = tp.batch_process([], pad_to_max=True)
+        case["empty_batch"] = {"ids_shape": list(ids.shape), "lengths": lengths, "masks_shape": list(masks.shape)}
+        for gname, fn in list(G2P.items()) + [(None, None)]:
+            for t in texts[:4]:
+                pids, phs = tp.process_text(t, g2p_processor=fn, max_length=5)
+                case["process"].append({"text": t, "g2p": gname, "ids": pids, "phonemes": phs})
+        case["ids_to_phonemes"] = {"ids": [0, 1, 2, 4, 77, 78, 79, 500, -1],
+                                   "phonemes": tp.ids_to_phonemes([0, 1, 2, 4, 77, 78, 79, 500, -1])}
+        emb = tp.create_phoneme_embedding(8)
+        case["embedding"] = {"num": emb.num_embeddings, "dim": emb.embedding_dim, "padding_idx": emb.padding_idx}
+        cases.append(case)
+    path = os.path.join(HERE, "text_processor.json")
+    with open(path, "w", encoding="utf-8") as f:
+        json.dump({"texts": texts, "cases": cases}, f, ensure_ascii=False, indent=0)
+    print(f"wrote text_processor.json: {os.path.getsize(path) / 1024:.1f} KiB")
+
+
 def main():
     torch.set_num_threads(8)
+    if sys.argv[1:] == ["text"]:
+        mte = import_reference_text_encoder()
+        gen_text(mte)
+        gen_text_processor(mte)
+        return
     mdec, msca = import_reference()
     if sys.argv[1:] == ["regulator"]:
         gen_regulator(msca)
@@ -325,6 +656,9 @@ def main():
     gen_decoder(mdec)
     gen_style(msca)
     gen_regulator(msca)
+    mte = import_reference_text_encoder()
+    gen_text(mte)
+    gen_text_processor(mte)
 
 
 if __name__ == "__main__":

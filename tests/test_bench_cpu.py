@@ -25,6 +25,12 @@ def _run(n):
 def test_bench_launches_two_ranks():
     rec = _run(2)
     assert rec["n_gpus"] == 2 and rec["allreduce_ok"] and rec["steps"] == 3 and rec["warmup"] == 1
+    # the N > 1 line explains itself: backward time, the all-reduce time left
+    # exposed after it, and the bucket layout (bench.py dp_breakdown)
+    dp = rec["dp"]
+    assert dp["backward_ms"] >= 0 and dp["allreduce_exposed_ms"] >= 0 and dp["steps"] == 3
+    assert dp["buckets"] >= 2 and len(dp["bucket_MB"]) == dp["buckets"] and dp["grad_MB"] > 0
+    assert dp["comm_dtype"] == "float32" and dp["reduce_op"] in ("avg", "sum+scale")
 
 
 def test_bench_single_rank_needs_no_launcher():

@@ -1,10 +1,16 @@
-"""GPU parity of the text encoder / duration predictor
-against the oracle's float64 restatement of FastSpeech2's FFTBlock /
-VariancePredictor (oracle.text_encoder_ref, duration_predictor_ref).
-PARITY UNPINNED: the reference builds these from ming024/FastSpeech2, which
-it neither vendors nor pins and which is absent here, so no reference output
-exists to pin the restatement to.  fp32, 1e-4 relative;
-dropout off (eval) for values, train-mode gradients with dropout 0."""
+"""GPU parity of the text encoder / duration predictor.
+
+* Against the REFERENCE text_encoder.py itself (tests/golden/text.npz, made
+  by tests/golden/make_golden.py importing /root/reference/text_encoder.py
+  behind a lib.FastSpeech2 shim): TextEncoder.forward in train mode and in
+  the eval branch for L > max_seq_len, every parameter gradient, a
+  zero-length row; DurationPredictor forward + compute_loss and gradients.
+  fp32 HIP path vs the float64 reference, per tensor max|err| <= 1e-4 *
+  max|ref| (the north star's fp32 tolerance is 1e-3).  The FastSpeech2
+  internals the shim restates (FFTBlock, VariancePredictor, the sinusoid
+  table) are third-party, unvendored and unpinned upstream: that restatement
+  is parity unpinned; the reference's own code around it is pinned.
+* Against the oracle's float64 restatement at a second, wider config."""
 import numpy as np
 import pytest
 import torch
@@ -97,3 +103,94 @@ def test_duration_predictor_and_loss_vs_oracle():
     close(xg.grad, xr.grad, rtol=1e-4, name="dx")
     for k, v in dp.named_parameters():
         close(v.grad, p[k].grad, rtol=1e-4, name=k)
+
+
+def _load_sd(mod, g, prefix):
+    sd = {k[len(prefix):]: torch.from_numpy(v) for k, v in g.items() if k.startswith(prefix)}
+    mod.load_state_dict(sd)
+
+
+@pytest.mark.parametrize("tag", ["train", "eval"])
+def test_text_encoder_vs_reference_golden(golden, tag):
+    """TextEncoder (text_encoder.py:87-128) on the HIP path against the
+    reference module's own float64 output and gradients: padded rows, the
+    padding id inside a valid span (its embedding row gets no gradient), and
+    (eval) the fresh unzeroed position table for L > max_seq_len (:107-112)."""
+    import text_encoder as te
+    g = golden("text.npz")
+    m = te.TextEncoder(40, d_model=64, n_layers=2, n_head=2, d_k=32, d_v=32, d_inner=128, kernel_size=(9, 1),
+                       dropout=0.0, max_seq_len=48, padding_idx=0)
+    _load_sd(m, g, "enc/sd/")
+    m = m.to(DEV).train(tag == "train")
+    ids = torch.from_numpy(g[f"{tag}/ids"]).to(DEV)
+    mask = torch.from_numpy(g[f"{tag}/mask"]).to(DEV)
+    out = m(ids, mask=mask)
+    close(out, torch.from_numpy(g[f"{tag}/out"]).double(), rtol=1e-4, name=f"{tag}/out")
+    (out * torch.from_numpy(g[f"{tag}/w"]).to(DEV)).sum().backward()
+    names = [k[len(f"{tag}/grad/"):] for k in g if k.startswith(f"{tag}/grad/")]
+    params = dict(m.named_parameters())
+    assert set(names) == {k for k, v in params.items() if v.requires_grad}
+    for k in names:
+        ref = torch.from_numpy(g[f"{tag}/grad/{k}"]).double()
+        if ref.abs().max() < 1e-9:
+            # the key bias: softmax is shift-invariant per query row (exact 0)
+            assert params[k].grad.abs().max().item() < 1e-5, k
+            continue
+        close(params[k].grad, ref, rtol=1e-4, name=k)
+    assert torch.count_nonzero(m.phoneme_emb.weight.grad[0]) == 0
+
+
+def test_text_encoder_zero_length_row_vs_reference_golden(golden):
+    """A zero-length row: every key padded, the attention row is NaN and the
+    reference's masked_fill zeroes it (the HIP path's select does the same);
+    the other rows match the reference."""
+    import text_encoder as te
+    g = golden("text.npz")
+    m = te.TextEncoder(40, d_model=64, n_layers=2, n_head=2, d_k=32, d_v=32, d_inner=128, dropout=0.0,
+                       max_seq_len=48)
+    _load_sd(m, g, "enc/sd/")
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        out = m(torch.from_numpy(g["empty/ids"]).to(DEV), mask=torch.from_numpy(g["empty/mask"]).to(DEV))
+    assert torch.isfinite(out).all() and not out[1].any()
+    close(out, torch.from_numpy(g["empty/out"]).double(), rtol=1e-4, name="empty/out")
+
+
+def test_duration_predictor_vs_reference_golden(golden):
+    """DurationPredictor forward, compute_loss (masked; a zero duration inside
+    a valid span) and the unmasked mean, and the input / parameter gradients
+    of the masked loss, against the reference module (text_encoder.py:131-209)."""
+    import text_encoder as te
+    g = golden("text.npz")
+    dp = te.DurationPredictor(d_model=64, filter_size=128, kernel_size=3, dropout=0.0)
+    _load_sd(dp, g, "dur/sd/")
+    dp = dp.to(DEV).train()
+    x = torch.from_numpy(g["dur/x"]).to(DEV).requires_grad_(True)
+    mask = torch.from_numpy(g["dur/mask"]).to(DEV)
+    target = torch.from_numpy(g["dur/target"]).to(DEV)
+    pred = dp(x, mask=mask)
+    close(pred, torch.from_numpy(g["dur/pred"]).double(), rtol=1e-4, name="pred")
+    loss = dp.compute_loss(pred, target, mask=mask)
+    close(loss.reshape(1), torch.from_numpy(g["dur/loss"]).double().reshape(1), rtol=1e-4, name="loss")
+    loss.backward()
+    close(x.grad, torch.from_numpy(g["dur/dx"]).double(), rtol=1e-4, name="dx")
+    for k, v in dp.named_parameters():
+        close(v.grad, torch.from_numpy(g[f"dur/grad/{k}"]).double(), rtol=1e-4, name=k)
+    with torch.no_grad():
+        nm = dp.compute_loss(dp(x.detach(), mask=None), target.clamp(min=1.0))
+    close(nm.reshape(1), torch.from_numpy(g["dur/loss_nomask"]).double().reshape(1), rtol=1e-4, name="loss_nomask")
+
+
+def test_text_encoder_int32_ids_backward():
+    """int32 phoneme ids (F.embedding accepts them) run forward and backward
+    and give the int64 ids' gradients."""
+    import text_encoder as te
+    torch.manual_seed(0)
+    m = te.TextEncoder(40, d_model=64, n_layers=1, n_head=2, d_k=32, d_v=32, d_inner=128, dropout=0.0).to(DEV)
+    ids, mask = _batch(2, 20, 40, 9)
+    grads = []
+    for dt in (torch.int64, torch.int32):
+        m.zero_grad(set_to_none=True)
+        m(ids.to(DEV, dt), mask=mask.to(DEV)).square().sum().backward()
+        grads.append(m.phoneme_emb.weight.grad.clone())
+    assert torch.equal(grads[0], grads[1])

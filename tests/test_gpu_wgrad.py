@@ -135,6 +135,74 @@ def test_listener_once_per_parameter():
         assert p.grad is not None and torch.isfinite(p.grad).all()
 
 
+def test_listener_sees_final_gradients_with_mid_backward_flushes(monkeypatch):
+    """GROUP_TILES = 1: every submit flushes at once, inside the parameter's
+    own backward.  Each parameter is announced exactly once, and the gradient
+    a listener sees at announcement is the final one; the gradients equal the
+    immediate path's."""
+    from mtts import wgrad
+    monkeypatch.setattr(wgrad, "GROUP_TILES", 1)
+    m = _model()
+    batch = _batch()
+    m.zero_grad(set_to_none=True)
+    _loss(m, *batch).backward()
+    imm = _grads(m)
+    seen = {}
+
+    def fn(p):
+        assert id(p) not in seen, "announced twice"
+        seen[id(p)] = p.grad.detach().clone()
+    wgrad.add_listener(fn)
+    try:
+        m.zero_grad(set_to_none=True)
+        with wgrad.deferred():
+            _loss(m, *batch).backward()
+    finally:
+        wgrad.remove_listener(fn)
+    assert len(seen) == L_ * 8
+    for p in m.parameters():
+        if id(p) in seen:
+            assert torch.equal(seen[id(p)], p.grad)
+    _check(_grads(m), imm)
+
+
+def test_row_sliced_parameter_announced_after_all_slices():
+    """CrossAttention with key is not value runs three row-sliced
+    in-projections (q, k, v rows of in_proj_weight, three separate submits):
+    in_proj_weight is announced once, after the last slice, with its final
+    gradient (mid-backward flushes between the slices must not announce it)."""
+    from mtts import wgrad
+    from mtts.attention import CrossAttention
+    torch.manual_seed(0)
+    att = CrossAttention(D, H).cuda()
+    g = torch.Generator().manual_seed(1)
+    # token counts multiples of 64: every slice takes the deferred TN route
+    q = torch.randn(B, 320, D, generator=g).cuda().bfloat16()
+    k = torch.randn(B, 256, D, generator=g).cuda().bfloat16()
+    v = torch.randn(B, 256, D, generator=g).cuda().bfloat16()
+    w = torch.randn(B, 320, D, generator=g).cuda()
+    att.zero_grad(set_to_none=True)
+    (att(q, k, v)[0].float() * w).sum().backward()
+    imm = {n: p.grad.clone() for n, p in att.named_parameters()}
+    seen = {}
+
+    def fn(p):
+        assert id(p) not in seen, "announced twice"
+        seen[id(p)] = p.grad.detach().clone()
+    wgrad.add_listener(fn)
+    try:
+        att.zero_grad(set_to_none=True)
+        with wgrad.deferred():
+            (att(q, k, v)[0].float() * w).sum().backward()
+    finally:
+        wgrad.remove_listener(fn)
+    assert id(att.in_proj_weight) in seen
+    for n, p in att.named_parameters():
+        if id(p) in seen:
+            assert torch.equal(seen[id(p)], p.grad), n
+    _check({n: p.grad for n, p in att.named_parameters()}, imm)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -161,7 +229,10 @@ def _worker(rank, port, q):
     tok, text, z, mask = _batch(2 * B)
     sl = slice(rank * B, (rank + 1) * B)
     out = []
-    for defer in (False, True):
+    for defer, group_tiles in ((False, 192), (True, 192), (True, 1)):
+        # group_tiles 1: every submit flushes inside its parameter's own
+        # backward (the listener and autograd's hook both see the parameter)
+        wgrad.GROUP_TILES = group_tiles
         dp.zero_grad()
         with wgrad.deferred(defer):
             _loss(m, tok[sl], text[sl], z[sl], mask[sl]).backward()
@@ -175,7 +246,10 @@ def _worker(rank, port, q):
 
 def test_deferred_world2_dp_matches_single_process():
     """Two gloo ranks on cuda:0: the deferred gradients land in the bucket
-    views and the listener launches the buckets.  The averaged gradients equal
+    views and the listener launches the buckets -- also with every submit
+    flushed inside its parameter's own backward (GROUP_TILES 1), where the
+    listener and autograd's post-accumulate hook both see the parameter and
+    the bucket must count it once.  The averaged gradients equal
     the same ranks' immediate-path (split-K) ones to 1e-4, and one process's
     gradient of the mean of the two shards' losses to 2e-2 (bf16 activations:
     per-shard and joint graphs round the activation gradients differently,
@@ -196,8 +270,10 @@ def test_deferred_world2_dp_matches_single_process():
     sum(_loss(m, tok[r * B:(r + 1) * B], text[r * B:(r + 1) * B], z[r * B:(r + 1) * B], mask[r * B:(r + 1) * B])
         for r in range(2)).div(2).backward()
     ref = {n: g.cpu() for n, g in _grads(m).items()}
-    for rank, (imm, dfr) in res:
+    for rank, (imm, dfr, dfr_mid) in res:
         imm = {n: torch.from_numpy(g) for n, g in imm.items()}
         dfr = {n: torch.from_numpy(g) for n, g in dfr.items()}
+        dfr_mid = {n: torch.from_numpy(g) for n, g in dfr_mid.items()}
         _check(dfr, imm)
+        _check(dfr_mid, imm)
         _check(dfr, ref, tol=2e-2)
