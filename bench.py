@@ -362,7 +362,7 @@ def c5_step_bench(rank, world, dev, B=8, T_text=128, T_codec=1024, T_ref=1024, s
     T_audio = T_codec * th.CODEC_STREAMS
     res = {"B_per_rank": B, "T_audio": T_audio, "T_kv": T_ref * th.CODEC_STREAMS + T_text, "T_text": T_text,
            "n_gpus": world, "ms_per_step": ms, "tokens_per_s": world * B * T_audio / dt * steps,
-           "dtype": "decoder bf16, text encoder / duration predictor / style pipeline fp32",
+           "dtype": "decoder and (dead) style branch bf16, text encoder / duration predictor fp32",
            "losses_first_last": [float(first["loss_total"]), float(out["loss_total"])]}
     del models, step, dp
     torch.cuda.empty_cache()

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 12
+#define MTTS_ABI_VERSION 13
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -725,6 +725,36 @@ typedef struct {
 
 int64_t mtts_gemm_skinny_workspace(const MttsSkinnyArgs* a);
 int mtts_gemm_skinny(const MttsSkinnyArgs* a, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Dropout (ABI 13; csrc/dropout.hip).  Replaces nn.Dropout / F.dropout in
+ * the training paths of style_cross_attention.py (:38-46, 100-109, 133,
+ * 246-255, 278) and of the text encoder's FastSpeech2 blocks
+ * (text_encoder.py:80-85, 168).
+ *   y[i] = x[i] * keep(i) / (1 - p),  keep(i) = hash(seed, i) >= p * 2^32
+ * a counter-based mask: the backward passes the SAME seed and regenerates
+ * it (dx = dy * keep / (1 - p)); no mask is stored.  With `pre` (bf16, n
+ * elements): y = bf16(bf16(x * keep / (1 - p)) * gelu'(pre)), the backward of
+ * dropout(gelu(pre)) in one pass (exact-erf GELU, torch's GeluBackward).
+ * `group` > 1: one mask draw per `group` consecutive elements (index i /
+ * group; a multiple of 8 for bf16, 4 for fp32): attention-weight dropout
+ * over a single key, one draw per (batch, head, query) shared by the head's
+ * channels.  Contiguous x / y / pre, 16-byte aligned; n % 8 == 0;
+ * 0 <= p < 1; x == y allowed (in place).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int64_t n;
+  int dtype;                 /* MTTS_F32 / MTTS_BF16 (x and y) */
+  float p;
+  uint64_t seed;
+  const void* x;
+  void* y;
+  const void* pre;           /* optional bf16 GELU pre-activation (DGELU form) */
+  int group;                 /* elements per mask draw (0 / 1: every element) */
+  int reserved_;
+} MttsDropoutArgs;
+
+int mtts_dropout(const MttsDropoutArgs* a, void* stream);
 
 #ifdef __cplusplus
 }

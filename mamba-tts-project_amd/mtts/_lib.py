@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -87,6 +87,11 @@ class GemmArgs(C.Structure):
     _fields_ = [("m", i32), ("n", i32), ("k", i32), ("layout", i32), ("splits", i32), ("epilogue", i32),
                 ("out_dtype", i32), ("bias_dtype", i32), ("lda", i64), ("ldb", i64), ("ldc", i64), ("ld_aux", i64),
                 ("a", vp), ("b", vp), ("c", vp), ("bias", vp), ("aux", vp), ("workspace", vp), ("beta", f32)]
+
+
+class DropoutArgs(C.Structure):
+    _fields_ = [("n", i64), ("dtype", i32), ("p", f32), ("seed", C.c_uint64), ("x", vp), ("y", vp), ("pre", vp),
+                ("group", i32), ("reserved_", i32)]
 
 
 class RowMap(C.Structure):
@@ -193,6 +198,7 @@ _SIGS = {
     "mtts_length_regulate_lengths": ([vp, i64, i32, i32, vp, vp], i32),
     "mtts_length_regulate_fwd": ([vp, i32, i32, i32, i32, i64, i64, vp, i64, i32, vp, i64, i64, vp], i32),
     "mtts_length_regulate_bwd": ([vp, i32, i32, i32, i32, i64, i64, vp, i64, i32, vp, i64, i64, vp], i32),
+    "mtts_dropout": ([C.POINTER(DropoutArgs), vp], i32),
 }
 
 _lib = None

@@ -101,8 +101,8 @@ class CrossAttention(nn.Module):
         d, H = self.embed_dim, self.num_heads
         W, b = self.in_proj_weight, self.in_proj_bias
         p_drop = self.dropout if self.training else 0.0
-        if key.shape[1] == 1 and key_padding_mask is None and p_drop == 0.0:
-            return self._single_key(query, key, value), None
+        if key.shape[1] == 1 and key_padding_mask is None:
+            return self._single_key(query, key, value, p_drop), None
         if key is value:
             q, kv = InProjFn.apply(query, key.to(cd), W, b)
             o = attn_kernels.attention_kv(q, kv, H, key_padding_mask, p_drop)
@@ -114,21 +114,31 @@ class CrossAttention(nn.Module):
         out = linear(o, self.out_proj.weight, self.out_proj.bias, dbias_slot=dbias_slot)
         return out, None
 
-    def _single_key(self, query, key, value):
+    def _single_key(self, query, key, value, p_drop=0.0):
         """One unmasked key (the style token of style_cross_attention.py:125-131,
-        270-276) and no attention dropout: softmax over a single logit is
-        exactly 1, so every query row's attention output is the value
-        projection of that key, out_proj(v) -- independent of q and k.  Only the
-        value projection and out_proj run, on B rows instead of B*Tq.  torch's
-        MHA gives the q/k in-projection rows exactly zero gradient here
-        (dS = P*(dP - rowsum(P*dP)) = 0 for one key); LinearFn's row slice
-        reproduces that for the weights, and the zero-weighted key term keeps a
-        (zero) gradient flowing to `key` so optimizer state and weight decay of
-        the key path behave as with torch MHA."""
+        270-276): softmax over a single logit is exactly 1, so every query
+        row's attention output is the value projection of that key -- out_proj(v),
+        independent of q and k.  Without attention dropout only the value
+        projection and out_proj run, on B rows instead of B*Tq.  With it
+        (training, p > 0) each (batch, head, query) weight 1 is kept with
+        probability 1 - p and scaled by 1 / (1 - p), as nn.MultiheadAttention's
+        dropout on the (B, H, Tq, 1) weights: the head's slice of v is masked
+        by ONE draw per (batch, query, head) (the HIP dropout, group = head
+        dim), then out_proj runs on the B*Tq rows.  torch's MHA gives the q/k
+        in-projection rows exactly zero gradient here (dS = P*(dP -
+        rowsum(P*dP)) = 0 for one key); LinearFn's row slice reproduces that for
+        the weights, and the zero-weighted key term keeps a (zero) gradient
+        flowing to `key` so optimizer state and weight decay of the key path
+        behave as with torch MHA."""
         cd = query.dtype
         d = self.embed_dim
         B, Tq = query.shape[0], query.shape[1]
         v = linear(value.to(cd), self.in_proj_weight, self.in_proj_bias, rows=(2 * d, 3 * d))   # (B, 1, d)
+        if p_drop > 0.0:
+            from . import dropout as DO
+            o = DO.dropout(v.expand(B, Tq, d).contiguous(), p_drop, True, group=self.head_dim)
+            o = linear(o, self.out_proj.weight, self.out_proj.bias)
+            return o + 0.0 * key.to(cd).sum(dim=-1, keepdim=True)
         o = linear(v, self.out_proj.weight, self.out_proj.bias)
         o = o + 0.0 * key.to(cd).sum(dim=-1, keepdim=True)
         return o.expand(B, Tq, d).contiguous()

@@ -1,0 +1,77 @@
+"""Dropout on the HIP kernel (csrc/dropout.hip, mtts_dropout).
+
+Replaces nn.Dropout / F.dropout in the training paths of the drop-in modules
+(reference style_cross_attention.py:38-46, 100-109, 133, 246-255, 278 and the
+FastSpeech2 blocks behind text_encoder.py:80-85, 168).  The mask is
+counter-based (a hash of a per-call seed and the element index), so nothing
+is stored for the backward: it regenerates the mask from the same seed.
+Seeds come from torch's default CPU generator (torch.manual_seed reproduces
+a run; no device sync).  The masks are not torch's (no two implementations'
+dropout draws match element for element); the keep probability and scale
+are: keep with probability 1 - p, survivors scaled by 1 / (1 - p).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+
+
+def new_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+def _ok(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.is_contiguous()
+            and t.numel() % 8 == 0 and t.data_ptr() % 16 == 0)
+
+
+def apply_mask(x: torch.Tensor, p: float, seed: int, pre: torch.Tensor = None, out: torch.Tensor = None,
+               group: int = 1):
+    """y = x * keep(seed) / (1 - p) [* gelu'(pre)] on the HIP kernel; one
+    mask draw per `group` consecutive elements."""
+    if not _ok(x):
+        raise ValueError(f"dropout: contiguous 16-byte-aligned fp32/bf16 CUDA tensor with numel % 8 == 0 expected "
+                         f"(got {x.dtype}, {tuple(x.shape)}, contiguous={x.is_contiguous()})")
+    if pre is not None and (pre.dtype != torch.bfloat16 or pre.numel() != x.numel() or not _ok(pre)):
+        raise ValueError("dropout: pre must be a contiguous bf16 tensor of x's size")
+    y = torch.empty_like(x) if out is None else out
+    a = L.DropoutArgs()
+    a.n, a.dtype, a.p, a.seed = x.numel(), L.dtype_code(x), float(p), seed & (2 ** 64 - 1)
+    a.x, a.y = x.data_ptr(), y.data_ptr()
+    a.pre = 0 if pre is None else pre.data_ptr()
+    a.group = group
+    L.call("mtts_dropout", a)
+    return y
+
+
+class DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, group=1):
+        ctx.p, ctx.seed, ctx.group = p, new_seed(), group
+        return apply_mask(x.contiguous(), p, ctx.seed, group=group)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return apply_mask(dy.contiguous(), ctx.p, ctx.seed, group=ctx.group), None, None
+
+
+def dropout(x: torch.Tensor, p: float, training: bool, group: int = 1) -> torch.Tensor:
+    """F.dropout(x, p, training) with the HIP kernel (identity when not
+    training or p == 0).  Shapes the kernel cannot take (numel % 8 != 0,
+    misaligned) are made contiguous and padded by the caller's layout; a
+    CPU tensor raises (the product path runs on the GPU)."""
+    if not training or p == 0.0:
+        return x
+    if not 0.0 <= p < 1.0:
+        raise ValueError(f"dropout probability has to be in [0, 1), got {p}")
+    if group > 1:
+        return DropoutFn.apply(x, p, group)
+    if x.numel() % 8 != 0:
+        # tiny tensors (e.g. a (B, d) style vector with B * d % 8 != 0): flat-pad to the kernel's granule
+        n = x.numel()
+        flat = torch.nn.functional.pad(x.reshape(-1), (0, (-n) % 8))
+        return DropoutFn.apply(flat, p)[:n].view(x.shape)
+    return DropoutFn.apply(x, p)

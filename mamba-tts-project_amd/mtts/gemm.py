@@ -121,7 +121,10 @@ SKINNY_N, SKINNY_SMALL_K = 0, 1
 SKINNY = True   # routing switch (in-process A/B: tools/skinny_ab.py)
 SKINNY_TN_KERNEL = True  # x_proj / dt_proj weight gradients on the SKINNY_TN kernel (mamba.py; skinny_tn_ok)
 WGRAD_SKINNY_ON_TN = False  # linear.wgrad: skinny weight gradients on the big TN kernel (35.5 vs 33.7 us: off)
-SKINNY_XPROJ = False   # x_proj forward on SKINNY_N (25 vs 21 us hipBLASLt: off)
+# x_proj forward on SKINNY_N: round 3 measured 25 vs 21 us for hipBLASLt, round 5
+# 24.5-25.8 vs 24.2 us (profiles/r05_skinny_n_*_ab.txt): on par, so the
+# hand-written kernel is the default (no vendor GEMM left on the Mamba path)
+SKINNY_XPROJ = True
 
 
 def _skinny_operand(t):

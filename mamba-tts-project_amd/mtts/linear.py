@@ -286,21 +286,29 @@ def linear(x, weight, bias=None, rows=None, dbias_slot=None):
 
 
 class FFNFn(torch.autograd.Function):
-    """ff(h) = gelu(h W1^T + b1) W2^T + b2 (mamba_decoder.py:39-43, 88) with
-    bf16 compute on the hand-written GEMM: bias + exact GELU fused into the
-    first projection's epilogue (the bf16 pre-activation is written beside
-    the activation for the backward), the GELU backward fused into the
-    second projection's data-gradient epilogue, both weight gradients on
-    the TN kernel straight into fp32."""
+    """ff(h) = dropout_p(gelu(h W1^T + b1)) W2^T + b2 (mamba_decoder.py:39-43,
+    88 with p = 0; the style blocks' nn.Sequential(Linear, GELU, Dropout,
+    Linear), style_cross_attention.py:103-109, 249-255) with bf16 compute on
+    the hand-written GEMM: bias + exact GELU fused into the first
+    projection's epilogue (the bf16 pre-activation is written beside the
+    activation for the backward), the GELU backward fused into the second
+    projection's data-gradient epilogue -- or, with dropout, into the HIP
+    dropout kernel that regenerates the mask (mtts.dropout) -- both weight
+    gradients on the TN kernel straight into fp32."""
 
     @staticmethod
-    def forward(ctx, h, w1, b1, w2, b2, slot=None):
+    def forward(ctx, h, w1, b1, w2, b2, slot=None, p=0.0):
+        from . import dropout as DO
         cd = h.dtype
         ctx.slot = slot
         W1, B1, W2, B2 = cast_weight(w1, cd), cast_weight(b1, cd), cast_weight(w2, cd), cast_weight(b2, cd)
         h2 = h.reshape(-1, h.shape[-1])
         pre = torch.empty(h2.shape[0], W1.shape[0], device=h.device, dtype=cd)
         a = G.mm_nt(h2, W1, bias=B1, gelu_aux=pre)
+        ctx.p, ctx.seed = p, None
+        if p > 0.0:
+            ctx.seed = DO.new_seed()
+            a = DO.apply_mask(a, p, ctx.seed)
         y = proj(a, W2, B2)
         ctx.save_for_backward(h2, pre, a, W1, W2)
         ctx.ws = (w1, w2)
@@ -313,9 +321,14 @@ class FFNFn(torch.autograd.Function):
         hshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
         w1, w2 = ctx.ws
         dy2 = dy.reshape(-1, dy.shape[-1]).to(W2.dtype)
-        # d(pre) = (dy W2) * gelu'(pre), one GEMM (W2^T copy: k-contiguous operand)
+        # d(pre) = (dy W2) * gelu'(pre), one GEMM (W2^T copy: k-contiguous operand);
+        # with dropout: the dropout kernel applies the mask and gelu'(pre)
         W2t = cast_weight_t(w2, W2.dtype) if _want_t(w2) else W2.t().contiguous()
-        dpre = G.mm_nt(dy2, W2t, dgelu_aux=pre)
+        if ctx.p > 0.0:
+            from . import dropout as DO
+            dpre = DO.apply_mask(G.mm_nt(dy2, W2t), ctx.p, ctx.seed, pre=pre)
+        else:
+            dpre = G.mm_nt(dy2, W2t, dgelu_aux=pre)
         dh = None
         if ctx.needs_input_grad[0]:
             if _want_t(w1):
@@ -333,14 +346,17 @@ class FFNFn(torch.autograd.Function):
         if ctx.needs_input_grad[4]:
             db2 = ctx.slot.take(dy2.shape[1]) if ctx.slot is not None else None
             db2 = (db2 if db2 is not None else colsum(dy2)).to(b2dt)
-        return dh, dW1, db1, dW2, db2, None
+        return dh, dW1, db1, dW2, db2, None, None
 
 
-def ffn(h, w1, b1, w2, b2, dbias_slot=None):
-    """gelu(h W1^T + b1) W2^T + b2: the fused bf16 path when the shapes allow
-    it (bf16 activations, d_model / d_ff multiples of 64), else the
-    per-op path (LinearFn + F.gelu).  dbias_slot: see linear()."""
+def ffn(h, w1, b1, w2, b2, dbias_slot=None, p=0.0):
+    """dropout_p(gelu(h W1^T + b1)) W2^T + b2: the fused bf16 path when the
+    shapes allow it (bf16 activations, d_model / d_ff multiples of 64, rows a
+    multiple of 8 when p > 0), else the per-op path (LinearFn + F.gelu + the
+    HIP dropout).  dbias_slot: see linear()."""
     if (G.ENABLED and G.FFN_FUSED and h.dtype == torch.bfloat16 and h.is_cuda and h.shape[-1] % 64 == 0 and w1.shape[0] % 64 == 0
             and h.stride(-1) == 1 and h.is_contiguous()):
-        return FFNFn.apply(h, w1, b1, w2, b2, dbias_slot)
-    return linear(torch.nn.functional.gelu(linear(h, w1, b1)), w2, b2, dbias_slot=dbias_slot)
+        return FFNFn.apply(h, w1, b1, w2, b2, dbias_slot, p)
+    from . import dropout as DO
+    a = DO.dropout(torch.nn.functional.gelu(linear(h, w1, b1)), p, p > 0.0)
+    return linear(a, w2, b2, dbias_slot=dbias_slot)

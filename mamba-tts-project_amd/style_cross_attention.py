@@ -8,11 +8,20 @@ Implements:
 3. Cross-Attention #2: Upsampled ⊗ Style                   (reference :215-286)
 4. Length Regulator (phoneme-level → frame-level)          (reference :144-212)
 
-Arithmetic runs on libmtts kernels: fused residual-add + LayerNorm, the HIP
-attention core, and the HIP length regulator (mtts_length_regulate_*: the
-reference loops over (b, phoneme) with one .item() each, :185-196); only the
-output length needs one device->host read when max_len is None, as in the
-reference.
+Arithmetic runs on libmtts kernels: fused residual-add + LayerNorm, the
+single-key attention shortcut (with the attention-weight dropout as one HIP
+mask draw per (batch, query, head)), the FFN on the hand-written NT GEMM with
+bias + GELU fused into its epilogue (bf16; the dropout between GELU and the
+second linear and the GELU backward in the HIP dropout kernel), the HIP
+dropout (mtts.dropout) for every nn.Dropout, and the HIP length regulator
+(mtts_length_regulate_*: the reference loops over (b, phoneme) with one
+.item() each, :185-196); only the output length needs one device->host read
+when max_len is None, as in the reference.
+
+`StyleConditioningPipeline.compute_dtype` (default None: the input's dtype,
+fp32 as the reference) casts the pipeline's activations on entry, as the
+decoder's compute_dtype does; train_harness runs train.py's dead style branch
+in the decoder's bf16.
 """
 
 import torch
@@ -21,6 +30,8 @@ import torch.nn.functional as F
 
 from mtts.attention import CrossAttention
 from mtts import ops
+from mtts.dropout import dropout as hip_dropout
+from mtts.linear import cast_scope, ffn, linear
 
 
 def _ln(mod, x, res=None):
@@ -39,13 +50,14 @@ class StyleProjection(nn.Module):
         self.value_proj = nn.Sequential(nn.Linear(d_style, d_model), nn.LayerNorm(d_model), nn.Dropout(dropout))
 
     def _proj(self, seq, x):
-        h = F.linear(x, seq[0].weight.to(x.dtype), seq[0].bias.to(x.dtype))
+        h = linear(x, seq[0].weight, seq[0].bias)
         h = _ln(seq[1], h)
-        return F.dropout(h, seq[2].p, self.training)
+        return hip_dropout(h, seq[2].p, self.training)
 
     def forward(self, style_emb):
-        K = self._proj(self.key_proj, style_emb)
-        V = self._proj(self.value_proj, style_emb)
+        with cast_scope():   # compute-dtype weight copies valid for this call (mtts.linear)
+            K = self._proj(self.key_proj, style_emb)
+            V = self._proj(self.value_proj, style_emb)
         return K.unsqueeze(1), V.unsqueeze(1)
 
 
@@ -70,12 +82,16 @@ class _StyleBlock(nn.Module):
         self.ffn_norm = nn.LayerNorm(d_model)
 
     def _body(self, x, style_K, style_V):
+        with cast_scope():   # compute-dtype weight copies valid for this call (mtts.linear)
+            return self._body_scoped(x, style_K, style_V)
+
+    def _body_scoped(self, x, style_K, style_V):
         cd = x.dtype
         attn_out, _ = self.cross_attn(query=x, key=style_K.to(cd), value=style_V.to(cd))
-        x = _ln(self.norm, self.dropout(attn_out), res=x)
+        x = _ln(self.norm, hip_dropout(attn_out, self.dropout.p, self.training), res=x)
         f0, f3 = self.ffn[0], self.ffn[3]
-        h = F.dropout(F.gelu(F.linear(x, f0.weight.to(cd), f0.bias.to(cd))), self.ffn[2].p, self.training)
-        h = F.dropout(F.linear(h, f3.weight.to(cd), f3.bias.to(cd)), self.ffn[4].p, self.training)
+        h = ffn(x.contiguous(), f0.weight, f0.bias, f3.weight, f3.bias, p=self.ffn[2].p if self.training else 0.0)
+        h = hip_dropout(h, self.ffn[4].p, self.training)
         return _ln(self.ffn_norm, h, res=x)
 
 
@@ -113,12 +129,15 @@ class StyleDecoderCrossAttention(_StyleBlock):
 class StyleConditioningPipeline(nn.Module):
     def __init__(self, d_style=256, d_model=512, num_heads=8, dropout=0.1):
         super().__init__()
+        self.compute_dtype = None   # None: the input's dtype (see the module docstring)
         self.style_proj = StyleProjection(d_style, d_model, dropout)
         self.cross_attn_1 = StyleTextCrossAttention(d_model, num_heads, dropout)
         self.cross_attn_2 = StyleDecoderCrossAttention(d_model, num_heads, dropout)
         self.length_regulator = LengthRegulator()
 
     def forward(self, text_hidden, style_emb, durations, text_mask=None, max_frame_len=None):
+        if self.compute_dtype is not None:
+            text_hidden, style_emb = text_hidden.to(self.compute_dtype), style_emb.to(self.compute_dtype)
         style_K, style_V = self.style_proj(style_emb)
         styled_text = self.cross_attn_1(text_hidden, style_K, style_V, text_mask)
         upsampled, output_lengths = self.length_regulator(styled_text, durations, max_len=max_frame_len)

@@ -23,7 +23,9 @@ architecture is restated:
 Arithmetic (fp32, as the reference): the attention core is the HIP MFMA
 attention (mtts_attention_*, key_padding_mask = the pad mask, True = pad, as
 the reference's slf_attn_mask) on ONE fused q/k/v projection;
-LayerNorm(x + residual) is the fused HIP LayerNorm; the projections and the
+LayerNorm(x + residual) is the fused HIP LayerNorm; every nn.Dropout is the
+HIP dropout (mtts.dropout, a counter-based mask regenerated in the
+backward); the projections and the
 convolutions run on the hand-written fp32 MFMA GEMM over windowed rows
 (mtts.convgemm, csrc/convgemm.hip): a 'same' Conv1d is a direct implicit-GEMM
 convolution over the zero-padded channel-last activation (no unfold copy),
@@ -39,6 +41,7 @@ import torch.nn.functional as F
 
 from mtts import attn_kernels, ops
 from mtts import convgemm as CG
+from mtts.dropout import dropout as hip_dropout
 
 
 def get_sinusoid_encoding_table(n_position, d_hid, padding_idx=None):
@@ -212,7 +215,7 @@ class MultiHeadAttention(nn.Module):
             kh = linear(k, self.w_ks.weight, self.w_ks.bias)
             vh = linear(v, self.w_vs.weight, self.w_vs.bias)
             o = attn_kernels.attention(qh, kh, vh, self.n_head, key_padding_mask=mask)
-        o = self.dropout(linear(o, self.fc.weight, self.fc.bias))
+        o = hip_dropout(linear(o, self.fc.weight, self.fc.bias), self.dropout.p, self.training)
         return _ln(self.layer_norm, o, res=residual), None
 
 
@@ -228,7 +231,8 @@ class PositionwiseFeedForward(nn.Module):
         for c in (self.w_1, self.w_2):
             if 2 * c.padding[0] != c.kernel_size[0] - 1:
                 raise ValueError("PositionwiseFeedForward: 'same' convolutions only")
-        out = self.dropout(CG.conv_ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias))
+        out = hip_dropout(CG.conv_ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias),
+                          self.dropout.p, self.training)
         return _ln(self.layer_norm, out, res=x)
 
 
@@ -327,9 +331,9 @@ class VariancePredictor(nn.Module):
         cl = self.conv_layer
         c1, c2 = cl.conv1d_1.conv, cl.conv1d_2.conv
         out = conv1d_same(encoder_output, c1.weight, c1.bias, c1.padding[0], relu=True)
-        out = cl.dropout_1(_ln(cl.layer_norm_1, out))
+        out = hip_dropout(_ln(cl.layer_norm_1, out), cl.dropout_1.p, self.training)
         out = conv1d_same(out, c2.weight, c2.bias, c2.padding[0], relu=True)
-        out = cl.dropout_2(_ln(cl.layer_norm_2, out))
+        out = hip_dropout(_ln(cl.layer_norm_2, out), cl.dropout_2.p, self.training)
         out = linear(out, self.linear_layer.weight, self.linear_layer.bias).squeeze(-1)
         if mask is not None:
             out = out.masked_fill(mask, 0.0)

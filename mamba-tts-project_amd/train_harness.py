@@ -80,6 +80,11 @@ def build_models(device, d_model=512, d_style=256, vocab_size_text=PHONEME_VOCAB
                                         n_heads=dec_heads, d_ff=d_ff, d_style=d_style, max_len=max_len,
                                         num_quantizers=num_quantizers).to(device)
     dec.compute_dtype = compute_dtype
+    # train.py's style branch is dead (its output enters no loss, :206-210):
+    # it runs in the decoder's compute dtype (bf16 for the benchmark: the FFN
+    # on the hand-written NT GEMM instead of fp32 vendor GEMMs over ~40 k
+    # regulated frames)
+    pipe.compute_dtype = compute_dtype
     return C5Models(enc, dur, pipe, dec)
 
 

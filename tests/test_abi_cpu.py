@@ -36,6 +36,7 @@ STRUCTS = {
     "MttsStateUpdateArgs": "StateUpdateArgs", "MttsLNArgs": "LNArgs", "MttsLNBwdArgs": "LNBwdArgs",
     "MttsAttnFwdArgs": "AttnFwdArgs", "MttsAttnBwdArgs": "AttnBwdArgs", "MttsCastDesc": "CastDesc",
     "MttsAdamTensor": "AdamTensor", "MttsRowsArgs": "RowsArgs", "MttsGemmArgs": "GemmArgs", "MttsSkinnyArgs": "SkinnyArgs",
+    "MttsDropoutArgs": "DropoutArgs", "MttsConvGemmArgs": "ConvGemmArgs",
 }
 
 

@@ -274,6 +274,13 @@ def test_deferred_world2_dp_matches_single_process():
         imm = {n: torch.from_numpy(g) for n, g in imm.items()}
         dfr = {n: torch.from_numpy(g) for n, g in dfr.items()}
         dfr_mid = {n: torch.from_numpy(g) for n, g in dfr_mid.items()}
-        _check(dfr, imm)
-        _check(dfr_mid, imm)
+        # the immediate and the two deferred paths sum the same bf16 products
+        # in a different order (1e-4 of each tensor's scale in one process);
+        # the averaged world-2 gradients of two gloo ranks sharing one card
+        # also move between runs by up to ~2.4e-3 of pos_embed's scale (its
+        # gradient is a batch sum that cancels to ~1e-4 of its terms, so
+        # last-bit differences upstream show; tools/dbg/wdp_race.py: in all
+        # three modes alike, never in the single-process runs)
+        _check(dfr, imm, tol=1e-2)
+        _check(dfr_mid, imm, tol=1e-2)
         _check(dfr, ref, tol=2e-2)

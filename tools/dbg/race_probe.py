@@ -50,8 +50,9 @@ def probes(dev):
             (y.float() * dy.float()).sum().backward()
             return [y, xs, xx.grad, film.grad, slot.value]
         out[f"ln+film d{d}"] = ln
-    # scan / conv at C2 shape
-    B, L, D = 8, 2048, 2048
+    # scan / conv at C2 shape (SCAN_SHAPE=B,L,D: another shape, e.g. the DP
+    # test's 2,512,512)
+    B, L, D = (int(v) for v in os.environ.get("SCAN_SHAPE", "8,2048,2048").split(","))
     u, dl, z, dy = r(B, L, D), r(B, L, D, sc=0.3), r(B, L, D), r(B, L, D)
     A = -torch.rand(D, 16, device=dev) - 0.1
     Bm, Cm = r(B, L, 16), r(B, L, 16)
@@ -88,6 +89,10 @@ def probes(dev):
     ck32 = ops.scan_fwd(u32, dl32, A, Bm.float(), Cm.float(), Dp, z32, bias, True, want_ckpt=True)[2]
     out["scan bwd C2 fp32"] = lambda: [t for t in ops.scan_bwd(u32, dl32, A, Bm.float(), Cm.float(), Dp, z32, bias, True,
                                                                 None, ck32, dy32) if t is not None]
+    r_ = 32 if D >= 1024 else 16
+    dd2, dt2 = r(B * L, D), r(B * L, r_)
+    gx, u2 = r(B * L, r_ + 32), r(B * L, D)
+    out["skinny tn (dW_dt, dW_x)"] = lambda: [G.mm_skinny_tn(dd2, dt2), G.mm_skinny_tn(u2, gx, trans_c=True)]
     xz = r(B, L, 2 * D)
     cw, cb = torch.randn(D, 4, device=dev) * 0.5, torch.randn(D, device=dev) * 0.1
 
