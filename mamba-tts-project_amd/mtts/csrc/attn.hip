@@ -1016,6 +1016,42 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdParams p) {
   }
 }
 
+// 16-byte / 4-byte LDS-DMA through a buffer descriptor (round 6, the long-key
+// backward passes): lane l's bytes land at lds + 16 * l (4 * l) -- M0 holds the
+// wave-uniform LDS base --, the row origin rides in the scalar offset and
+// offsets past the descriptor's range read 0.  Inline asm (invisible to the
+// compiler's wait insertion): every consumer waits by an explicit counted
+// vmcnt + block_sync.  Default cache policy: each slice is re-read by every
+// key group of its (batch, head) from L2.
+typedef int i32x4a __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4a rsrc4a(const void* p, uint32_t bytes) {   // p, bytes wave-uniform
+  const uint64_t q = (uint64_t)(uintptr_t)p;
+  return i32x4a{__builtin_amdgcn_readfirstlane((int)(uint32_t)q), __builtin_amdgcn_readfirstlane((int)((q >> 32) & 0xffff)),
+                __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* lds) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds);
+}
+__device__ __forceinline__ void dma16_lds(const i32x4a& rs, uint32_t voff, int soff, uint32_t lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"
+               ::"v"(voff), "s"(lds), "s"(rs), "s"(soff) : "memory", "m0");
+#endif
+}
+__device__ __forceinline__ void dma4_lds(const i32x4a& rs, uint32_t voff, int soff, uint32_t lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %0, %2, %3 offen lds"
+               ::"v"(voff), "s"(lds), "s"(rs), "s"(soff) : "memory", "m0");
+#endif
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+#endif
+}
+
 // Long key side, bf16, dQ pass (replaces mode 2 for hd 64 / 128): a
 // workgroup owns 128 queries, one 32-query slice per WAVE; Q and dO stay in
 // registers as MFMA B fragments for the whole sweep.  Everything is computed
@@ -1036,9 +1072,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   constexpr int KB = 64;
   constexpr int NQ = HD / 16, ND = HD / 32;
   constexpr int NPF = KB * HD / 8 / 256;   // 16-byte K (and V) chunks per thread per block
-  __shared__ __attribute__((aligned(16))) bf16_t sK[2][KB * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[2][KB * HD];
+  // round 6 (kDqDma, hd 64): K / V blocks by LDS-DMA into a 3-deep ring (block
+  // j + 2 issued while block j computes; per wave two 1 KiB pieces of K and of
+  // V whose per-lane source offsets un-apply the kimg swizzle, wave 0 also the
+  // block's 64 key-mask bytes), one counted vmcnt + barrier per block; this
+  // frees the 16 staging VGPRs of the register-staged form (kept for hd 128,
+  // whose three 32 KiB buffers would not leave room for two workgroups)
+  constexpr bool kDqDma = HD == 64;
+  constexpr int NBUF = kDqDma ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) bf16_t sK[NBUF][KB * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[NBUF][KB * HD];
   __shared__ uint32_t sMask[2][KB / 32];
+  __shared__ __attribute__((aligned(16))) uint32_t sMraw[NBUF][64];   // kDqDma: mask bytes of the block (16 dwords + zeros)
   const MttsAttnBwdArgs& a = p.a;
   const MttsAttnFwdArgs& f = a.f;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1132,18 +1177,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) QA[dt] = f32x16{};
   const int nblk = (f.kv_len + KB - 1) / KB;
-  if (nblk > 0) {
-    fetch(0);
-    put(0);
-  }
-  block_sync();
-  // hd 128: the next block's 32 staging registers do not fit beside Q / dO /
-  // dQ (256 VGPRs); it is loaded after this block's math instead
-  constexpr bool kPrefetch = HD == 64;
-  constexpr int kTileUnroll = kPrefetch ? 2 : 1;
-  for (int j = 0; j < nblk; ++j) {
-    const int buf = j & 1, k0 = j * KB;
-    if constexpr (kPrefetch) fetch(min(k0 + KB, (nblk - 1) * KB));   // in flight under this block's math
+  // the math of one 64-key block from LDS buffer `buf` (key mask: the staged
+  // 32-bit words, or -- kDqDma -- the raw mask bytes)
+  constexpr int kTileUnroll = HD == 64 ? 2 : 1;   // hd 128: no room for two tiles' registers
+  auto block = [&](int buf, int k0) __attribute__((always_inline)) {
 #pragma unroll kTileUnroll
     for (int t = 0; t < KB / 32; ++t) {
       if (k0 + t * 32 >= f.kv_len) break;
@@ -1160,7 +1197,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
         S = mfma_bf16(*(const s16x8*)(kt + oR[s]), Qf[s], S);
         D = mfma_bf16(*(const s16x8*)(vt + oR[s]), Gf[s], D);
       }
-      const uint32_t wm = __builtin_amdgcn_readfirstlane(sMask[buf][t]);
+      uint32_t wm;
+      if constexpr (kDqDma) {
+        const int kl = t * 32 + r;   // lanes r and r + 32 test the same key
+        const uint8_t mbyte = ((const uint8_t*)sMraw[buf])[kl];
+        wm = (uint32_t)__ballot(k0 + kl < f.kv_len && mbyte == 0);
+      } else {
+        wm = __builtin_amdgcn_readfirstlane(sMask[buf][t]);
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float pr = exp2_raw(c * S[i]);
@@ -1176,11 +1220,72 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
           QA[dt] = mfma_bf16(cat(tr_read(ks + oT[0][dt]), tr_read(ks + oT[1][dt])), pb, QA[dt]);
       }
     }
-    if (j + 1 < nblk) {
-      if constexpr (!kPrefetch) fetch(k0 + KB);
-      put(buf ^ 1);
+  };
+  if constexpr (kDqDma) {
+    static_assert(NPF == 2, "kDqDma: two 1 KiB pieces per wave and tensor per block");
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    // LDS slot s = 64 * (4 * i + wave) + lane of piece i: image row s / 8,
+    // physical chunk s % 8 = logical chunk ^ kswz(row)
+    uint32_t vk[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int srow = 8 * (4 * i + wv) + (lane >> 3);
+      const int sch = (lane & 7) ^ kswz<HD>(srow);
+      vk[i] = (uint32_t)((srow * f.k_ls + 8 * sch) * 2);
+    }
+    const uint32_t vm = lane < 16 ? (uint32_t)lane * 4 : 0xFFFFFFF0u;   // 16 dwords = 64 mask bytes
+    const i32x4a rk4 = rsrc4a(kbase, (uint32_t)(((int64_t)(f.kv_len - 1) * f.k_ls + HD) * 2));
+    const i32x4a rv4 = rsrc4a(vbase, (uint32_t)(((int64_t)(f.kv_len - 1) * f.k_ls + HD) * 2));
+    const i32x4a rm4 = rsrc4a(mb ? mb : (const uint8_t*)kbase, mb ? (uint32_t)f.kv_len : 0u);
+    auto sgpr = [](int v) __attribute__((always_inline)) { return __builtin_amdgcn_readfirstlane(v); };
+    auto dma_blk = [&](int k0, int buf) __attribute__((always_inline)) {
+      const int sk = sgpr(k0 * f.k_ls * 2);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        dma16_lds(rk4, vk[i], sk, sgpr((int)lds_addr(sK[buf]) + 1024 * (4 * i + wv)));
+        dma16_lds(rv4, vk[i], sk, sgpr((int)lds_addr(sV[buf]) + 1024 * (4 * i + wv)));
+      }
+      if (wv == 0) dma4_lds(rm4, vm, sgpr(k0), lds_addr(sMraw[buf]));
+    };
+    // VMEM operations one block issues per wave: 5 on wave 0, 4 on the others
+    auto wait_blocks = [&](int later) __attribute__((always_inline)) {
+      if (wv == 0) {
+        if (later >= 1) wait_vmcnt<5>(); else wait_vmcnt<0>();
+      } else {
+        if (later >= 1) wait_vmcnt<4>(); else wait_vmcnt<0>();
+      }
+    };
+    if (nblk > 0) {
+      dma_blk(0, 0);
+      if (nblk > 1) dma_blk(KB, 1);
+      wait_blocks(nblk > 1 ? 1 : 0);
     }
     block_sync();
+    for (int j = 0; j < nblk; ++j) {
+      if (j + 2 < nblk) dma_blk((j + 2) * KB, (j + 2) % 3);   // buffer last read in block j - 1
+      block(j % 3, j * KB);
+      if (j + 1 < nblk) wait_blocks(j + 2 < nblk ? 1 : 0);    // block j + 1 landed
+      block_sync();
+    }
+  } else {
+    if (nblk > 0) {
+      fetch(0);
+      put(0);
+    }
+    block_sync();
+    // hd 128: the next block's 32 staging registers do not fit beside Q / dO /
+    // dQ (256 VGPRs); it is loaded after this block's math instead
+    constexpr bool kPrefetch = HD == 64;
+    for (int j = 0; j < nblk; ++j) {
+      const int buf = j & 1, k0 = j * KB;
+      if constexpr (kPrefetch) fetch(min(k0 + KB, (nblk - 1) * KB));   // in flight under this block's math
+      block(buf, k0);
+      if (j + 1 < nblk) {
+        if constexpr (!kPrefetch) fetch(k0 + KB);
+        put(buf ^ 1);
+      }
+      block_sync();
+    }
   }
   // ---- dQ^T tile dt: lane = query, registers = dims dt*32 + acc_row(i, h)
   if (qv) {
@@ -1209,12 +1314,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
 // slices.  The wave's K / V rows stay in registers as MFMA B fragments (they
 // are the same for every slice); a slice's Q / dO rows are staged ONCE per
 // workgroup in LDS (kimg layout: A-fragment row reads and the transposed
-// reads of the dV / dK products are both conflict-free), double-buffered with
-// the next slice loaded into registers under this one's MFMAs: one barrier
-// per slice.
+// reads of the dV / dK products are both conflict-free).
 //   S = Q K^T - lse/scale, dP = dO V^T - delta     (query rows, key lane)
 //   P = exp2(c S) (masked keys 0), dS = P dP
 //   dV += P^T dO, dK += dS^T Q   (the accumulators' registers as A operands)
+// Round 6 (kKvDma): the slices arrive by LDS-DMA straight into a 3-deep LDS
+// ring (slice j + 2 issued while slice j computes; each wave's 1 KiB piece
+// of Q and of dO is ONE buffer_load_dwordx4 ... lds whose per-lane source
+// offset un-applies the kimg chunk swizzle, wave 0 also moves the slice's
+// lse / delta), one counted vmcnt + barrier per slice.  This frees the 20
+// prefetch VGPRs of the register-staged form (round 4/5: two register sets
+// of Q / dO / lse / delta, whose 5 spilled VGPRs were reloaded inside the
+// slice loop -- and a spill reload's vmcnt wait also waited for the next
+// slices' prefetch, the kernel's memory wait).
+constexpr bool kKvDma = false;   // measured slower (profiles/r06_attn_ab_kv_dma.txt), kept for reference
 template <int HD>
 __global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
   static_assert(HD == 64, "kv kernel: hd 64 (its K / V / dK / dV registers)");
@@ -1222,9 +1335,11 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
   constexpr int QS = 32;                   // queries per staged slice
   constexpr int NPF = QS * HD / 8 / 256;   // 16-byte Q (and dO) chunks per thread per slice
   static_assert(NPF >= 1, "slice staging");
-  __shared__ __attribute__((aligned(16))) bf16_t sQ[2][QS * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t sG[2][QS * HD];
-  __shared__ __attribute__((aligned(16))) float sL[2][QS], sD[2][QS];
+  static_assert(!kKvDma || NPF == 1, "LDS-DMA staging: one 16-byte piece per thread and tensor per slice");
+  constexpr int NB = kKvDma ? 3 : 2;       // slice buffers
+  __shared__ __attribute__((aligned(16))) bf16_t sQ[NB][QS * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t sG[NB][QS * HD];
+  __shared__ __attribute__((aligned(16))) float sL[NB][64], sD[NB][64];
   const MttsAttnBwdArgs& a = p.a;
   const MttsAttnFwdArgs& f = a.f;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1267,84 +1382,24 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt) oT[u][dt] = kimg<HD>(4 * h + qq + 8 * u, 4 * dt + 2 * g + (pp >> 1)) + 4 * (pp & 1);
 
-  // ---- slice staging: loads issued unconditionally (clamped), consumed in put()
-  // slices as buffer loads (round 4): lane-constant row / column offsets,
-  // the slice origin in the scalar offset, rows at or past qend read zeros.
-  // Two register sets: slice j+2 is loaded while slice j computes and slice
-  // j+1 (loaded an iteration earlier) goes to LDS at its end -- two slices
-  // of L2 latency cover instead of one (the kernel's stall was memory wait,
-  // profiles/r04_attn_c5_pmc.txt)
-  f32x4 pq[2][NPF], pg[2][NPF];
-  float pl[2] = {0.f, 0.f}, pd[2] = {0.f, 0.f};
-  int ps0[2] = {qbeg, qbeg};
-  const __amdgpu_buffer_rsrc_t rq = brsrc(qb, (uint32_t)(((int64_t)(qend - 1) * f.q_ls + HD) * 2));
-  const __amdgpu_buffer_rsrc_t rg = brsrc(gb, (uint32_t)(((int64_t)(qend - 1) * a.do_ls + HD) * 2));
-  const __amdgpu_buffer_rsrc_t rl = brsrc(lbuf, (uint32_t)qend * 4);
-  const __amdgpu_buffer_rsrc_t rd = brsrc(dbuf, (uint32_t)qend * 4);
-  uint32_t oq_[NPF], og_[NPF];
-#pragma unroll
-  for (int i = 0; i < NPF; ++i) {
-    const int idx = tid + 256 * i;
-    const int row = idx / (HD / 8), cc = (idx % (HD / 8)) * 8;
-    oq_[i] = (uint32_t)((row * f.q_ls + cc) * 2);
-    og_[i] = (uint32_t)((row * a.do_ls + cc) * 2);
-  }
-  auto fetch = [&](auto set_c, int q0) __attribute__((always_inline)) {
-    constexpr int st = decltype(set_c)::value;
-    ps0[st] = q0;
-    const int sq = (int)(q0 * f.q_ls * 2), sg = (int)(q0 * a.do_ls * 2);
-#pragma unroll
-    for (int i = 0; i < NPF; ++i) {
-      pq[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, oq_[i], sq, 0));
-      pg[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, og_[i], sg, 0));
-    }
-    const uint32_t ol = (uint32_t)(tid & (QS - 1)) * 4;
-    pl[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, ol, q0 * 4, 0));
-    pd[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, ol, q0 * 4, 0));
-  };
-  auto put = [&](auto set_c, int buf) __attribute__((always_inline)) {
-    constexpr int st = decltype(set_c)::value;
-#pragma unroll
-    for (int i = 0; i < NPF; ++i) {
-      const int idx = tid + 256 * i;
-      const int row = idx / (HD / 8), ch = idx % (HD / 8);
-      *(f32x4*)(sQ[buf] + kimg<HD>(row, ch)) = pq[st][i];
-      *(f32x4*)(sG[buf] + kimg<HD>(row, ch)) = pg[st][i];
-    }
-    if (tid < QS) {
-      const bool in = ps0[st] + tid < qend;
-      sL[buf][tid] = in ? -pl[st] * inv_scale : 0.f;   // P = exp2(c (S + L))
-      sD[buf][tid] = in ? pd[st] : 0.f;
-    }
-  };
-
   f32x16 dK[ND], dV[ND];
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) dK[dt] = dV[dt] = f32x16{};
   const int nsl = qend > qbeg ? (qend - qbeg + QS - 1) / QS : 0;
-  const int qlast = qbeg + QS * (nsl - 1);
-  using S0_ = std::integral_constant<int, 0>;
-  using S1_ = std::integral_constant<int, 1>;
-  if (nsl > 0) {
-    fetch(S0_{}, qbeg);
-    put(S0_{}, 0);
-    fetch(S1_{}, min(qbeg + QS, qlast));
-  }
-  block_sync();
-  // slice j (LDS buffer j & 1); register set j & 1 is free (its slice went to
-  // LDS at the end of iteration j-1) and takes slice j+2, set (j+1) & 1
-  // holds slice j+1
-  auto slice = [&](auto par_c, int j) __attribute__((always_inline)) {
-    constexpr int par = decltype(par_c)::value;
-    const int q0 = qbeg + QS * j;
-    fetch(std::integral_constant<int, par>{}, min(q0 + 2 * QS, qlast));   // in flight under two slices' math
-    const bf16_t* qs = sQ[par];
-    const bf16_t* gs = sG[par];
+
+  // one slice of the query sweep from LDS buffer `buf`
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const bf16_t* qs = sQ[buf];
+    const bf16_t* gs = sG[buf];
     f32x16 S, D;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      S[i] = sL[par][acc_row(i, h)];
-      D[i] = sD[par][acc_row(i, h)];
+      if constexpr (kKvDma) {
+        S[i] = -sL[buf][acc_row(i, h)] * inv_scale;   // raw lse (0 past the chunk: P = 1 x zero rows)
+      } else {
+        S[i] = sL[buf][acc_row(i, h)];
+      }
+      D[i] = sD[buf][acc_row(i, h)];
     }
 #pragma unroll
     for (int s = 0; s < NQ; ++s) {
@@ -1366,12 +1421,119 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_kv_kernel(BwdParams p) {
         dK[dt] = mfma_bf16(da, cat(tr_read(qs + o0), tr_read(qs + o1)), dK[dt]);
       }
     }
-    if (j + 1 < nsl) put(std::integral_constant<int, par ^ 1>{}, par ^ 1);
-    block_sync();
   };
-  for (int j = 0; j < nsl; j += 2) {
-    slice(S0_{}, j);
-    if (j + 1 < nsl) slice(S1_{}, j + 1);
+
+  if constexpr (kKvDma) {
+    // LDS slot s of a slice image (16-byte chunk, s = 64 * wave + lane):
+    // image row s / 8, physical chunk s % 8 = logical chunk ^ kswz(row)
+    const int srow = 8 * wave + (lane >> 3);
+    const int sch = (lane & 7) ^ kswz<HD>(srow);
+    const uint32_t vq = (uint32_t)((srow * f.q_ls + 8 * sch) * 2);
+    const uint32_t vg = (uint32_t)((srow * a.do_ls + 8 * sch) * 2);
+    const uint32_t vl = lane < QS ? (uint32_t)lane * 4 : 0xFFFFFFF0u;   // lanes >= 32: past every range, read 0
+    // descriptors over the chunk's rows: rows at or past qend read zeros
+    const i32x4a rq = rsrc4a(qb, (uint32_t)(((int64_t)(qend - 1) * f.q_ls + HD) * 2));
+    const i32x4a rg = rsrc4a(gb, (uint32_t)(((int64_t)(qend - 1) * a.do_ls + HD) * 2));
+    const i32x4a rl = rsrc4a(lbuf, (uint32_t)qend * 4);
+    const i32x4a rd = rsrc4a(dbuf, (uint32_t)qend * 4);
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    auto sgpr = [](int v) __attribute__((always_inline)) { return __builtin_amdgcn_readfirstlane(v); };
+    auto dma_slice = [&](int q0, int buf) __attribute__((always_inline)) {
+      dma16_lds(rq, vq, sgpr(q0 * f.q_ls * 2), sgpr((int)lds_addr(sQ[buf]) + 1024 * wv));
+      dma16_lds(rg, vg, sgpr(q0 * a.do_ls * 2), sgpr((int)lds_addr(sG[buf]) + 1024 * wv));
+      if (wv == 0) {
+        dma4_lds(rl, vl, sgpr(q0 * 4), lds_addr(sL[buf]));
+        dma4_lds(rd, vl, sgpr(q0 * 4), lds_addr(sD[buf]));
+      }
+    };
+    // VMEM operations one slice issues per wave: 4 on wave 0, 2 on the others;
+    // wait until at most `later` slices' operations are outstanding
+    auto wait_slices = [&](int later) __attribute__((always_inline)) {
+      if (wv == 0) {
+        if (later >= 1) wait_vmcnt<4>(); else wait_vmcnt<0>();
+      } else {
+        if (later >= 1) wait_vmcnt<2>(); else wait_vmcnt<0>();
+      }
+    };
+    if (nsl > 0) {
+      dma_slice(qbeg, 0);
+      if (nsl > 1) dma_slice(qbeg + QS, 1);
+      wait_slices(nsl > 1 ? 1 : 0);
+    }
+    block_sync();
+    for (int j = 0; j < nsl; ++j) {
+      if (j + 2 < nsl) dma_slice(qbeg + QS * (j + 2), (j + 2) % 3);   // buffer last read in slice j - 1
+      compute(j % 3);
+      if (j + 1 < nsl) wait_slices(j + 2 < nsl ? 1 : 0);              // slice j + 1 landed
+      block_sync();
+    }
+  } else {
+    // register-staged slices (round 4/5 form, kept for A/B): slice j + 2 is
+    // loaded while slice j computes and slice j + 1 goes to LDS at its end
+    f32x4 pq[2][NPF], pg[2][NPF];
+    float pl[2] = {0.f, 0.f}, pd[2] = {0.f, 0.f};
+    int ps0[2] = {qbeg, qbeg};
+    const __amdgpu_buffer_rsrc_t rq = brsrc(qb, (uint32_t)(((int64_t)(qend - 1) * f.q_ls + HD) * 2));
+    const __amdgpu_buffer_rsrc_t rg = brsrc(gb, (uint32_t)(((int64_t)(qend - 1) * a.do_ls + HD) * 2));
+    const __amdgpu_buffer_rsrc_t rl = brsrc(lbuf, (uint32_t)qend * 4);
+    const __amdgpu_buffer_rsrc_t rd = brsrc(dbuf, (uint32_t)qend * 4);
+    uint32_t oq_[NPF], og_[NPF];
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / (HD / 8), cc = (idx % (HD / 8)) * 8;
+      oq_[i] = (uint32_t)((row * f.q_ls + cc) * 2);
+      og_[i] = (uint32_t)((row * a.do_ls + cc) * 2);
+    }
+    auto fetch = [&](auto set_c, int q0) __attribute__((always_inline)) {
+      constexpr int st = decltype(set_c)::value;
+      ps0[st] = q0;
+      const int sq = (int)(q0 * f.q_ls * 2), sg = (int)(q0 * a.do_ls * 2);
+#pragma unroll
+      for (int i = 0; i < NPF; ++i) {
+        pq[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, oq_[i], sq, 0));
+        pg[st][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rg, og_[i], sg, 0));
+      }
+      const uint32_t ol = (uint32_t)(tid & (QS - 1)) * 4;
+      pl[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, ol, q0 * 4, 0));
+      pd[st] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, ol, q0 * 4, 0));
+    };
+    auto put = [&](auto set_c, int buf) __attribute__((always_inline)) {
+      constexpr int st = decltype(set_c)::value;
+#pragma unroll
+      for (int i = 0; i < NPF; ++i) {
+        const int idx = tid + 256 * i;
+        const int row = idx / (HD / 8), ch = idx % (HD / 8);
+        *(f32x4*)(sQ[buf] + kimg<HD>(row, ch)) = pq[st][i];
+        *(f32x4*)(sG[buf] + kimg<HD>(row, ch)) = pg[st][i];
+      }
+      if (tid < QS) {
+        const bool in = ps0[st] + tid < qend;
+        sL[buf][tid] = in ? -pl[st] * inv_scale : 0.f;   // P = exp2(c (S + L))
+        sD[buf][tid] = in ? pd[st] : 0.f;
+      }
+    };
+    const int qlast = qbeg + QS * (nsl - 1);
+    using S0_ = std::integral_constant<int, 0>;
+    using S1_ = std::integral_constant<int, 1>;
+    if (nsl > 0) {
+      fetch(S0_{}, qbeg);
+      put(S0_{}, 0);
+      fetch(S1_{}, min(qbeg + QS, qlast));
+    }
+    block_sync();
+    auto slice = [&](auto par_c, int j) __attribute__((always_inline)) {
+      constexpr int par = decltype(par_c)::value;
+      const int q0 = qbeg + QS * j;
+      fetch(std::integral_constant<int, par>{}, min(q0 + 2 * QS, qlast));   // in flight under two slices' math
+      compute(par);
+      if (j + 1 < nsl) put(std::integral_constant<int, par ^ 1>{}, par ^ 1);
+      block_sync();
+    };
+    for (int j = 0; j < nsl; j += 2) {
+      slice(S0_{}, j);
+      if (j + 1 < nsl) slice(S1_{}, j + 1);
+    }
   }
   // ---- dK (scaled), dV: rows = keys (registers), cols = dims (lanes)
 #pragma unroll
