@@ -1078,7 +1078,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   // block's 64 key-mask bytes), one counted vmcnt + barrier per block; this
   // frees the 16 staging VGPRs of the register-staged form (kept for hd 128,
   // whose three 32 KiB buffers would not leave room for two workgroups)
-  constexpr bool kDqDma = HD == 64;
+  // OFF: the dK / dV form of this staging measured 3 % slower
+  // (profiles/r06_attn_ab_kv_dma.txt); this one also reads the key mask as
+  // dwords, whose per-dword range check drops the last partial dword of a
+  // row (kv_len % 4 != 0) -- byte loads would be needed before enabling it
+  constexpr bool kDqDma = false;
   constexpr int NBUF = kDqDma ? 3 : 2;
   __shared__ __attribute__((aligned(16))) bf16_t sK[NBUF][KB * HD];
   __shared__ __attribute__((aligned(16))) bf16_t sV[NBUF][KB * HD];

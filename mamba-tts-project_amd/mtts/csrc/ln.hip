@@ -101,8 +101,15 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
   const bool film = f.gamma != nullptr;
   const int grp = film ? row0 / f.rows_per_group : 0;
   const bool csum = a.dx_colsum != nullptr;
+  // Parameter-gradient partials from TWO running sums per column (round 6):
+  // the block's RB rows lie in one FiLM group (ln_rb), so gamma_g is a
+  // constant per column and, with A = sum dy * xhat, S = sum dy over the rows:
+  //   dw = gamma_g A, db = gamma_g S (no FiLM: gamma_g = 1),
+  //   dgamma = w A + b S, dbeta = S
+  // -- 32 fewer accumulator VGPRs than four running sums, which pays for the
+  // residual-gradient row (dx_acc) prefetched with x / dy one row ahead.
   float wv[NV][VEC], bv[NV][VEC], gv[NV][VEC];
-  float pdw[NV][VEC], pdb[NV][VEC], pdg[NV][VEC], pdbe[NV][VEC], pdx[NV][VEC];
+  float pA[NV][VEC], pS[NV][VEC], pdx[NV][VEC];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c0 = (k * 64 + lane) * VEC;
@@ -112,13 +119,17 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < VEC; ++q) {
       if (!film) gv[k][q] = 1.f;
-      pdw[k][q] = pdb[k][q] = pdg[k][q] = pdbe[k][q] = pdx[k][q] = 0.f;
+      pA[k][q] = pS[k][q] = pdx[k][q] = 0.f;
     }
   }
   const T* xsrc = (const T*)((f.res && f.x_sum) ? f.x_sum : f.x);
   const int64_t xrs = (f.res && f.x_sum) ? f.xsum_rs : f.x_rs;
   const int rend = min(RB, f.rows - row0);
+  const bool acc = a.dx_acc != nullptr;
+  // raw 16-byte pieces of the residual-gradient row when a vector holds 16 bytes
+  constexpr bool kRawAcc = VEC * sizeof(T) == 16;
   float nxv[NV][VEC], ndy[NV][VEC];
+  uint4 nacc[kRawAcc ? NV : 1];
   auto load_row = [&](int rr) __attribute__((always_inline)) {
     const int row = row0 + rr;
 #pragma unroll
@@ -126,6 +137,9 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
       const int c0 = (k * 64 + lane) * VEC;
       ld_vec<T, VEC>(xsrc + (int64_t)row * xrs + c0, nxv[k]);
       ld_vec<T, VEC>((const T*)a.dy + (int64_t)row * a.dy_rs + c0, ndy[k]);
+      if constexpr (kRawAcc) {
+        if (acc) nacc[k] = *reinterpret_cast<const uint4*>((const T*)a.dx_acc + (int64_t)row * a.dxacc_rs + c0);
+      }
     }
   };
   if (wave < rend) load_row(wave);
@@ -133,31 +147,26 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
     const int row = row0 + r;
     const float mean = f.mean[row], rstd = f.rstd[row];
     float cxv[NV][VEC], cdy[NV][VEC];
+    uint4 cacc[kRawAcc ? NV : 1];
 #pragma unroll
-    for (int k = 0; k < NV; ++k)
+    for (int k = 0; k < NV; ++k) {
 #pragma unroll
       for (int q = 0; q < VEC; ++q) { cxv[k][q] = nxv[k][q]; cdy[k][q] = ndy[k][q]; }
+      if constexpr (kRawAcc) cacc[k] = nacc[k];
+    }
     if (r + kLnBwdWaves < rend) load_row(r + kLnBwdWaves);
     float xh[NV][VEC], dxh[NV][VEC];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-      const int c0 = (k * 64 + lane) * VEC;
-      float xv[VEC], dy[VEC];
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) { xv[q] = cxv[k][q]; dy[q] = cdy[k][q]; }
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
-        const float h = (xv[q] - mean) * rstd;
+        const float h = (cxv[k][q] - mean) * rstd;
         xh[k][q] = h;
-        const float g = dy[q] * gv[k][q];
-        pdw[k][q] = fmaf(g, h, pdw[k][q]);
-        pdb[k][q] += g;
-        if (film) {
-          pdg[k][q] = fmaf(dy[q], fmaf(h, wv[k][q], bv[k][q]), pdg[k][q]);
-          pdbe[k][q] += dy[q];
-        }
-        const float d = g * wv[k][q];
+        const float dy = cdy[k][q];
+        pA[k][q] = fmaf(dy, h, pA[k][q]);
+        pS[k][q] += dy;
+        const float d = dy * gv[k][q] * wv[k][q];
         dxh[k][q] = d;
         s1 += d;
         s2 = fmaf(d, h, s2);
@@ -170,9 +179,23 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
       float o[VEC];
 #pragma unroll
       for (int q = 0; q < VEC; ++q) o[q] = rstd * (dxh[k][q] - m1 - xh[k][q] * m2);
-      if (a.dx_acc) {
+      if (acc) {
         float t[VEC];
-        ld_vec<T, VEC>((const T*)a.dx_acc + (int64_t)row * a.dxacc_rs + c0, t);
+        if constexpr (kRawAcc) {
+          if constexpr (sizeof(T) == 2) {
+            const uint32_t w4[4] = {cacc[k].x, cacc[k].y, cacc[k].z, cacc[k].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              t[2 * q] = __uint_as_float(w4[q] << 16);
+              t[2 * q + 1] = __uint_as_float(w4[q] & 0xffff0000u);
+            }
+          } else {
+            t[0] = __uint_as_float(cacc[k].x); t[1] = __uint_as_float(cacc[k].y);
+            t[2] = __uint_as_float(cacc[k].z); t[3] = __uint_as_float(cacc[k].w);
+          }
+        } else {
+          ld_vec<T, VEC>((const T*)a.dx_acc + (int64_t)row * a.dxacc_rs + c0, t);
+        }
 #pragma unroll
         for (int q = 0; q < VEC; ++q) o[q] += t[q];
       }
@@ -194,8 +217,9 @@ __global__ __launch_bounds__((64 * ln_bwd_waves<VEC, NV>())) void ln_bwd_kernel(
       const int c0 = (k * 64 + lane) * VEC;
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
-        const float val = which == 0 ? pdw[k][q] : which == 1 ? pdb[k][q] : which == 2 ? pdg[k][q]
-                        : which == 3 ? pdbe[k][q] : pdx[k][q];
+        const float A = pA[k][q], S = pS[k][q];
+        const float val = which == 0 ? gv[k][q] * A : which == 1 ? gv[k][q] * S
+                        : which == 2 ? fmaf(wv[k][q], A, bv[k][q] * S) : which == 3 ? S : pdx[k][q];
         sm[wave * n + c0 + q] = val;
       }
     }
