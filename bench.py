@@ -305,17 +305,26 @@ def style_bench(B=8, T_text=128, d_model=1024, d_style=256, iters=20):
                 ops.LengthRegulateFn.apply(text, dur, max_len)
     reg_ms = timed(graph.replay) / 10
     reg_bytes = B * max_len * d_model * 2 + B * T_text * d_model * 2
+    # as train_harness runs it: fp32 master parameters, bf16 compute
+    # (compute_dtype), gradients set to None before each step (no accumulation
+    # kernels), and a fixed upstream gradient for the frames (the loss that
+    # would consume them is not part of the pipeline)
     pipe = sca.StyleConditioningPipeline(d_style=d_style, d_model=d_model, num_heads=8, dropout=0.1).to(dev)
-    pipe = pipe.to(torch.bfloat16)
+    pipe.compute_dtype = torch.bfloat16
     pipe.eval()
     with torch.no_grad():
         eval_ms = timed(lambda: pipe(text, style, dur, max_frame_len=max_len))
     pipe.train()
     textg = text.detach().requires_grad_(True)
+    gframes = torch.randn(B, max_len, d_model, device=dev, generator=g).to(torch.bfloat16)
+    params = list(pipe.parameters())
 
     def train_step():
+        for prm in params:
+            prm.grad = None
+        textg.grad = None
         frames, _, _, _ = pipe(textg, style, dur, max_frame_len=max_len)
-        frames.float().square().mean().backward()
+        frames.backward(gframes)
     train_ms = timed(train_step)
     return {"B": B, "T_text": T_text, "T_frame": max_len, "d_model": d_model, "dtype": "bf16",
             "regulator": {"ms": reg_ms, "bound": "hbm", "achieved": reg_bytes / reg_ms / 1e6, "peak": HBM_PEAK / 1e9,

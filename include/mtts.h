@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MTTS_ABI_VERSION 13
+#define MTTS_ABI_VERSION 14
 
 enum { MTTS_F32 = 0, MTTS_BF16 = 1 };
 enum {
@@ -465,6 +465,20 @@ int mtts_embed_sum(const int64_t* tokens, int64_t tok_bs, const int* quant_ids, 
                    const float* tok_w, const float* q_w, const float* pos_w, int batch, int L, int d, int vocab,
                    void* out, int dtype, int64_t out_bs, int* err_flag, void* stream);
 
+/* Gradient of a small embedding table (ABI 14; csrc/regulate.hip): the
+ * token-embedding backward of mamba_decoder.py:167 (token_embed) and
+ * train.py:115-131 (the reference embedding through the same table) for the
+ * codec vocabulary (train.py's 10 codes):
+ *   out[v, c] = sum over rows r with ids[r] == v of g[r * g_rs + c]   (fp32)
+ * ids int64 (n), g (n, d) MTTS_F32 / MTTS_BF16 rows of whole 16-byte pieces
+ * (d and g_rs multiples of 4 / 8, g 16-byte aligned), vocab <= 16; ids
+ * outside [0, vocab) contribute nothing (the forward flags them).  One pass
+ * over g, fixed-order sums (bitwise reproducible).  workspace: at least
+ * mtts_embed_table_grad_workspace(n, d, vocab) bytes. */
+int64_t mtts_embed_table_grad_workspace(int64_t n, int d, int vocab);
+int mtts_embed_table_grad(const int64_t* ids, int64_t n, const void* g, int dtype, int64_t g_rs, int d, int vocab,
+                          float* out, void* workspace, void* stream);
+
 /* ------------------------------------------------------------------------
  * Decode-step projections (MambaTTSDecoder.decode_step, mamba_decoder.py:
  * 188-256 -> Mamba.step in_proj/x_proj/out_proj, the cross-attention q/out
@@ -741,6 +755,11 @@ int mtts_gemm_skinny(const MttsSkinnyArgs* a, void* stream);
  * over a single key, one draw per (batch, head, query) shared by the head's
  * channels.  Contiguous x / y / pre, 16-byte aligned; n % 8 == 0;
  * 0 <= p < 1; x == y allowed (in place).
+ * `x_rep` > 1 (ABI 14): x is broadcast over a middle dimension -- y is
+ * (n / (x_rep * x_inner), x_rep, x_inner), x is (n / (x_rep * x_inner),
+ * x_inner) and y[o, r, c] drops x[o, c] (x_inner a multiple of 8 / 4; no
+ * `pre`, not in place): the single-key attention's value row expanded over
+ * the queries without a materialised copy.
  * ------------------------------------------------------------------------ */
 typedef struct {
   int64_t n;
@@ -751,6 +770,8 @@ typedef struct {
   void* y;
   const void* pre;           /* optional bf16 GELU pre-activation (DGELU form) */
   int group;                 /* elements per mask draw (0 / 1: every element) */
+  int x_rep;                 /* ABI 14: > 1 = x broadcast x_rep times over the middle dimension */
+  int x_inner;               /* ABI 14: the broadcast rows' length (elements) */
   int reserved_;
 } MttsDropoutArgs;
 

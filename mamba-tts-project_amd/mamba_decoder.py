@@ -26,7 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from mtts.mamba import Mamba
-from mtts.attention import CrossAttention
+from mtts.attention import CrossAttention, kv_all, kv_all_ok
 from mtts import ops
 from mtts.linear import BiasGradSlot, cast_scope, ffn, linear
 from mtts.decode import DecodeEngine
@@ -94,7 +94,7 @@ class MambaTTSDecoderLayer(nn.Module):
         return x + ff_out, new_state                                          # :88-89
 
     def forward_fused(self, x, pending, text_hidden, z_style, text_mask=None, mamba_state=None, kpm=None, gb=None,
-                      ff_slot=True):
+                      ff_slot=True, kv=None):
         """Same math as forward(); the input residual `x + pending` and the
         output residual `x + ff_out` are left to the neighbouring fused
         residual+LayerNorm kernels.  `gb` (B, 2d): this layer's
@@ -103,6 +103,8 @@ class MambaTTSDecoderLayer(nn.Module):
         residual+LayerNorm backward that consumes those outputs (BiasGradSlot;
         `ff_slot`: ff_out feeds only the next fused LayerNorm, which reads the
         slot attached to it as `_mtts_dbias_slot`).
+        `kv`: this layer's K/V projection of text_hidden when the decoder
+        ran all layers' at once (mtts.attention.kv_all).
         Returns (x, ff_out, new_state)."""
         T = x.shape[1]
         # 1) (x += pending) ; h = norm_mamba(x) ; Mamba   (mamba_decoder.py:59-64)
@@ -120,7 +122,7 @@ class MambaTTSDecoderLayer(nn.Module):
             key_padding_mask = ~text_mask                                   # :68-70 (sic)
         attn_slot = BiasGradSlot()
         attn_out, _ = self.cross_attn(query=h, key=text_hidden, value=text_hidden,
-                                      key_padding_mask=key_padding_mask, _dbias_slot=attn_slot)
+                                      key_padding_mask=key_padding_mask, _dbias_slot=attn_slot, _kv=kv)
 
         # 3) x = x + attn ; h = gamma * norm_ff(x) + beta   (fused, :78-86);
         # gamma | beta as ONE fp32 (B, 2d) tensor (its gradient written in place)
@@ -230,10 +232,15 @@ class MambaTTSDecoder(nn.Module):
         new_states = []
         kpm = None if text_mask is None else ~text_mask                     # :68-70 (sic), once for all layers
         gbs = self._style_all(z_style, x.dtype) if x.shape[1] > 1 else None
+        # every layer's K/V projection of the shared text (+ reference) states
+        # in one GEMM (mtts.attention.KVAllFn; reference :72-77 per layer)
+        attns = [l.cross_attn for l in self.layers]
+        kvs = kv_all(text_hidden, attns) if kv_all_ok(text_hidden, attns) else None
         for i, layer in enumerate(self.layers):
             x, pending, st = layer.forward_fused(x, pending, text_hidden, z_style, text_mask,
                                                  None if states is None else states[i], kpm=kpm,
-                                                 gb=None if gbs is None else gbs[i])
+                                                 gb=None if gbs is None else gbs[i],
+                                                 kv=None if kvs is None else kvs[i])
             new_states.append(st)
         return x, pending, new_states
 

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MTTS_LIB", os.path.join(_HERE, "libmtts.so"))
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 F32, BF16 = 0, 1
 i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
@@ -91,7 +91,7 @@ class GemmArgs(C.Structure):
 
 class DropoutArgs(C.Structure):
     _fields_ = [("n", i64), ("dtype", i32), ("p", f32), ("seed", C.c_uint64), ("x", vp), ("y", vp), ("pre", vp),
-                ("group", i32), ("reserved_", i32)]
+                ("group", i32), ("x_rep", i32), ("x_inner", i32), ("reserved_", i32)]
 
 
 class RowMap(C.Structure):
@@ -193,6 +193,8 @@ _SIGS = {
     "mtts_adam_workspace": ([i64], i64),
     "mtts_clip_adam": ([vp, i32, i64, vp, f32, f32, f32, f32, f32, f32, vp, vp, vp], i32),
     "mtts_embed_sum": ([vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, i32, i64, vp, vp], i32),
+    "mtts_embed_table_grad_workspace": ([i64, i32, i32], i64),
+    "mtts_embed_table_grad": ([vp, i64, vp, i32, i64, i32, i32, vp, vp, vp], i32),
     "mtts_cast_tiles": ([i32, i32], i64),
     "mtts_cast_bf16_multi": ([vp, i32, i64, vp], i32),
     "mtts_length_regulate_lengths": ([vp, i64, i32, i32, vp, vp], i32),

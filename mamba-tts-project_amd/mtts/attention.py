@@ -70,6 +70,132 @@ class InProjFn(torch.autograd.Function):
         return dquery, dkey, dW, db
 
 
+class DkvSink:
+    """One (M, L*2d) buffer for the K/V gradients of the L layers whose K/V
+    projections ran as one GEMM (KVAllFn): each layer's attention backward
+    writes its dK / dV straight into its column slice, so the projection's
+    backward reads them as ONE operand (no per-layer copies or adds)."""
+
+    def __init__(self, rows, n_layers, width, shape, device, dtype):
+        self.rows, self.L, self.width, self.shape = rows, n_layers, width, shape
+        self.device, self.dtype = device, dtype
+        self.buf = None
+
+    def view(self, layer):
+        if self.buf is None:
+            self.buf = torch.empty(self.rows, self.L * self.width, device=self.device, dtype=self.dtype)
+        return self.buf[:, layer * self.width:(layer + 1) * self.width].view(*self.shape, self.width)
+
+
+class KVAllFn(torch.autograd.Function):
+    """kv_l = key W_l[d:]^T + b_l[d:] for every decoder layer l at once: the
+    layers' cross-attention K/V in-projections (nn.MultiheadAttention's
+    packed in_proj, mamba_decoder.py:72-77) all read the SAME text (+ voice
+    prompt) hidden states, so they run as ONE (M, L*2d) NT GEMM over the
+    stacked weight rows instead of L short-M GEMMs (C2: M = B*T_text = 1024,
+    twelve 1024 x 2048 x 1024 products).  The outputs are column views of
+    that product; the backward takes the L K/V gradients as one operand (the
+    attention backward writes them into a DkvSink) for ONE key gradient GEMM
+    (K = L*2d: the sum over layers inside the reduction, no autograd adds of
+    L (B, T_kv, d) gradients), the layers' weight gradients (row slices d:3d,
+    deferred like the rest, mtts.wgrad) and one bias column sum."""
+
+    @staticmethod
+    def forward(ctx, key, sink, *params):
+        cd = key.dtype
+        d = key.shape[-1]
+        Ws, bs = params[0::2], params[1::2]
+        k2 = key.reshape(-1, d)
+        Wst = torch.cat([cast_weight(W, cd)[d:] for W in Ws])             # (L*2d, d)
+        bst = torch.cat([cast_weight(b, cd)[d:] for b in bs])
+        kv = proj(k2, Wst, bst)                                           # (M, L*2d)
+        ctx.save_for_backward(k2)
+        ctx.Ws, ctx.bs, ctx.kshape, ctx.sink = Ws, bs, key.shape, sink
+        return tuple(kv[:, l * 2 * d:(l + 1) * 2 * d].view(*key.shape[:-1], 2 * d) for l in range(len(Ws)))
+
+    @staticmethod
+    def backward(ctx, *dkvs):
+        (k2,) = ctx.saved_tensors
+        Ws, bs, sink = ctx.Ws, ctx.bs, ctx.sink
+        nl, d = len(Ws), k2.shape[1]
+        w2 = 2 * d
+        cd = k2.dtype
+        in_sink = sink.buf is not None and all(
+            g is not None and g.data_ptr() == sink.buf.data_ptr() + l * w2 * sink.buf.element_size()
+            and g.stride()[-2] == nl * w2 for l, g in enumerate(dkvs))
+        if in_sink:
+            dkv = sink.buf
+        else:   # a layer's gradient arrived elsewhere (unused layer, accumulated use): assemble
+            dkv = torch.zeros(k2.shape[0], nl * w2, device=k2.device, dtype=cd)
+            for l, g in enumerate(dkvs):
+                if g is not None:
+                    dkv[:, l * w2:(l + 1) * w2] = g.reshape(-1, w2)
+        sink.buf = None
+        dkey = None
+        if ctx.needs_input_grad[0]:
+            if cd == torch.bfloat16:
+                WstT = torch.cat([cast_weight_t(W, cd)[:, d:] for W in Ws], dim=1)   # (d, L*2d)
+                dkey = proj(dkv, WstT).view(ctx.kshape)
+            else:
+                dkey = (dkv @ torch.cat([cast_weight(W, cd)[d:] for W in Ws])).view(ctx.kshape)
+        grads = [dkey, None]
+        cs = colsum(dkv) if any(ctx.needs_input_grad[3::2]) else None
+        for l in range(nl):
+            W, b = Ws[l], bs[l]
+            dy = dkv[:, l * w2:(l + 1) * w2]
+            dW = db = None
+            if ctx.needs_input_grad[2 + 2 * l] and not WG.submit([(dy, k2, W, (d, 3 * d))]):
+                dW = torch.zeros(W.shape, device=W.device, dtype=W.dtype)
+                dW[d:] = wgrad(dy.contiguous(), k2).to(W.dtype)
+            if ctx.needs_input_grad[3 + 2 * l]:
+                db = torch.zeros(b.shape, device=b.device, dtype=b.dtype)
+                db[d:] = cs[l * w2:(l + 1) * w2].to(b.dtype)
+            grads += [dW, db]
+        return tuple(grads)
+
+
+def kv_all(key: torch.Tensor, attns) -> list:
+    """The K/V in-projections of `attns` (CrossAttention modules of equal
+    width, packed in_proj with bias) over one shared `key`, as KVAllFn; a
+    list of (B, T_kv, 2d) column views, one per module."""
+    params = []
+    for a in attns:
+        params += [a.in_proj_weight, a.in_proj_bias]
+    d = attns[0].embed_dim
+    sink = DkvSink(key.numel() // d, len(attns), 2 * d, tuple(key.shape[:-1]), key.device, key.dtype)
+    outs = list(KVAllFn.apply(key, sink, *params))
+    for l, o in enumerate(outs):
+        o._mtts_dkv_sink = (sink, l)     # read by the attention backward (attn_kernels.AttentionKVFn)
+    return outs
+
+
+def kv_all_ok(key: torch.Tensor, attns) -> bool:
+    a0 = attns[0]
+    d = a0.embed_dim
+    return (len(attns) >= 2 and key.dim() == 3 and key.shape[-1] == d and key.shape[1] > 1 and key.is_cuda
+            and all(a.embed_dim == d and a.in_proj_bias is not None and a.in_proj_weight.dtype == torch.float32
+                    and a.in_proj_bias.dtype == torch.float32 and a.in_proj_weight.is_contiguous()
+                    and a.dropout == 0.0 for a in attns))
+
+
+class _KeyTie(torch.autograd.Function):
+    """Returns `o` unchanged and gives `key` an exactly-zero gradient (torch
+    MHA's gradient to a single key: dS = P * (dP - rowsum(P * dP)) = 0), so
+    optimizer state / weight decay of the key path behave as with torch MHA,
+    without a (B, Tq, d) broadcast add in the forward and its reduction over
+    Tq in the backward (what `o + 0 * key.sum()` would cost)."""
+
+    @staticmethod
+    def forward(ctx, o, key):
+        ctx.kmeta = (key.shape, key.dtype, key.device)
+        return o.view_as(o)
+
+    @staticmethod
+    def backward(ctx, do):
+        shape, dt, dev = ctx.kmeta
+        return do, torch.zeros(shape, dtype=dt, device=dev)
+
+
 class CrossAttention(nn.Module):
     def __init__(self, embed_dim, num_heads, dropout=0.0, batch_first=True, bias=True, device=None, dtype=None):
         super().__init__()
@@ -89,18 +215,24 @@ class CrossAttention(nn.Module):
         nn.init.constant_(self.in_proj_bias, 0.0)
         nn.init.constant_(self.out_proj.bias, 0.0)
 
-    def forward(self, query, key, value, key_padding_mask=None, need_weights=False, _dbias_slot=None):
+    def forward(self, query, key, value, key_padding_mask=None, need_weights=False, _dbias_slot=None, _kv=None):
         """`_dbias_slot` (internal, linear.BiasGradSlot): out_proj's bias
         gradient is delivered by the consumer of the output (the decoder
-        layer's fused residual + LayerNorm backward)."""
+        layer's fused residual + LayerNorm backward).  `_kv` (internal): this
+        module's K/V projection of `key` (= `value`), computed with other
+        layers' by `kv_all`."""
         with cast_scope():
-            return self._forward(query, key, value, key_padding_mask, _dbias_slot)
+            return self._forward(query, key, value, key_padding_mask, _dbias_slot, _kv)
 
-    def _forward(self, query, key, value, key_padding_mask, dbias_slot=None):
+    def _forward(self, query, key, value, key_padding_mask, dbias_slot=None, kv_pre=None):
         cd = query.dtype
         d, H = self.embed_dim, self.num_heads
         W, b = self.in_proj_weight, self.in_proj_bias
         p_drop = self.dropout if self.training else 0.0
+        if kv_pre is not None:
+            q = linear(query, W, b, rows=(0, d))
+            o = attn_kernels.attention_kv(q, kv_pre, H, key_padding_mask, p_drop)
+            return linear(o, self.out_proj.weight, self.out_proj.bias, dbias_slot=dbias_slot), None
         if key.shape[1] == 1 and key_padding_mask is None:
             return self._single_key(query, key, value, p_drop), None
         if key is value:
@@ -136,9 +268,9 @@ class CrossAttention(nn.Module):
         v = linear(value.to(cd), self.in_proj_weight, self.in_proj_bias, rows=(2 * d, 3 * d))   # (B, 1, d)
         if p_drop > 0.0:
             from . import dropout as DO
-            o = DO.dropout(v.expand(B, Tq, d).contiguous(), p_drop, True, group=self.head_dim)
+            # the value row broadcast over the queries and dropped in one HIP pass
+            o = DO.dropout_bcast(v.reshape(B, d), Tq, p_drop, group=self.head_dim)
             o = linear(o, self.out_proj.weight, self.out_proj.bias)
-            return o + 0.0 * key.to(cd).sum(dim=-1, keepdim=True)
-        o = linear(v, self.out_proj.weight, self.out_proj.bias)
-        o = o + 0.0 * key.to(cd).sum(dim=-1, keepdim=True)
-        return o.expand(B, Tq, d).contiguous()
+        else:
+            o = linear(v, self.out_proj.weight, self.out_proj.bias).expand(B, Tq, d).contiguous()
+        return _KeyTie.apply(o, key) if torch.is_grad_enabled() and key.requires_grad else o

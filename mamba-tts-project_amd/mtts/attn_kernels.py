@@ -197,6 +197,9 @@ class AttentionKVFn(torch.autograd.Function):
     def forward(ctx, q, kv, n_heads, kpm):
         d = q.shape[-1]
         q = _prep(q)
+        # the K/V gradient's destination when kv is a column view of the
+        # layers' batched K/V projection (attention.KVAllFn / DkvSink)
+        ctx.sink = getattr(kv, "_mtts_dkv_sink", None)
         if not _aligned(kv[..., :d]) or not _aligned(kv[..., d:]):
             kv = kv.contiguous()
         out, lse = attention_fwd(q, kv[..., :d], kv[..., d:], n_heads, kpm, want_lse=True)
@@ -208,7 +211,14 @@ class AttentionKVFn(torch.autograd.Function):
     def backward(ctx, dout):
         q, kv, out, lse, kpm = ctx.saved_tensors
         d = q.shape[-1]
-        dkv = torch.empty(kv.shape, device=kv.device, dtype=kv.dtype)
+        dkv = None
+        if ctx.sink is not None:
+            sink, layer = ctx.sink
+            dkv = sink.view(layer)
+            if dkv.shape != kv.shape or not (_aligned(dkv[..., :d]) and _aligned(dkv[..., d:])):
+                dkv = None
+        if dkv is None:
+            dkv = torch.empty(kv.shape, device=kv.device, dtype=kv.dtype)
         dq, _, _ = attention_bwd(q, kv[..., :d], kv[..., d:], ctx.n_heads, kpm, out, lse, dout,
                                  dk=dkv[..., :d], dv=dkv[..., d:])
         return dq, dkv, None, None

@@ -14,6 +14,10 @@
 // finalizer of seed + i * golden, one 64-bit hash per element pair (its two
 // 32-bit halves).  HBM-bound: 16-byte loads / stores, 8 (bf16) or 4 (fp32)
 // elements per lane, a grid-stride loop over ~2 waves per SIMD.
+// x_rep > 1 (round 6): x is broadcast over a middle dimension -- y is
+// (outer, x_rep, x_inner) and x (outer, x_inner), read as x[o, c] for y[o, r, c]:
+// the single-key attention's value row expanded over the queries and dropped in
+// one pass (no materialised (B, Tq, d) copy).
 #include "common.h"
 
 namespace mtts {
@@ -54,14 +58,18 @@ __device__ __forceinline__ float gelu_grad(float x) {
 template <typename T, bool DGELU>
 __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                       const bf16_t* __restrict__ pre, int64_t n, uint64_t seed,
-                                                      uint32_t thresh, float scale, int group) {
+                                                      uint32_t thresh, float scale, int group, int x_rep,
+                                                      int x_inner) {
   constexpr int V = 16 / sizeof(T);   // elements per 16-byte piece
   const int64_t nv = n / V;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t inner_v = x_inner / V, outer_v = (int64_t)x_rep * inner_v;   // in 16-byte pieces
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    // source piece: v itself, or x[o, c] for a broadcast x
+    const int64_t sv = x_rep > 1 ? (v / outer_v) * inner_v + v % inner_v : v;
     float f[V];
     if constexpr (sizeof(T) == 2) {
-      const uint4 r = reinterpret_cast<const uint4*>(x)[v];
+      const uint4 r = reinterpret_cast<const uint4*>(x)[sv];
       const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -69,7 +77,7 @@ __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T
         f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
       }
     } else {
-      const float4 r = reinterpret_cast<const float4*>(x)[v];
+      const float4 r = reinterpret_cast<const float4*>(x)[sv];
       f[0] = r.x; f[1] = r.y; f[2] = r.z; f[3] = r.w;
     }
     float g[V];
@@ -143,6 +151,10 @@ extern "C" int mtts_dropout(const MttsDropoutArgs* a, void* stream) {
   const int vlen = a->dtype == MTTS_F32 ? 4 : 8;
   const int group = a->group > 0 ? a->group : 1;
   MTTS_CHECK(group == 1 || group % vlen == 0, "dropout: group=%d must be 1 or a multiple of %d", group, vlen);
+  const int x_rep = a->x_rep > 1 ? a->x_rep : 1;
+  MTTS_CHECK(x_rep == 1 || (a->x_inner > 0 && a->x_inner % vlen == 0 && a->n % ((int64_t)x_rep * a->x_inner) == 0),
+             "dropout: x_rep=%d needs x_inner=%d a multiple of %d dividing n / x_rep", x_rep, a->x_inner, vlen);
+  MTTS_CHECK(x_rep == 1 || (!a->pre && a->x != a->y), "dropout: a broadcast x takes no pre and is not in place");
   if (a->n == 0) return MTTS_OK;
   const uint32_t thresh = (uint32_t)fmin((double)a->p * 4294967296.0, 4294967295.0);
   const float scale = 1.f / (1.f - a->p);
@@ -152,17 +164,17 @@ extern "C" int mtts_dropout(const MttsDropoutArgs* a, void* stream) {
   if (a->dtype == MTTS_F32) {
     if (a->pre)
       hipLaunchKernelGGL((dropout_kernel<float, true>), dim3(blocks), dim3(256), 0, st, (const float*)a->x,
-                         (float*)a->y, (const bf16_t*)a->pre, a->n, a->seed, thresh, scale, group);
+                         (float*)a->y, (const bf16_t*)a->pre, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner);
     else
       hipLaunchKernelGGL((dropout_kernel<float, false>), dim3(blocks), dim3(256), 0, st, (const float*)a->x,
-                         (float*)a->y, nullptr, a->n, a->seed, thresh, scale, group);
+                         (float*)a->y, nullptr, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner);
   } else {
     if (a->pre)
       hipLaunchKernelGGL((dropout_kernel<bf16_t, true>), dim3(blocks), dim3(256), 0, st, (const bf16_t*)a->x,
-                         (bf16_t*)a->y, (const bf16_t*)a->pre, a->n, a->seed, thresh, scale, group);
+                         (bf16_t*)a->y, (const bf16_t*)a->pre, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner);
     else
       hipLaunchKernelGGL((dropout_kernel<bf16_t, false>), dim3(blocks), dim3(256), 0, st, (const bf16_t*)a->x,
-                         (bf16_t*)a->y, nullptr, a->n, a->seed, thresh, scale, group);
+                         (bf16_t*)a->y, nullptr, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner);
   }
   MTTS_LAUNCH_CHECK("dropout");
   return MTTS_OK;

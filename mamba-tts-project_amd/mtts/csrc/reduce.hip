@@ -10,12 +10,18 @@ namespace mtts {
 template <typename T, int W = 4>
 __global__ __launch_bounds__(64 * W) void colsum_kernel(const T* __restrict__ part, int nparts, int ppg,
                                                         int64_t pstride, int ncols, float* __restrict__ out,
-                                                        int64_t out_gstride) {
+                                                        int64_t out_gstride, int outer = 0) {
   __shared__ float red[W][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const int g = blockIdx.y;
-  const int p0 = g * ppg, p1 = min(nparts, p0 + ppg);
+  int p0 = g * ppg, p1 = min(nparts, p0 + ppg);
+  if (outer > 0) {   // chunks of ppg rows within groups of `outer` rows (the last chunk of a group ragged)
+    const int cpg = (outer + ppg - 1) / ppg;
+    const int og = g / cpg;
+    p0 = og * outer + (g % cpg) * ppg;
+    p1 = min(min(nparts, p0 + ppg), (og + 1) * outer);
+  }
   float acc[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) acc[q] = 0.f;
@@ -214,20 +220,22 @@ extern "C" int mtts_colsum(const void* in, int dtype, int rows, int cols, int64_
   }
   if (rows_per_group > 1024) {
     // two stages: 256-row chunks -> fp32 partial slab -> per-group sum of chunks
+    // (a group of rows_per_group % 256 != 0 rows ends in a ragged chunk)
     MTTS_CHECK(workspace, "colsum: workspace required (mtts_colsum_workspace)");
-    MTTS_CHECK(rows_per_group % 256 == 0 || rows_per_group >= rows, "colsum: rows_per_group %% 256 != 0");
-    const int chunks = (rows + 255) / 256;
+    const int rpg = std::min(rows_per_group, rows);
+    const bool ragged = rpg % 256 != 0 && rpg < rows;
+    const int cpg = (rpg + 255) / 256;
+    const int chunks = ragged ? ((rows + rpg - 1) / rpg) * cpg : (rows + 255) / 256;
     float* part = (float*)workspace;
     dim3 g1((cols + 63) / 64, chunks);
     if (dtype == MTTS_F32)
       hipLaunchKernelGGL((colsum_kernel<float, 4>), g1, dim3(256), 0, st, (const float*)in, rows, 256, row_stride, cols,
-                         part, (int64_t)cols);
+                         part, (int64_t)cols, ragged ? rpg : 0);
     else
       hipLaunchKernelGGL((colsum_kernel<bf16_t, 4>), g1, dim3(256), 0, st, (const bf16_t*)in, rows, 256, row_stride,
-                         cols, part, (int64_t)cols);
+                         cols, part, (int64_t)cols, ragged ? rpg : 0);
     MTTS_LAUNCH_CHECK("colsum stage 1");
-    const int cpg = rows_per_group >= rows ? chunks : rows_per_group / 256;
-    colsum(part, chunks, cpg, cols, cols, out, out_gstride, st);
+    colsum(part, chunks, rows_per_group >= rows ? chunks : cpg, cols, cols, out, out_gstride, st);
     MTTS_LAUNCH_CHECK("colsum stage 2");
     return MTTS_OK;
   }

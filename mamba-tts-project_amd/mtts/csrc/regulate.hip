@@ -289,3 +289,116 @@ extern "C" int mtts_embed_sum(const int64_t* tokens, int64_t tok_bs, const int* 
   MTTS_LAUNCH_CHECK("embed_sum");
   return MTTS_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Gradient of a small embedding table (the codec vocabulary, train.py's 10
+// codes: mamba_decoder.py:167 token_embed and train.py:115-131's reference
+// embedding share it):  out[v, :] = sum over rows r with ids[r] == v of g[r, :].
+// nn.Embedding's backward sorts the ids and scatters; a one-hot GEMM
+// (onehot^T g, K = all rows, M = V) runs as a long thin reduction on hipBLASLt
+// (~91 us per C5 call).  Here one pass over g: a lane owns 16 bytes of a row
+// (8 bf16 / 4 fp32 columns) and keeps V <= 16 bins of them in registers (an
+// fma by (id == v) per bin: no dynamic register indexing, no atomics), a
+// block's 4 waves combine in LDS in a fixed order, and the per-block (V, d)
+// slabs are summed by the deterministic column sum.  HBM-bound: reads g once.
+namespace mtts {
+
+constexpr int kEmbGradVMax = 16;
+
+template <typename T>
+__global__ __launch_bounds__(256) void embed_table_grad_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                                               const T* __restrict__ g, int64_t g_rs, int d, int V,
+                                                               int rpb, float* __restrict__ part) {
+  constexpr int EPL = 16 / (int)sizeof(T);
+  constexpr int CB = 64 * EPL;
+  __shared__ float red[4][CB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * CB + lane * EPL;
+  const int64_t r0 = (int64_t)blockIdx.y * rpb, r1 = min(n, r0 + rpb);
+  float acc[kEmbGradVMax][EPL];
+#pragma unroll
+  for (int v = 0; v < kEmbGradVMax; ++v)
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) acc[v][q] = 0.f;
+  if (c < d) {
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+      const int64_t id = ids[r];
+      const uint4 raw = *reinterpret_cast<const uint4*>(g + r * g_rs + c);
+      float x[EPL];
+      if constexpr (sizeof(T) == 2) {
+        const uint32_t u[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          x[2 * q] = __uint_as_float(u[q] << 16);
+          x[2 * q + 1] = __uint_as_float(u[q] & 0xffff0000u);
+        }
+      } else {
+        x[0] = __uint_as_float(raw.x); x[1] = __uint_as_float(raw.y);
+        x[2] = __uint_as_float(raw.z); x[3] = __uint_as_float(raw.w);
+      }
+#pragma unroll
+      for (int v = 0; v < kEmbGradVMax; ++v) {
+        const float m = id == v ? 1.f : 0.f;
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) acc[v][q] = fmaf(m, x[q], acc[v][q]);
+      }
+    }
+  }
+  for (int v = 0; v < V; ++v) {   // block-uniform loop
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) red[w][lane * EPL + q] = acc[v][q];
+    block_sync();
+    for (int k = threadIdx.x; k < CB; k += 256) {
+      const int cc = blockIdx.x * CB + k;
+      if (cc < d) part[((int64_t)blockIdx.y * V + v) * d + cc] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    }
+    block_sync();
+  }
+}
+
+static int emb_grad_blocks(int64_t n, int* rpb) {
+  int r = (int)std::max<int64_t>(64, (n + 255) / 256);
+  r = (r + 3) / 4 * 4;
+  *rpb = r;
+  return (int)((n + r - 1) / r);
+}
+
+}  // namespace mtts
+
+extern "C" int64_t mtts_embed_table_grad_workspace(int64_t n, int d, int vocab) {
+  int rpb = 0;
+  const int nblk = mtts::emb_grad_blocks(n, &rpb);
+  return (int64_t)nblk * vocab * d * 4 + 256;
+}
+
+extern "C" int mtts_embed_table_grad(const int64_t* ids, int64_t n, const void* g, int dtype, int64_t g_rs, int d,
+                                     int vocab, float* out, void* workspace, void* stream) {
+  using namespace mtts;
+  MTTS_CHECK(n >= 0 && d > 0 && vocab > 0 && vocab <= kEmbGradVMax, "embed_table_grad: vocab=%d must be in [1, %d]",
+             vocab, kEmbGradVMax);
+  MTTS_CHECK(dtype == MTTS_F32 || dtype == MTTS_BF16, "embed_table_grad: bad dtype");
+  MTTS_CHECK(out, "embed_table_grad: null output");
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    (void)hipMemsetAsync(out, 0, (size_t)vocab * d * 4, st);
+    return MTTS_OK;
+  }
+  const int vl = dtype == MTTS_F32 ? 4 : 8;
+  MTTS_CHECK(ids && g && workspace, "embed_table_grad: null pointer");
+  MTTS_CHECK(d % vl == 0 && g_rs % vl == 0 && (uintptr_t)g % 16 == 0,
+             "embed_table_grad: rows must be whole 16-byte pieces (d=%d, row stride=%lld)", d, (long long)g_rs);
+  int rpb = 0;
+  const int nblk = emb_grad_blocks(n, &rpb);
+  float* part = (float*)workspace;
+  const dim3 grid((d + 64 * vl - 1) / (64 * vl), nblk);
+  if (dtype == MTTS_F32)
+    hipLaunchKernelGGL(embed_table_grad_kernel<float>, grid, dim3(256), 0, st, ids, n, (const float*)g, g_rs, d, vocab,
+                       rpb, part);
+  else
+    hipLaunchKernelGGL(embed_table_grad_kernel<bf16_t>, grid, dim3(256), 0, st, ids, n, (const bf16_t*)g, g_rs, d,
+                       vocab, rpb, part);
+  MTTS_LAUNCH_CHECK("embed_table_grad");
+  colsum(part, nblk, nblk, (int64_t)vocab * d, vocab * d, out, 0, st);
+  MTTS_LAUNCH_CHECK("embed_table_grad sum");
+  return MTTS_OK;
+}

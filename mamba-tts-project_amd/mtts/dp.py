@@ -113,6 +113,10 @@ class GradAllReduce:
             # no gradient for p -- the deferred weight gradients (mtts.wgrad)
             # do exactly that and announce p through the engine's listener
             return
+        if not from_listener and wgrad.owns(p):
+            # a deferred gradient still incomplete (some row slices queued or
+            # not yet submitted): the engine's listener announces it when done
+            return
         if id(p) in self.counted:
             # counted once per step: a deferred gradient flushed inside p's own
             # backward (mtts.wgrad's mid-backward flush) is announced by the

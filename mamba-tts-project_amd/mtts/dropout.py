@@ -29,20 +29,28 @@ def _ok(t: torch.Tensor) -> bool:
 
 
 def apply_mask(x: torch.Tensor, p: float, seed: int, pre: torch.Tensor = None, out: torch.Tensor = None,
-               group: int = 1):
+               group: int = 1, rep: int = 1):
     """y = x * keep(seed) / (1 - p) [* gelu'(pre)] on the HIP kernel; one
-    mask draw per `group` consecutive elements."""
+    mask draw per `group` consecutive elements.  `rep` > 1: x (O, C) is
+    broadcast to y (O, rep, C) (y[o, r] drops x[o]) without a copy."""
     if not _ok(x):
         raise ValueError(f"dropout: contiguous 16-byte-aligned fp32/bf16 CUDA tensor with numel % 8 == 0 expected "
                          f"(got {x.dtype}, {tuple(x.shape)}, contiguous={x.is_contiguous()})")
     if pre is not None and (pre.dtype != torch.bfloat16 or pre.numel() != x.numel() or not _ok(pre)):
         raise ValueError("dropout: pre must be a contiguous bf16 tensor of x's size")
-    y = torch.empty_like(x) if out is None else out
+    if rep > 1:
+        inner = x.shape[-1]
+        y = torch.empty(x.numel() // inner, rep, inner, device=x.device, dtype=x.dtype) if out is None else out
+        if y.numel() != x.numel() * rep or not y.is_contiguous():
+            raise ValueError("dropout: broadcast output must be a contiguous (O, rep, C) tensor")
+    else:
+        y = torch.empty_like(x) if out is None else out
     a = L.DropoutArgs()
-    a.n, a.dtype, a.p, a.seed = x.numel(), L.dtype_code(x), float(p), seed & (2 ** 64 - 1)
+    a.n, a.dtype, a.p, a.seed = y.numel(), L.dtype_code(x), float(p), seed & (2 ** 64 - 1)
     a.x, a.y = x.data_ptr(), y.data_ptr()
     a.pre = 0 if pre is None else pre.data_ptr()
     a.group = group
+    a.x_rep, a.x_inner = (rep, x.shape[-1]) if rep > 1 else (1, 0)
     L.call("mtts_dropout", a)
     return y
 
@@ -56,6 +64,35 @@ class DropoutFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         return apply_mask(dy.contiguous(), ctx.p, ctx.seed, group=ctx.group), None, None
+
+
+class BcastDropoutFn(torch.autograd.Function):
+    """dropout(x[:, None, :].expand(O, rep, C)) in one HIP pass (x (O, C));
+    backward: the same mask on dy, then the column sums over each o's rep rows
+    (mtts_colsum, fp32) -- the expand's gradient."""
+
+    @staticmethod
+    def forward(ctx, x, rep, p, group):
+        ctx.p, ctx.seed, ctx.group, ctx.rep = p, new_seed(), group, rep
+        ctx.xmeta = (x.shape, x.dtype)
+        return apply_mask(x.contiguous(), p, ctx.seed, group=group, rep=rep)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .linear import colsum_groups
+        O, R, Cn = dy.shape
+        g = apply_mask(dy.contiguous(), ctx.p, ctx.seed, group=ctx.group)
+        dx = colsum_groups(g.view(O * R, Cn), R).to(ctx.xmeta[1]).view(ctx.xmeta[0])
+        return dx, None, None, None
+
+
+def dropout_bcast(x: torch.Tensor, rep: int, p: float, group: int = 1) -> torch.Tensor:
+    """Training-mode dropout of x (O, C) broadcast to (O, rep, C) (e.g. one
+    value row per batch expanded over the queries), without the (O, rep, C)
+    copy the expand would need."""
+    if not 0.0 < p < 1.0:
+        raise ValueError(f"dropout_bcast: p must be in (0, 1), got {p}")
+    return BcastDropoutFn.apply(x.reshape(-1, x.shape[-1]), rep, p, group)
 
 
 def dropout(x: torch.Tensor, p: float, training: bool, group: int = 1) -> torch.Tensor:

@@ -13,8 +13,10 @@ on).  Here, with S = sum over the batch of dy (L, d) in fp32:
   * position table: pid = arange(L) -> d_pos[:L] = S; pid = arange(T).repeat(Q)
     -> d_pos[:T] = sum of S's Q blocks; otherwise index_add_;
   * quantizer table (<= 64 rows): onehot(qid)^T @ S;
-  * token table (<= 64 rows, the codec vocabulary): onehot(ids)^T @ dy, one
-    skinny GEMM reading dy once; larger tables: index_add_ (atomic scatter).
+  * token table (<= 16 rows, the codec vocabulary): mtts_embed_table_grad, one
+    HIP pass over dy with the vocabulary's bins in registers (the one-hot GEMM
+    it replaces ran ~91 us per C5 call on hipBLASLt); up to 64 rows
+    onehot(ids)^T @ dy; larger tables: index_add_ (atomic scatter).
 All parameter gradients are fp32 (the master dtype).
 """
 from __future__ import annotations
@@ -25,10 +27,22 @@ import torch.nn.functional as F
 from . import _lib as L
 
 SMALL_VOCAB = 64
+HIP_VOCAB = 16      # mtts_embed_table_grad's register bins
 _err = {}
 
 
 def _table_grad(ids2d, g2d, rows):
+    ids = ids2d.reshape(-1)
+    if (rows <= HIP_VOCAB and ids.dtype == torch.int64 and g2d.dtype in (torch.float32, torch.bfloat16)
+            and g2d.stride(-1) == 1 and g2d.stride(0) % 8 == 0 and g2d.shape[1] % 8 == 0
+            and g2d.data_ptr() % 16 == 0):
+        ids = ids.contiguous()
+        n, d = g2d.shape
+        out = torch.empty(rows, d, device=g2d.device, dtype=torch.float32)
+        ws = torch.empty(L.lib().mtts_embed_table_grad_workspace(n, d, rows), device=g2d.device, dtype=torch.uint8)
+        L.call_raw("mtts_embed_table_grad", ids.data_ptr(), n, g2d.data_ptr(), L.dtype_code(g2d), g2d.stride(0), d,
+                   rows, out.data_ptr(), ws.data_ptr())
+        return out
     if rows <= SMALL_VOCAB:
         oh = F.one_hot(ids2d.reshape(-1), rows).to(g2d.dtype)
         if g2d.dtype == torch.float32:

@@ -149,6 +149,22 @@ def colsum(x2d: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     return out
 
 
+def colsum_groups(x2d: torch.Tensor, rows_per_group: int) -> torch.Tensor:
+    """fp32 column sums of each group of `rows_per_group` consecutive rows:
+    (rows, cols) -> (rows / rows_per_group, cols)."""
+    if x2d.stride(-1) != 1:
+        x2d = x2d.contiguous()
+    rows, cols = x2d.shape
+    if rows % rows_per_group:
+        raise ValueError(f"colsum_groups: rows={rows} not a multiple of {rows_per_group}")
+    out = torch.empty(rows // rows_per_group, cols, device=x2d.device, dtype=torch.float32)
+    wsz = L.lib().mtts_colsum_workspace(rows, cols, rows_per_group)
+    ws = torch.empty(wsz, device=x2d.device, dtype=torch.uint8) if wsz > 0 else None
+    L.call_raw("mtts_colsum", x2d.data_ptr(), L.dtype_code(x2d), rows, cols, x2d.stride(0), rows_per_group,
+               out.data_ptr(), cols, L.ptr(ws))
+    return out
+
+
 # weight gradients with both output dims >= this run on the hand-written TN
 # kernel (mtts_gemm, csrc/gemm.hip: 0.9-1.1 PF/s on the C2 shapes vs 0.6-0.83
 # for the split-K bmm below); the skinny x_proj / dt_proj ones stay on it
@@ -189,9 +205,20 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int = 4, out: torch.Tensor 
         return torch.mm(dy.t(), x, out=out) if out is not None else dy.t() @ x
     big = dy.shape[1] >= HIP_WGRAD_MIN and x.shape[1] >= HIP_WGRAD_MIN
     skinny = G.WGRAD_SKINNY_ON_TN and min(dy.shape[1], x.shape[1]) >= 64 and max(dy.shape[1], x.shape[1]) >= HIP_WGRAD_MIN
-    if ((big or skinny) and G.tn_ok(dy, x)
-            and (out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0))):
+    out_ok = out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0)
+    if (big or skinny) and G.tn_ok(dy, x) and out_ok:
         return G.mm_tn(dy, x, out=out)
+    M64 = M // 64 * 64
+    if (big or skinny) and M64 >= 1024 and M != M64 and out_ok and G.tn_ok(dy[:M64], x[:M64]):
+        # a ragged token count (the style frames, B * T_frame): the < 64 rows
+        # past the last whole K-step by torch, then the 64-row-aligned bulk
+        # accumulated on the TN kernel (beta = 1)
+        tail = torch.mm(dy[M64:].t(), x[M64:], out_dtype=torch.float32)
+        if out is None:
+            out = tail
+        else:
+            out.copy_(tail)
+        return G.mm_tn(dy[:M64], x[:M64], out=out, beta=1.0)
     if splits > 1 and M % splits == 0 and M >= 2048:
         m = M // splits
         part = torch.bmm(dy.reshape(splits, m, -1).transpose(1, 2), x.reshape(splits, m, -1),

@@ -117,6 +117,17 @@ def deferred(enable: bool = True):
             _end_of_backward()
 
 
+def owns(p) -> bool:
+    """True while this backward's engine holds jobs for `p` that it has not
+    announced: queued, or flushed for only some of its row slices (e.g. the
+    q rows of a cross-attention in_proj_weight before the layers' batched K/V
+    rows).  A listener must then wait for the announcement, even if autograd's
+    post-accumulate hook already sees a partial p.grad."""
+    if id(p) in _E.done:
+        return False
+    return id(p) in _E.covered or any(j.param is p for j in _E.jobs)
+
+
 def add_listener(fn):
     """fn(param) is called once per backward when param.grad is complete."""
     _E.listeners.append(fn)

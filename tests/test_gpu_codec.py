@@ -40,6 +40,28 @@ def test_embed_sum_prologue_vs_torch(vocab, out_dtype):
         close(a.grad, b.grad, rtol=1e-5, name=n)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("vocab,n,d", [(10, 40960, 512), (16, 1000, 64), (1, 77, 8), (10, 0, 64)])
+def test_embed_table_grad_kernel(dtype, vocab, n, d):
+    """mtts_embed_table_grad (the codec vocabulary's token-table gradient):
+    per-id row sums of g in fp32 against float64, from a row-strided g; an id
+    outside [0, vocab) adds nothing; two calls are bit-identical."""
+    from mtts.embed import _table_grad
+    g = torch.Generator(device=DEV).manual_seed(n + vocab)
+    ids = torch.randint(0, vocab, (n,), device=DEV, generator=g)
+    if n > 3:
+        ids[3] = vocab          # out of range: skipped (the forward flags it)
+    big = torch.randn(n, d + 8, device=DEV, generator=g).to(dtype)
+    gr = big[:, :d]
+    out = _table_grad(ids, gr, vocab)
+    ref = torch.zeros(vocab, d, dtype=torch.float64, device=DEV)
+    ok = ids < vocab
+    ref.index_add_(0, ids[ok], gr[ok].double())
+    assert out.dtype == torch.float32 and out.shape == (vocab, d)
+    close(out, ref, rtol=1e-5, name="table grad")
+    assert torch.equal(out, _table_grad(ids, gr, vocab))
+
+
 def test_embed_sum_flags_out_of_range_ids():
     from mtts.embed import embed_sum, check_errors
     w = [torch.randn(n, 8, device=DEV) for n in (10, 1, 16)]

@@ -59,6 +59,29 @@ def test_dropout_group_one_draw_per_group():
         DO.apply_mask(torch.ones(64, device=DEV), 0.1, 1, group=6)
 
 
+@pytest.mark.parametrize("dtype,R", [(torch.float32, 37), (torch.bfloat16, 37), (torch.bfloat16, 1090)])
+def test_dropout_broadcast_source_equals_the_expanded_copy(dtype, R):
+    """rep > 1 (ABI 14): x (O, C) read as x[o] for every y[o, r] -- the same
+    output, bit for bit, as dropping the materialised expand; the autograd form's
+    backward sums the masked gradient over each o's rows (fp32)."""
+    from mtts import dropout as DO
+    O, Cn, p, seed = 3, 256, 0.25, 777     # R = 1090: the column sums' ragged > 1024-row groups
+    x = torch.randn(O, Cn, device=DEV).to(dtype)
+    for group in (1, 64):
+        y = DO.apply_mask(x, p, seed, group=group, rep=R)
+        ref = DO.apply_mask(x[:, None, :].expand(O, R, Cn).contiguous(), p, seed, group=group)
+        assert y.shape == (O, R, Cn) and torch.equal(y, ref)
+    with pytest.raises(RuntimeError):
+        DO.apply_mask(torch.randn(4, 6, device=DEV), p, seed, rep=R)      # rows of 6 fp32: not whole 16-byte pieces
+    xg = x.float().requires_grad_(True)
+    torch.manual_seed(3)
+    y = DO.dropout_bcast(xg, R, p, group=64)
+    g = torch.randn_like(y)
+    y.backward(g)
+    keep = (y != 0).float() / (1 - p)
+    close(xg.grad, (g.double() * keep).sum(1), rtol=1e-5, name="dx")
+
+
 def test_dropout_fn_backward_regenerates_the_mask():
     from mtts import dropout as DO
     torch.manual_seed(0)

@@ -516,6 +516,18 @@ def test_colsum(rows, cols, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rpg,groups", [(1090, 3), (2048, 2), (700, 4), (1300, 1)])
+def test_colsum_groups_ragged(dtype, rpg, groups):
+    """Per-group column sums (mtts_colsum rows_per_group): groups of > 1024
+    rows that are not a multiple of 256 (the style frames' per-batch sums)
+    end in a ragged chunk; every group sums exactly its own rows."""
+    from mtts.linear import colsum_groups
+    torch.manual_seed(rpg)
+    x = torch.randn(rpg * groups, 320, device=DEV).to(dtype)
+    close(colsum_groups(x, rpg), x.double().view(groups, rpg, -1).sum(1), rtol=1e-5, name="colsum_groups")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_linear_fn_grads(dtype):
     from mtts.linear import linear
     torch.manual_seed(0)
@@ -737,6 +749,23 @@ def test_wgrad_split_k_matches_fp64():
     wgrad(dy, x, out=big[1024:2048])
     close(big[1024:2048], ref, rtol=1e-5, name="wgrad row slice")
     assert big[:1024].abs().max().item() == 0 and big[2048:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("M", [8720, 1089])
+def test_wgrad_ragged_token_count(M):
+    """A token count that is not a multiple of 64 (the style frames): the
+    aligned bulk on the TN kernel plus the < 64 remainder rows, into a fresh
+    tensor and into a row slice of a larger one."""
+    from mtts.linear import wgrad
+    g = torch.Generator(device="cpu").manual_seed(M)
+    dy = torch.randn(M, 1024, generator=g).to(DEV, torch.bfloat16)
+    x = torch.randn(M, 512, generator=g).to(DEV, torch.bfloat16)
+    ref = dy.double().t() @ x.double()
+    close(wgrad(dy, x), ref, rtol=1e-5, name="wgrad ragged")
+    big = torch.zeros(2048, 512, device=DEV)
+    wgrad(dy, x, out=big[512:1536])
+    close(big[512:1536], ref, rtol=1e-5, name="wgrad ragged row slice")
+    assert big[:512].abs().max().item() == 0 and big[1536:].abs().max().item() == 0
 
 
 @pytest.mark.parametrize("M,N,K", [(32, 4096, 1024), (32, 1024, 2048), (32, 1024, 4096), (32, 96, 2048),
