@@ -135,13 +135,28 @@ class StyleConditioningPipeline(nn.Module):
         self.cross_attn_2 = StyleDecoderCrossAttention(d_model, num_heads, dropout)
         self.length_regulator = LengthRegulator()
 
+    def _gemm_weights(self):
+        ws = []
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                ws += [m.weight, m.bias]
+            elif isinstance(m, CrossAttention):
+                ws += [m.in_proj_weight, m.in_proj_bias]
+        return [w for w in ws if w is not None]
+
     def forward(self, text_hidden, style_emb, durations, text_mask=None, max_frame_len=None):
         if self.compute_dtype is not None:
             text_hidden, style_emb = text_hidden.to(self.compute_dtype), style_emb.to(self.compute_dtype)
-        style_K, style_V = self.style_proj(style_emb)
-        styled_text = self.cross_attn_1(text_hidden, style_K, style_V, text_mask)
-        upsampled, output_lengths = self.length_regulator(styled_text, durations, max_len=max_frame_len)
-        styled_frames = self.cross_attn_2(upsampled, style_K, style_V)
+        # ONE cast scope for the whole pipeline: every GEMM weight cast to the
+        # compute dtype in one launch (with the W^T copies the data gradients
+        # read), valid for this forward and its backward -- per-block scopes
+        # would re-cast each weight at every block entry and again in the
+        # backward (mtts.linear.cast_scope)
+        with cast_scope(self._gemm_weights(), text_hidden.dtype):
+            style_K, style_V = self.style_proj(style_emb)
+            styled_text = self.cross_attn_1(text_hidden, style_K, style_V, text_mask)
+            upsampled, output_lengths = self.length_regulator(styled_text, durations, max_len=max_frame_len)
+            styled_frames = self.cross_attn_2(upsampled, style_K, style_V)
         return styled_frames, output_lengths, style_K, style_V
 
 
