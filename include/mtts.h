@@ -65,7 +65,8 @@ enum {
   MTTS_OVR_ATTN_GENERIC = 7,  /* 1: generic MFMA attention kernels only (no short-key / long-key / q_len-1 kernels) */
   MTTS_OVR_CONV_UNTILED = 8,  /* 1: the untiled causal-conv kernels */
   MTTS_OVR_GEMM_TILE = 9,     /* NT bf16 GEMM: 1 eight-wave ping-pong tile, 2 four-wave 128x128-per-wave tile */
-  MTTS_OVR_COUNT = 10
+  MTTS_OVR_ATTN_DQ_DMA = 10,  /* long-key attention dQ pass (bf16 hd 64): 1 K / V blocks by LDS-DMA, else registers */
+  MTTS_OVR_COUNT = 11
 };
 int mtts_set_override(int key, int value);
 int mtts_get_override(int key);
@@ -759,7 +760,10 @@ int mtts_gemm_skinny(const MttsSkinnyArgs* a, void* stream);
  * (n / (x_rep * x_inner), x_rep, x_inner), x is (n / (x_rep * x_inner),
  * x_inner) and y[o, r, c] drops x[o, c] (x_inner a multiple of 8 / 4; no
  * `pre`, not in place): the single-key attention's value row expanded over
- * the queries without a materialised copy.
+ * the queries without a materialised copy.  `seed_in` (optional, device
+ * int64): added to `seed` -- a base that a captured step advances, so a
+ * replayed hipGraph draws fresh masks; `seed_out` (optional) receives the
+ * base the forward used, for its backward's `seed_in`.
  * ------------------------------------------------------------------------ */
 typedef struct {
   int64_t n;
@@ -773,6 +777,8 @@ typedef struct {
   int x_rep;                 /* ABI 14: > 1 = x broadcast x_rep times over the middle dimension */
   int x_inner;               /* ABI 14: the broadcast rows' length (elements) */
   int reserved_;
+  const int64_t* seed_in;    /* ABI 14, optional: device int64 added to `seed` (graph-replayable base) */
+  int64_t* seed_out;         /* ABI 14, optional: receives *seed_in (the forward's record for its backward) */
 } MttsDropoutArgs;
 
 int mtts_dropout(const MttsDropoutArgs* a, void* stream);

@@ -91,7 +91,8 @@ class GemmArgs(C.Structure):
 
 class DropoutArgs(C.Structure):
     _fields_ = [("n", i64), ("dtype", i32), ("p", f32), ("seed", C.c_uint64), ("x", vp), ("y", vp), ("pre", vp),
-                ("group", i32), ("x_rep", i32), ("x_inner", i32), ("reserved_", i32)]
+                ("group", i32), ("x_rep", i32), ("x_inner", i32), ("reserved_", i32), ("seed_in", vp),
+                ("seed_out", vp)]
 
 
 class RowMap(C.Structure):
@@ -248,7 +249,8 @@ def call_raw(name, *args):
 
 # kernel-path override keys (include/mtts.h MTTS_OVR_*): test / measurement hooks
 OVERRIDES = {"scan_path": 0, "scan_p": 1, "scan_segs": 2, "scan_bwd_segs": 3, "gemm_narrow": 4,
-             "attn_chunks": 5, "attn_bwd": 6, "attn_generic": 7, "conv_untiled": 8, "gemm_tile": 9}
+             "attn_chunks": 5, "attn_bwd": 6, "attn_generic": 7, "conv_untiled": 8, "gemm_tile": 9,
+             "attn_dq_dma": 10}
 SCAN_C1, SCAN_W2, SCAN_NARROW = 1, 2, 3
 ATTN_BWD_FUSED, ATTN_BWD_SPLIT = 1, 2
 

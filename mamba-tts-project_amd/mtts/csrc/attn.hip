@@ -1066,7 +1066,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // block j's MFMAs, one barrier per block.  delta = rowsum(dO * O) is
 // computed once per query and written for the dK/dV pass (mode 1).
 
-template <int HD>
+template <int HD, bool DMA>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   static_assert(HD == 64 || HD == 128, "dq kernel head dims");
   constexpr int KB = 64;
@@ -1078,11 +1078,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdParams p) {
   // block's 64 key-mask bytes), one counted vmcnt + barrier per block; this
   // frees the 16 staging VGPRs of the register-staged form (kept for hd 128,
   // whose three 32 KiB buffers would not leave room for two workgroups)
-  // OFF: the dK / dV form of this staging measured 3 % slower
-  // (profiles/r06_attn_ab_kv_dma.txt); this one also reads the key mask as
-  // dwords, whose per-dword range check drops the last partial dword of a
-  // row (kv_len % 4 != 0) -- byte loads would be needed before enabling it
-  constexpr bool kDqDma = false;
+  // The key mask arrives as dwords, whose per-dword range check drops the
+  // last partial dword of a row: the host takes this form only for
+  // kv_len % 4 == 0 (or no mask) with 4-byte aligned mask rows, and only when
+  // MTTS_OVR_ATTN_DQ_DMA = 1 (the dK / dV form of this staging measured 3 %
+  // slower, profiles/r06_attn_ab_kv_dma.txt; this one: r06_attn_ab_dq_dma.txt)
+  constexpr bool kDqDma = DMA && HD == 64;
   constexpr int NBUF = kDqDma ? 3 : 2;
   __shared__ __attribute__((aligned(16))) bf16_t sK[NBUF][KB * HD];
   __shared__ __attribute__((aligned(16))) bf16_t sV[NBUF][KB * HD];
@@ -1988,8 +1989,13 @@ void launch_bwd(const BwdParams& p, bool split, hipStream_t st) {
   if (split) {
     constexpr int KG = BwdCfg<T, HD>::KG;
     if constexpr (std::is_same<T, bf16_t>::value && (HD == 64 || HD == 128)) {
-      if (span_ok && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1)
-        attn_bwd_dq_kernel<HD><<<dim3((f.q_len + 127) / 128, f.heads, f.batch), 256, 0, st>>>(p);
+      const bool dq_dma = HD == 64 && mtts::override_of(MTTS_OVR_ATTN_DQ_DMA) == 1 &&
+                          (!f.key_padding_mask || (f.kv_len % 4 == 0 && f.mask_bs % 4 == 0 &&
+                                                   (uintptr_t)f.key_padding_mask % 4 == 0));
+      if (span_ok && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1 && dq_dma)
+        attn_bwd_dq_kernel<HD, true><<<dim3((f.q_len + 127) / 128, f.heads, f.batch), 256, 0, st>>>(p);
+      else if (span_ok && mtts::override_of(MTTS_OVR_ATTN_GENERIC) != 1)
+        attn_bwd_dq_kernel<HD, false><<<dim3((f.q_len + 127) / 128, f.heads, f.batch), 256, 0, st>>>(p);
       else
         attn_bwd_kernel<T, HD, kBwdQ><<<dim3((f.q_len + 31) / 32, f.heads, f.batch), NT, 0, st>>>(p);
     } else {

@@ -275,6 +275,29 @@ def test_backward_long_key_side(case, dtype, path):
     close(dkv, rkv, tol)
 
 
+@pytest.mark.parametrize("case,masked", [((2, 64, 776, 4, 64), True), ((2, 160, 300, 8, 64), True),
+                                         ((1, 300, 701, 2, 64), False), ((1, 5120, 5248, 8, 64), True)])
+def test_backward_dq_lds_dma_form(case, masked):
+    """The dQ pass's LDS-DMA staging form (override attn_dq_dma = 1: K / V
+    blocks and the key-mask bytes by buffer_load ... lds into a 3-deep ring,
+    the kimg swizzle undone in the per-lane source offsets) equals the
+    register-staged form bit for bit, where the host takes it (kv_len % 4 == 0
+    with a mask; any kv_len without), and matches float64."""
+    from mtts import _lib as L
+    B, T, S, H, hd = case
+    q, kv, kpm = make(B, T, S, H, hd, torch.bfloat16, seed=7)
+    if not masked:
+        kpm = None
+    with L.override(attn_bwd=L.ATTN_BWD_SPLIT, attn_dq_dma=0):
+        o, dq0, dkv0, do = _grads(q, kv, H, kpm, fused=True)
+    with L.override(attn_bwd=L.ATTN_BWD_SPLIT, attn_dq_dma=1):
+        o1, dq1, dkv1, do1 = _grads(q, kv, H, kpm, fused=True)
+    assert torch.equal(do, do1) and torch.equal(dq0, dq1) and torch.equal(dkv0, dkv1)
+    if T * S <= 300 * 1000:
+        rq, rkv = _ref_grads(q, kv, H, kpm, do)
+        close(dq1, rq, 3e-2)
+
+
 @pytest.mark.parametrize("hd", [128, 64])
 def test_backward_c5_shape_bf16(hd):
     """train.py decoder shape: T_audio = 5120 queries, 5120 reference keys +
