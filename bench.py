@@ -319,17 +319,32 @@ def style_bench(B=8, T_text=128, d_model=1024, d_style=256, iters=20):
     gframes = torch.randn(B, max_len, d_model, device=dev, generator=g).to(torch.bfloat16)
     params = list(pipe.parameters())
 
+    from mtts import dropout as DO
+
     def train_step():
+        DO.advance()             # fresh dropout masks on every (replayed) step
         for prm in params:
             prm.grad = None
         textg.grad = None
         frames, _, _, _ = pipe(textg, style, dur, max_frame_len=max_len)
         frames.backward(gframes)
     train_ms = timed(train_step)
+    # the same step captured once as a hipGraph (~110 launches: the eager
+    # step is partly bound by host launch work)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        train_step()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        train_step()
+    graph_ms = timed(graph.replay)
     return {"B": B, "T_text": T_text, "T_frame": max_len, "d_model": d_model, "dtype": "bf16",
             "regulator": {"ms": reg_ms, "bound": "hbm", "achieved": reg_bytes / reg_ms / 1e6, "peak": HBM_PEAK / 1e9,
                           "unit": "GB/s", "frac": reg_bytes / (reg_ms * 1e-3) / HBM_PEAK},
-            "pipeline_eval_ms": eval_ms, "pipeline_train_fwd_bwd_ms": train_ms}
+            "pipeline_eval_ms": eval_ms, "pipeline_train_fwd_bwd_ms": train_ms,
+            "pipeline_train_fwd_bwd_graph_ms": graph_ms}
 
 
 def c5_step_bench(rank, world, dev, B=8, T_text=128, T_codec=1024, T_ref=1024, steps=3, warmup=2):
@@ -396,7 +411,10 @@ def text_bench(B=8, T_text=128, d_model=512, iters=10):
 
     params = list(enc.parameters()) + list(dur.parameters())
 
+    from mtts import dropout as DO
+
     def step():
+        DO.advance()             # fresh dropout masks on every (replayed) step
         for p in params:
             p.grad = None
         h = enc(ids, mask=mask)
@@ -418,9 +436,10 @@ def text_bench(B=8, T_text=128, d_model=512, iters=10):
             step()
     torch.cuda.current_stream().wait_stream(side)
     eager_ms = clock(step)
-    # the same fwd + bwd (dropout included: its RNG offsets advance per
-    # replay) captured once as a hipGraph: ~400 launches of 2-15 us each, so
-    # an eager step is bound by host launch work on a slow host core
+    # the same fwd + bwd (dropout included: the HIP dropout's device seed
+    # base advances per replay, mtts.dropout.advance) captured once as a
+    # hipGraph: ~400 launches of 2-15 us each, so an eager step is bound by
+    # host launch work on a slow host core
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         step()

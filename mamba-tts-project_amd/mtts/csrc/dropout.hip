@@ -18,6 +18,10 @@
 // (outer, x_rep, x_inner) and x (outer, x_inner), read as x[o, c] for y[o, r, c]:
 // the single-key attention's value row expanded over the queries and dropped in
 // one pass (no materialised (B, Tq, d) copy).
+// seed_in (ABI 14): a device int64 added to the scalar seed (the library's
+// per-device base, advanced once per training step by a captured add, so a
+// replayed hipGraph draws fresh masks); seed_out: the forward records the
+// base it used, and the backward reads it back as its seed_in.
 #include "common.h"
 
 namespace mtts {
@@ -59,8 +63,14 @@ template <typename T, bool DGELU>
 __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                       const bf16_t* __restrict__ pre, int64_t n, uint64_t seed,
                                                       uint32_t thresh, float scale, int group, int x_rep,
-                                                      int x_inner) {
+                                                      int x_inner, const int64_t* __restrict__ seed_in,
+                                                      int64_t* __restrict__ seed_out) {
   constexpr int V = 16 / sizeof(T);   // elements per 16-byte piece
+  if (seed_in) {
+    const int64_t base = *seed_in;
+    if (seed_out && blockIdx.x == 0 && threadIdx.x == 0) *seed_out = base;
+    seed += (uint64_t)base;
+  }
   const int64_t nv = n / V;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t inner_v = x_inner / V, outer_v = (int64_t)x_rep * inner_v;   // in 16-byte pieces
@@ -164,17 +174,17 @@ extern "C" int mtts_dropout(const MttsDropoutArgs* a, void* stream) {
   if (a->dtype == MTTS_F32) {
     if (a->pre)
       hipLaunchKernelGGL((dropout_kernel<float, true>), dim3(blocks), dim3(256), 0, st, (const float*)a->x,
-                         (float*)a->y, (const bf16_t*)a->pre, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner);
+                         (float*)a->y, (const bf16_t*)a->pre, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner, a->seed_in, a->seed_out);
     else
       hipLaunchKernelGGL((dropout_kernel<float, false>), dim3(blocks), dim3(256), 0, st, (const float*)a->x,
-                         (float*)a->y, nullptr, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner);
+                         (float*)a->y, nullptr, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner, a->seed_in, a->seed_out);
   } else {
     if (a->pre)
       hipLaunchKernelGGL((dropout_kernel<bf16_t, true>), dim3(blocks), dim3(256), 0, st, (const bf16_t*)a->x,
-                         (bf16_t*)a->y, (const bf16_t*)a->pre, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner);
+                         (bf16_t*)a->y, (const bf16_t*)a->pre, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner, a->seed_in, a->seed_out);
     else
       hipLaunchKernelGGL((dropout_kernel<bf16_t, false>), dim3(blocks), dim3(256), 0, st, (const bf16_t*)a->x,
-                         (bf16_t*)a->y, nullptr, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner);
+                         (bf16_t*)a->y, nullptr, a->n, a->seed, thresh, scale, group, x_rep, a->x_inner, a->seed_in, a->seed_out);
   }
   MTTS_LAUNCH_CHECK("dropout");
   return MTTS_OK;

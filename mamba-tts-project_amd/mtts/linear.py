@@ -335,7 +335,8 @@ class FFNFn(torch.autograd.Function):
         ctx.p, ctx.seed = p, None
         if p > 0.0:
             ctx.seed = DO.new_seed()
-            a = DO.apply_mask(a, p, ctx.seed)
+            base, ctx.used = DO._slot(a)
+            a = DO.apply_mask(a, p, ctx.seed, seed_in=base, seed_out=ctx.used)
         y = proj(a, W2, B2)
         ctx.save_for_backward(h2, pre, a, W1, W2)
         ctx.ws = (w1, w2)
@@ -353,7 +354,7 @@ class FFNFn(torch.autograd.Function):
         W2t = cast_weight_t(w2, W2.dtype) if _want_t(w2) else W2.t().contiguous()
         if ctx.p > 0.0:
             from . import dropout as DO
-            dpre = DO.apply_mask(G.mm_nt(dy2, W2t), ctx.p, ctx.seed, pre=pre)
+            dpre = DO.apply_mask(G.mm_nt(dy2, W2t), ctx.p, ctx.seed, pre=pre, seed_in=ctx.used)
         else:
             dpre = G.mm_nt(dy2, W2t, dgelu_aux=pre)
         dh = None

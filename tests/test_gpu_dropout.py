@@ -98,6 +98,53 @@ def test_dropout_fn_backward_regenerates_the_mask():
     assert z.grad.shape == z.shape
 
 
+def test_dropout_in_a_replayed_graph_draws_fresh_masks():
+    """A training step captured in a hipGraph (CPU seeds frozen at capture)
+    draws a new mask on every replay when it advances the device seed base
+    (mtts.dropout.advance, captured); the backward of each replay uses its
+    own forward's mask (the base recorded per call), also when the base moves
+    between a forward and its backward (eager)."""
+    from mtts import dropout as DO
+    base = DO.device_base(DEV)
+    try:
+        torch.manual_seed(0)
+        x = torch.randn(4096, 64, device=DEV, requires_grad=True)
+        g = torch.randn(4096, 64, device=DEV)
+        static = {}
+
+        def step():
+            DO.advance()
+            x.grad = None
+            y = DO.dropout(x, 0.3, True)
+            y.backward(g)
+            static["y"], static["dx"] = y.detach(), x.grad
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        masks = []
+        for _ in range(3):
+            graph.replay()
+            torch.cuda.synchronize()
+            keep = static["y"] != 0
+            masks.append(keep.clone())
+            close(static["dx"], g * keep / 0.7, rtol=1e-6, name="dx of the same replay")
+        assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+        # eager: the base moves between forward and backward -- the backward keeps the forward's mask
+        x.grad = None
+        y = DO.dropout(x, 0.3, True)
+        DO.advance()
+        y.backward(g)
+        close(x.grad, g * (y != 0) / 0.7, rtol=1e-6, name="dx after advance")
+    finally:
+        base.zero_()
+
+
 def test_dropout_dgelu_form():
     """dropout(gelu(pre)) backward in one pass: bf16(bf16(dy * keep / (1 - p)) * gelu'(pre))."""
     from mtts import dropout as DO
