@@ -80,11 +80,31 @@ class DkvSink:
         self.rows, self.L, self.width, self.shape = rows, n_layers, width, shape
         self.device, self.dtype = device, dtype
         self.buf = None
+        self.key2 = None                   # the (M, d) key rows the projections read (set by KVAllFn)
+        self.written = [False] * n_layers  # the layer's dK / dV landed (attention backward)
+        self.taken = [False] * n_layers    # its weight / bias gradients were produced by the q projection
 
     def view(self, layer):
         if self.buf is None:
             self.buf = torch.empty(self.rows, self.L * self.width, device=self.device, dtype=self.dtype)
+        self.written[layer] = True
         return self.buf[:, layer * self.width:(layer + 1) * self.width].view(*self.shape, self.width)
+
+    def partner(self, layer):
+        """For the layer's q projection (linear(..., partner=)): hands over the
+        layer's K/V gradient rows d:3d of in_proj once its attention backward
+        has written them."""
+        sink = self
+
+        class _P:
+            @staticmethod
+            def take():
+                if not sink.written[layer] or sink.buf is None or sink.key2 is None:
+                    return None
+                sink.taken[layer] = True
+                d = sink.width // 2
+                return (sink.buf[:, layer * sink.width:(layer + 1) * sink.width], sink.key2, (d, 3 * d))
+        return _P()
 
 
 class KVAllFn(torch.autograd.Function):
@@ -97,8 +117,10 @@ class KVAllFn(torch.autograd.Function):
     that product; the backward takes the L K/V gradients as one operand (the
     attention backward writes them into a DkvSink) for ONE key gradient GEMM
     (K = L*2d: the sum over layers inside the reduction, no autograd adds of
-    L (B, T_kv, d) gradients), the layers' weight gradients (row slices d:3d,
-    deferred like the rest, mtts.wgrad) and one bias column sum."""
+    L (B, T_kv, d) gradients).  Each layer's K/V weight / bias gradient rows
+    d:3d are produced by that layer's q projection together with its own rows
+    0:d (LinearFn `partner`): one submit to the grouped engine per layer (in
+    that layer's launch), one bias tensor, no zero fills or adds."""
 
     @staticmethod
     def forward(ctx, key, sink, *params):
@@ -111,6 +133,7 @@ class KVAllFn(torch.autograd.Function):
         kv = proj(k2, Wst, bst)                                           # (M, L*2d)
         ctx.save_for_backward(k2)
         ctx.Ws, ctx.bs, ctx.kshape, ctx.sink = Ws, bs, key.shape, sink
+        sink.key2 = k2
         return tuple(kv[:, l * 2 * d:(l + 1) * 2 * d].view(*key.shape[:-1], 2 * d) for l in range(len(Ws)))
 
     @staticmethod
@@ -139,18 +162,22 @@ class KVAllFn(torch.autograd.Function):
             else:
                 dkey = (dkv @ torch.cat([cast_weight(W, cd)[d:] for W in Ws])).view(ctx.kshape)
         grads = [dkey, None]
-        cs = colsum(dkv) if any(ctx.needs_input_grad[3::2]) else None
+        # the layers' weight / bias gradients were produced by each layer's q
+        # projection (LinearFn partner); only a layer whose q projection did
+        # not take them is handled here
         for l in range(nl):
             W, b = Ws[l], bs[l]
-            dy = dkv[:, l * w2:(l + 1) * w2]
             dW = db = None
-            if ctx.needs_input_grad[2 + 2 * l] and not WG.submit([(dy, k2, W, (d, 3 * d))]):
-                dW = torch.zeros(W.shape, device=W.device, dtype=W.dtype)
-                dW[d:] = wgrad(dy.contiguous(), k2).to(W.dtype)
-            if ctx.needs_input_grad[3 + 2 * l]:
-                db = torch.zeros(b.shape, device=b.device, dtype=b.dtype)
-                db[d:] = cs[l * w2:(l + 1) * w2].to(b.dtype)
+            if not sink.taken[l]:
+                dy = dkv[:, l * w2:(l + 1) * w2]
+                if ctx.needs_input_grad[2 + 2 * l] and not WG.submit([(dy, k2, W, (d, 3 * d))]):
+                    dW = torch.zeros(W.shape, device=W.device, dtype=W.dtype)
+                    dW[d:] = wgrad(dy.contiguous(), k2).to(W.dtype)
+                if ctx.needs_input_grad[3 + 2 * l]:
+                    db = torch.zeros(b.shape, device=b.device, dtype=b.dtype)
+                    db[d:] = colsum(dy).to(b.dtype)
             grads += [dW, db]
+        sink.key2 = None
         return tuple(grads)
 
 
@@ -230,7 +257,8 @@ class CrossAttention(nn.Module):
         W, b = self.in_proj_weight, self.in_proj_bias
         p_drop = self.dropout if self.training else 0.0
         if kv_pre is not None:
-            q = linear(query, W, b, rows=(0, d))
+            sk = getattr(kv_pre, "_mtts_dkv_sink", None)
+            q = linear(query, W, b, rows=(0, d), partner=None if sk is None else sk[0].partner(sk[1]))
             o = attn_kernels.attention_kv(q, kv_pre, H, key_padding_mask, p_drop)
             return linear(o, self.out_proj.weight, self.out_proj.bias, dbias_slot=dbias_slot), None
         if key.shape[1] == 1 and key_padding_mask is None:

@@ -251,9 +251,10 @@ class LinearFn(torch.autograd.Function):
     full weight/bias (zero outside [r0, r1) when a row slice is used)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, r0, r1, slot=None):
+    def forward(ctx, x, weight, bias, r0, r1, slot=None, partner=None):
         cd = x.dtype
         ctx.slot = slot
+        ctx.partner = partner
         w = cast_weight(weight, cd)
         if r0 is not None:
             w = w[r0:r1]
@@ -286,6 +287,34 @@ class LinearFn(torch.autograd.Function):
             else:
                 dx = (dy2 @ w).view(xshape)
         dW = db = None
+        rest = ctx.partner.take() if ctx.partner is not None else None
+        if rest is not None and r0 is not None:
+            # this projection also owns the parameter's other rows (rest: the
+            # layer's K/V rows of in_proj, attention.KVAllFn): ONE submit and
+            # ONE bias tensor for the whole parameter -- no zero fills, copies
+            # or autograd adds, and the weight gradient stays in this layer's
+            # grouped launch
+            dyr, xr, (q0, q1) = rest
+            if ctx.needs_input_grad[1] and not WG.submit([(dy2, x2, ctx.weight, (r0, r1)),
+                                                          (dyr, xr, ctx.weight, (q0, q1))]):
+                dW = torch.empty(wshape, device=dy2.device, dtype=torch.float32)
+                wgrad(dy2, x2, out=dW[r0:r1])
+                wgrad(dyr.contiguous(), xr, out=dW[q0:q1])
+                if r1 - r0 + q1 - q0 < wshape[0]:
+                    for a, b in ((0, min(r0, q0)), (max(r1, q1), wshape[0])):
+                        if b > a:
+                            dW[a:b].zero_()
+                dW = dW.to(wdt)
+            if bdt is not None and ctx.needs_input_grad[2]:
+                db = torch.empty(wshape[0], device=dy2.device, dtype=torch.float32)
+                colsum(dy2, out=db[r0:r1])
+                colsum(dyr, out=db[q0:q1])
+                if r1 - r0 + q1 - q0 < wshape[0]:
+                    for a, b in ((0, min(r0, q0)), (max(r1, q1), wshape[0])):
+                        if b > a:
+                            db[a:b].zero_()
+                db = db.to(bdt)
+            return dx, dW, db, None, None, None, None
         if ctx.needs_input_grad[1] and not WG.submit([(dy2, x2, ctx.weight, None if r0 is None else (r0, r1))]):
             g = wgrad(dy2, x2).to(wdt)
             if r0 is not None:
@@ -301,15 +330,18 @@ class LinearFn(torch.autograd.Function):
                 full[r0:r1] = gb
                 gb = full
             db = gb
-        return dx, dW, db, None, None, None
+        return dx, dW, db, None, None, None, None
 
 
-def linear(x, weight, bias=None, rows=None, dbias_slot=None):
+def linear(x, weight, bias=None, rows=None, dbias_slot=None, partner=None):
     """Functional form; `rows=(r0, r1)` selects a row slice of weight/bias;
     `dbias_slot` (BiasGradSlot): the bias gradient arrives from the consumer's
-    backward (the caller guarantees the output feeds only that consumer)."""
+    backward (the caller guarantees the output feeds only that consumer);
+    `partner.take()` -> (dy, x, (q0, q1)) or None: the gradient operands of
+    the same parameter's other rows, whose weight / bias gradients this
+    backward then produces together with its own."""
     r0, r1 = (None, None) if rows is None else rows
-    return LinearFn.apply(x, weight, bias, r0, r1, dbias_slot)
+    return LinearFn.apply(x, weight, bias, r0, r1, dbias_slot, partner)
 
 
 class FFNFn(torch.autograd.Function):

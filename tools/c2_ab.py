@@ -19,6 +19,8 @@ try:   # the deferred grouped weight gradients (round 5); DEFER=0 turns them off
     from mtts import wgrad as _wg  # noqa: E402
     defer = lambda: _wg.deferred(os.environ.get("DEFER", "1") == "1")  # noqa: E731
     _wg.SIDE_STREAM = os.environ.get("SIDE", "1") == "1"
+    if hasattr(_wg, "FUSE_BIAS"):
+        _wg.FUSE_BIAS = os.environ.get("FUSE", "1") == "1"
 except ImportError:
     import contextlib  # noqa: E402
     defer = contextlib.nullcontext
