@@ -4,7 +4,8 @@ python tools/bench_ln.py"""
 import os
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "mamba-tts-project_amd")]
+# AB_ROOT: another package tree (tools/ab/base) for a same-box A/B
+sys.path[:0] = [ROOT, os.path.join(os.environ.get("AB_ROOT", ROOT), "mamba-tts-project_amd")]
 import torch  # noqa: E402
 from mtts import ops  # noqa: E402
 
