@@ -177,7 +177,9 @@ class KVAllFn(torch.autograd.Function):
                     db = torch.zeros(b.shape, device=b.device, dtype=b.dtype)
                     db[d:] = colsum(dy).to(b.dtype)
             grads += [dW, db]
-        sink.key2 = None
+        # ready for another backward through the same graph (retain_graph)
+        sink.written = [False] * nl
+        sink.taken = [False] * nl
         return tuple(grads)
 
 

@@ -60,3 +60,26 @@ def test_decoder_kv_all_equals_per_layer_projections(cd, deferred, monkeypatch):
     assert set(new[2]) == set(ref[2])
     for n in ref[2]:
         close(new[2][n], ref[2][n], rtol=tol, name=n)
+
+
+def test_kv_all_backward_twice_through_a_retained_graph():
+    """retain_graph: a second backward through the same forward (the K/V sink
+    re-armed) adds exactly the first backward's gradients again."""
+    import mamba_decoder
+    torch.manual_seed(1)
+    d, B, T, Tt = 256, 2, 128, 64
+    model = mamba_decoder.MambaTTSDecoder(12, d_model=d, n_layers=2, n_heads=4, d_ff=512, d_style=64).to(DEV)
+    model.compute_dtype = torch.bfloat16
+    tokens = torch.randint(0, 12, (B, T), device=DEV)
+    text = torch.randn(B, Tt, d, device=DEV, requires_grad=True)
+    z = torch.randn(B, 64, device=DEV)
+    out = model(tokens, text, z)
+    gy = torch.randn(out.shape, device=DEV).to(out.dtype)
+    out.backward(gy, retain_graph=True)
+    once = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    t1 = text.grad.clone()
+    out.backward(gy)
+    for n, p in model.named_parameters():
+        if n in once:
+            close(p.grad, 2 * once[n], rtol=1e-5, name=n)
+    close(text.grad, 2 * t1, rtol=1e-2, name="d text_hidden")
