@@ -108,6 +108,28 @@ def probes(dev):
     def gemm():
         return [G.mm_nt(a1, w1), G.mm_tn(dyy, xx)]
     out["gemm nt/tn"] = gemm
+    # round-6 kernels: dropout forms, the codec token-table gradient, ragged
+    # per-group column sums, the grouped TN weight-gradient launch
+    from mtts import dropout as DO
+    from mtts import wgrad as WG
+    from mtts.embed import _table_grad
+    from mtts.linear import colsum_groups
+    xd, v8 = r(8 * 1090, 1024), r(8, 1024)
+    dpre, pre = r(8 * 1090, 4096), r(8 * 1090, 4096)
+    out["dropout (plain, group, broadcast, dgelu)"] = lambda: [
+        DO.apply_mask(xd, 0.1, 77), DO.apply_mask(xd, 0.1, 77, group=128),
+        DO.apply_mask(v8, 0.1, 77, group=128, rep=1090), DO.apply_mask(dpre, 0.1, 77, pre=pre)]
+    ids = torch.randint(0, 10, (40960,), generator=g).to(dev)
+    gt = r(40960, 512)
+    out["embed token-table grad (V = 10)"] = lambda: [_table_grad(ids, gt, 10)]
+    out["colsum groups (ragged 1090-row groups)"] = lambda: [colsum_groups(xd, 1090)]
+    dyA, xA, dyB = r(16384, 1024), r(16384, 1024), r(16384, 4096)
+
+    def grouped():
+        outs = [torch.empty(1024, 1024, device=dev), torch.empty(4096, 1024, device=dev)]
+        WG._launch([(dyB, xA, outs[1], 0.0), (dyA, xA, outs[0], 0.0)])
+        return outs
+    out["grouped tn (2 problems)"] = grouped
     return out
 
 
