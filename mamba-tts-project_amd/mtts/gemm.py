@@ -122,9 +122,10 @@ SKINNY = True   # routing switch (in-process A/B: tools/skinny_ab.py)
 SKINNY_TN_KERNEL = True  # x_proj / dt_proj weight gradients on the SKINNY_TN kernel (mamba.py; skinny_tn_ok)
 WGRAD_SKINNY_ON_TN = False  # linear.wgrad: skinny weight gradients on the big TN kernel (35.5 vs 33.7 us: off)
 # x_proj forward on SKINNY_N: round 3 measured 25 vs 21 us for hipBLASLt, round 5
-# 24.5-25.8 vs 24.2 us (profiles/r05_skinny_n_*_ab.txt): on par, so the
-# hand-written kernel is the default (no vendor GEMM left on the Mamba path)
-SKINNY_XPROJ = True
+# 24.5-25.8 vs 24.2 us (profiles/r05_skinny_n_*_ab.txt), round 6 25.6 vs 19.9 us
+# per call and C2 steps 33.63 / 33.71 / 33.55 vs 33.47 / 33.61 / 33.53 ms
+# (profiles/r06_skinny_xproj_ab.txt): hipBLASLt stays the x_proj forward
+SKINNY_XPROJ = False
 
 
 def _skinny_operand(t):
