@@ -126,6 +126,12 @@ WGRAD_SKINNY_ON_TN = False  # linear.wgrad: skinny weight gradients on the big T
 # per call and C2 steps 33.63 / 33.71 / 33.55 vs 33.47 / 33.61 / 33.53 ms
 # (profiles/r06_skinny_xproj_ab.txt): hipBLASLt stays the x_proj forward
 SKINNY_XPROJ = False
+# dt_proj forward and the x_proj data gradient (du += d(x_dbl) W_x) on the
+# skinny kernels (SMALL_K); per call 22.9 / 37.3 us vs 21.5 / 31.7 for
+# hipBLASLt in round 6 (tools/skinny_ab.py ops), but C2 steps equal either
+# way (32.68-32.72 vs 32.69-32.75 ms, profiles/r06_skinny_xproj_ab.txt): kept
+SKINNY_DTPROJ = True
+SKINNY_DU = True
 
 
 def _skinny_operand(t):

@@ -54,7 +54,8 @@ class MambaInnerFn(torch.autograd.Function):
             *u.shape[:-1], r + 2 * N)
         dt, Bm, Cm = x_dbl[..., :r], x_dbl[..., r:r + N], x_dbl[..., r + N:]
         dt2 = x_dbl.view(-1, r + 2 * N)[:, :r]
-        delta = (G.mm_skinny(dt2, Wdt) if G.skinny_ok(dt2, Wdt) else dt2 @ Wdt.t()).view(*u.shape[:-1], di)
+        delta = (G.mm_skinny(dt2, Wdt) if G.SKINNY_DTPROJ and G.skinny_ok(dt2, Wdt) else dt2 @ Wdt.t()).view(
+            *u.shape[:-1], di)
         # A = -exp(A_log) is formed inside the scan kernels (a_is_log): no per-layer exp / neg launches
         A_log32 = A_log.detach().float().contiguous()
         need = any(ctx.needs_input_grad)
@@ -105,7 +106,7 @@ class MambaInnerFn(torch.autograd.Function):
         gx = dx_dbl.to(cd).view(-1, r + 2 * N)
         du2 = du.view(-1, di)
         WxT = cast_weight_t(W_x, cd) if cd == torch.bfloat16 else None     # (di, r + 2N): k-contiguous
-        if WxT is not None and G.skinny_ok(gx, WxT, out=du2):
+        if WxT is not None and G.SKINNY_DU and G.skinny_ok(gx, WxT, out=du2):
             G.mm_skinny(gx, WxT, out=du2, beta=1.0)
         else:
             du2.addmm_(gx, Wx)

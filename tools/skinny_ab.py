@@ -93,10 +93,12 @@ if __name__ == "__main__":
     op_bench()
     if len(sys.argv) > 1 and sys.argv[1] == "ops":
         sys.exit(0)
-    res = {"skinny": [], "skinny+xproj": [], "off": []}
+    res = {"skinny": [], "skinny+xproj": [], "skinny-du": [], "skinny-du-dtproj": [], "off": []}
     for _ in range(3):
         for kind in res:
             G.SKINNY = kind != "off"
             G.SKINNY_XPROJ = kind == "skinny+xproj"
+            G.SKINNY_DU = kind not in ("skinny-du", "skinny-du-dtproj")
+            G.SKINNY_DTPROJ = kind != "skinny-du-dtproj"
             res[kind].append(timeit())
     print({k: [round(x, 2) for x in v] for k, v in res.items()}, flush=True)
