@@ -15,10 +15,10 @@ import mamba_decoder  # noqa: E402
 assert mamba_decoder.__file__.startswith(PKG), (mamba_decoder.__file__, PKG)
 from mtts.loss import cross_entropy  # noqa: E402
 from mtts.optim import FusedClipAdam  # noqa: E402
-try:   # the deferred grouped weight gradients (round 5); DEFER=0 turns them off, SIDE=0 the side stream
+try:   # the deferred grouped weight gradients (round 5); DEFER=0 turns them off, SIDE=1 the side stream on
     from mtts import wgrad as _wg  # noqa: E402
     defer = lambda: _wg.deferred(os.environ.get("DEFER", "1") == "1")  # noqa: E731
-    _wg.SIDE_STREAM = os.environ.get("SIDE", "1") == "1"
+    _wg.SIDE_STREAM = os.environ.get("SIDE", "0") == "1"   # product default: off (unsafe, wgrad.py)
     if hasattr(_wg, "FUSE_BIAS"):
         _wg.FUSE_BIAS = os.environ.get("FUSE", "1") == "1"
 except ImportError:

@@ -3,7 +3,9 @@ processes run the same probe on cuda:0 at once; each op is run REPS times on
 fixed inputs and compared bit for bit with its first result.  A kernel with an
 intra-workgroup race (LDS read before its write is visible, a missing wait)
 shows up as mismatches when other work shares its CUs.
-  NPROC=2 python tools/dbg/race_probe.py"""
+  NPROC=2 python tools/dbg/race_probe.py
+BG=1 ONLY0=<probe> ONLY1=<other probes>: process 1 runs its probes back to back
+(unchecked) for as long as process 0 checks its own."""
 import os
 import sys
 
@@ -23,7 +25,6 @@ def probes(dev):
     bf = torch.bfloat16
     r = lambda *s, sc=1.0, dt=bf: (torch.randn(*s, generator=g) * sc).to(dev, dt)  # noqa: E731
     out = {}
-    only = os.environ.get("ONLY")
     for (B, T, S, d, H) in [(2, 512, 64, 256, 4), (8, 2048, 128, 1024, 8)]:
         q, kv, dout = r(B, T, d), r(B, S, 2 * d), r(B, T, d)
         kpm = torch.zeros(B, S, dtype=torch.bool, device=dev)
@@ -76,19 +77,28 @@ def probes(dev):
     from mtts import _lib as LL
     nws = LL.lib().mtts_selective_scan_bwd_workspace(B, D, L, 16)
     nblk = D // 64
-    nslab, K6 = B * nblk * L * 32, 6
+    nslab = B * nblk * L * 32
 
-    def scan_bwd_ws():
-        ws = torch.zeros(nws, device=dev, dtype=torch.uint8)
-        gr = ops.scan_bwd(u, dl, A, Bm, Cm, Dp, z, bias, True, None, ck0, dy, workspace=ws)
+    K6 = ((nws - 256) // 4 - B * nblk * L * 32) // (B * D * 35)   # segments of the backward's plan
+
+    def scan_bwd_ws(u, dl, Bm, Cm, z, ck, dy):
+        # workspace poisoned with NaN (0xFF bytes): an entry the kernels did not
+        # write this call stays NaN (bitwise compare: equal when unwritten in
+        # both runs); the call's du, ddelta, dB and reduced dA / dD / dbias too
+        ws = torch.full((nws,), 255, device=dev, dtype=torch.uint8)
+        gr = ops.scan_bwd(u, dl, A, Bm, Cm, Dp, z, bias, True, None, ck, dy, workspace=ws)
         f = ws[:(nws // 4) * 4].view(torch.float32)
         npar = B * K6 * D * 18
-        return [f[:nslab], f[nslab:nslab + npar], f[nslab + npar:nslab + npar + B * K6 * D * 17], gr[0]]
-    out["scan bwd C2 workspace (slab, par, seg, du)"] = scan_bwd_ws
+        return [f[:nslab], f[nslab:nslab + npar], f[nslab + npar:nslab + npar + B * K6 * D * 17], gr[0], gr[1],
+                gr[3]] + [t for t in gr[5:8] if t is not None]
+    out["scan bwd C2 workspace (slab, par, seg, du, ddelta, dB, dA, dD, dbias)"] = \
+        lambda: scan_bwd_ws(u, dl, Bm, Cm, z, ck0, dy)
     u32, dl32, z32, dy32 = (t.float() for t in (u, dl, z, dy))
     ck32 = ops.scan_fwd(u32, dl32, A, Bm.float(), Cm.float(), Dp, z32, bias, True, want_ckpt=True)[2]
     out["scan bwd C2 fp32"] = lambda: [t for t in ops.scan_bwd(u32, dl32, A, Bm.float(), Cm.float(), Dp, z32, bias, True,
                                                                 None, ck32, dy32) if t is not None]
+    out["scan bwd C2 fp32 workspace (slab, par, seg, du, ddelta, dB, dA, dD, dbias)"] = \
+        lambda: scan_bwd_ws(u32, dl32, Bm.float(), Cm.float(), z32, ck32, dy32)
     r_ = 32 if D >= 1024 else 16
     dd2, dt2 = r(B * L, D), r(B * L, r_)
     gx, u2 = r(B * L, r_ + 32), r(B * L, D)
@@ -133,36 +143,86 @@ def probes(dev):
     return out
 
 
-def worker(rank, q):
+def bits(t):
+    """bit patterns of a float tensor (NaN == NaN when the bits agree)"""
+    if not t.is_floating_point():
+        return t
+    return t.view({4: torch.int32, 2: torch.int16}[t.element_size()])
+
+
+def background(rank, ps, only, go, done):
+    """BG=1, rank > 0: run this process's probes back to back (no checks) until
+    rank 0 has finished, so one chosen kernel mix keeps running beside it"""
+    import time
+    if only and only.startswith("ubench:"):
+        # one aggressor kernel class of tools/ubench/aggressor.hip instead of a probe
+        import ctypes
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "ubench", "aggressor.so"))
+        mode = int(only.split(":")[1])
+        buf = torch.zeros(4096, device="cuda")
+
+        def agg():
+            st = torch.cuda.current_stream().cuda_stream
+            rc = lib.aggress(mode, 1024, 50000, ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(st))
+            assert rc == 0, rc
+        fns = [agg]
+    else:
+        fns = [fn for name, fn in ps.items() if not only or any(o in name for o in only.split(","))]
+    n, t0 = 0, time.time()
+    while not done.is_set() and time.time() - t0 < 300:
+        for fn in fns:
+            fn()
+        n += 1
+        if n == 2:
+            go.set()
+        torch.cuda.synchronize()
+    go.set()
+    print(f"[proc {rank}] background: {n} rounds of {len(fns)} probes", flush=True)
+
+
+def worker(rank, q, go, done):
     torch.cuda.set_device(0)
     ps = probes("cuda")
     res = {}
-    only = os.environ.get("ONLY")
+    # ONLY<rank> / REPS<rank>: this process's own filter and count (e.g. proc 1
+    # keeps one other kernel running beside proc 0's probe)
+    only = os.environ.get(f"ONLY{rank}", os.environ.get("ONLY"))
+    reps = int(os.environ.get(f"REPS{rank}", REPS))
+    bg = os.environ.get("BG") == "1"
+    if bg and rank > 0:
+        background(rank, ps, only, go, done)
+        q.put({})
+        return
+    if bg:
+        go.wait(300)
     for name, fn in ps.items():
         if only and not any(o in name for o in only.split(",")):
             continue
         ref = [t.clone() if t is not None else None for t in fn()]
         bad = 0
         which = {}
-        for _ in range(REPS):
+        for _ in range(reps):
             got = fn()
             diff = False
             for i, (a, b) in enumerate(zip(got, ref)):
-                if a is None or torch.equal(a, b):
+                if a is None or torch.equal(bits(a), bits(b)):
                     continue
                 diff = True
-                ne = (a != b) & ~(torch.isnan(a) & torch.isnan(b))
+                ne = bits(a) != bits(b)
                 idx = ne.nonzero()
                 w = which.setdefault(i, [0, 0, None, tuple(a.shape)])
                 w[0] += 1
                 w[1] = max(w[1], int(ne.sum()))
                 if w[2] is None and len(idx):
-                    w[2] = (idx[0].tolist(), idx[-1].tolist(), float((a.float() - b.float()).abs().max()))
+                    w[2] = (idx[0].tolist(), idx[-1].tolist(), float((a.float() - b.float()).abs().max()),
+                            int(torch.isnan(a[ne]).sum()), int(torch.isnan(b[ne]).sum()))
             bad += diff
         torch.cuda.synchronize()
         res[name] = bad
-        print(f"[proc {rank}] {name}: {bad}/{REPS} runs differ; per output (runs, max #elements, first/last index, "
+        print(f"[proc {rank}] {name}: {bad}/{reps} runs differ; per output (runs, max #elements, first/last index, "
               f"max |diff|, shape): {which}", flush=True)
+    if rank == 0:
+        done.set()
     q.put(res)
 
 
@@ -170,7 +230,8 @@ if __name__ == "__main__":
     n = int(os.environ.get("NPROC", "2"))
     ctx = mp.get_context("spawn")
     qq = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(i, qq)) for i in range(n)]
+    go, done = ctx.Event(), ctx.Event()
+    ps = [ctx.Process(target=worker, args=(i, qq, go, done)) for i in range(n)]
     for p in ps:
         p.start()
     for _ in range(n):
