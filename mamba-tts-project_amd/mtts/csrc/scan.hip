@@ -1048,6 +1048,16 @@ __device__ __forceinline__ void wave_reduce_scatter32(float (&v)[32], float& o0,
   }
 }
 
+// kPackedHazard (round 6, profiles/r06_race_bg.txt): in the two backward
+// kernels, a few packed-f32 ops (v_pk_mul_f32 / v_pk_fma_f32) gave results
+// that changed from run to run whenever another kernel's MFMA waves shared
+// the SIMD (another process's skinny TN GEMM or attention, or a bare MFMA
+// loop: tools/ubench/aggressor.hip) -- the carry pass's adjoint update and its
+// exp argument, the main pass's dA accumulation, all with an operand
+// broadcast from the per-wave dt / dy table.  Those few are plain ops
+// (an empty asm keeps the SLP vectorizer from re-packing them): 0 of 200
+// mismatching runs under every aggressor, 0.500 -> 0.524 ms per C2 backward.
+// Building the kernels with no packed f32 at all also fixes it, at 3.5x.
 // Backward pass 1 (only when L is split into K > 1 segments): for segments
 // k = 1..K-1, run the adjoint recurrence  dh_t = dy_t C_t + exp(dt_{t+1} A) dh_{t+1}
 // from zero carry-in at the segment end and record the carry leaving the
@@ -1216,10 +1226,15 @@ __global__ __launch_bounds__(kBlock, 4) void scan_bwd_carry_kernel(const MttsSca
         const f4 Cq = *reinterpret_cast<const f4*>(&sC[buf][(g * kPB + s) * kN + j * kNSB]);
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-          const f2 x = f2{dts, dts} * A2v[p];
+          float x0 = dts * A2v[p][0], x1 = dts * A2v[p][1];
+          asm volatile("" : "+v"(x0), "+v"(x1));   // plain ops, not re-packed (kPackedHazard)
+          const f2 x = {x0, x1};
           const f2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
           const f2 cv = p ? f2{Cq[2], Cq[3]} : f2{Cq[0], Cq[1]};
-          carry2[p] = e * __builtin_elementwise_fma(f2{dys, dys}, cv, carry2[p]);
+          float g0 = fmaf(dys, cv[0], carry2[p][0]) * e[0];
+          float g1 = fmaf(dys, cv[1], carry2[p][1]) * e[1];
+          asm volatile("" : "+v"(g0), "+v"(g1));   // plain ops, not re-packed (kPackedHazard)
+          carry2[p] = f2{g0, g1};
         }
       }
 #pragma unroll
@@ -1541,7 +1556,13 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
           const f2 t1 = dh * e * hp;
           ddtA = __builtin_elementwise_fma(Anv[p], t1, ddtA);
           dus = __builtin_elementwise_fma(dh, bv, dus);
-          dA2[p] = __builtin_elementwise_fma(t1, dts2, dA2[p]);
+          {   // plain ops, not re-packed (kPackedHazard)
+            float a0 = dA2[p][0], a1 = dA2[p][1];
+            a0 = fmaf(t1[0], dts, a0);
+            a1 = fmaf(t1[1], dts, a1);
+            asm volatile("" : "+v"(a0), "+v"(a1));
+            dA2[p] = f2{a0, a1};
+          }
           vB[p] = dh * dtus2;           // dB contribution (0 on lanes past `dim`)
           vC[p] = dys2 * hh[tl][p];     // dC contribution
           carry2[p] = e * dh;

@@ -5,12 +5,12 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r6nopk
+O=$R/gpurun_out/${OUTD:-r6nopk}
 mkdir -p $O
 cd $R
 timeout -k 10 300 python -u -m pytest -q -x --timeout 120 --timeout-method thread tests/test_gpu_ops.py -k "scan" > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit 1
-OUT=r6nopk/race MIXES="ubench:1;skinny tn;attn" ONLY0="workspace,one segment,scan bwd C2 (du" REPS0=200 \
+OUT=${OUTD:-r6nopk}/race MIXES="ubench:1;skinny tn;attn" ONLY0="workspace,one segment,scan bwd C2 (du" REPS0=200 \
   timeout -k 10 600 bash tools/gpu/r6_race_bg.sh > $O/race.txt 2>&1 || { tail -5 $O/race.txt; exit 1; }
 grep -E "==|differ" $O/race.txt | cut -c1-160
 for i in 1 2 3; do
