@@ -16,10 +16,10 @@ workgroup, straight into the fp32 master gradient (no slabs, no reduce pass,
 no per-GEMM launch).  The rest of the queue is flushed by a callback at the
 end of the backward pass, before `loss.backward()` returns.
 
-The grouped launches can run on a side stream (SIDE_STREAM, off: no gain,
-and unsafe -- see below), so the next layer's data-gradient kernels fill the
-CUs the ~224 long tiles leave idle; the end-of-backward callback makes the
-caller's stream wait for it.
+The grouped launches can run on a side stream (SIDE_STREAM, off: no gain),
+so the next layer's data-gradient kernels fill the CUs the ~224 long tiles
+leave idle; the end-of-backward callback makes the caller's stream wait for
+it.
 
 Gradient semantics are autograd's: a parameter whose .grad is None gets a
 fresh gradient (or its data-parallel bucket view, mtts.dp), one whose .grad
@@ -60,10 +60,11 @@ MIN_GROUP_TILES = 128
 # run the grouped launches on a side stream (the layer's long tiles leave some
 # CUs idle for the next layer's data-gradient kernels); the end-of-backward
 # callback joins the streams
-# Off: no gain (31.8-32.0 ms either way, profiles/r05_c2_ab_side_stream.txt),
-# and NOT SAFE: it lets the grouped GEMM's MFMA waves share SIMDs with the
-# next layer's scan backward, whose packed-f32 results are then wrong from run
-# to run (round 6, profiles/r06_race_bg.txt).
+# Off: no gain (31.8-32.0 ms either way, profiles/r05_c2_ab_side_stream.txt).
+# It lets the grouped GEMM's MFMA waves share SIMDs with the next layer's scan
+# backward: the overlap that exposed the round-6 packed-f32 hazard there
+# (fixed, scan.hip kPackedHazard; profiles/r06_race_bg.txt).  The GPU test
+# suite does not run this path.
 SIDE_STREAM = False
 
 _depth = 0
@@ -183,9 +184,6 @@ def _side_stream(dev):
     i = dev.index if dev.index is not None else torch.cuda.current_device()
     st = _E.side.get(i)
     if st is None:
-        import warnings
-        warnings.warn("mtts.wgrad.SIDE_STREAM: grouped weight-gradient GEMMs overlap the scan backward, whose "
-                      "results then vary from run to run (profiles/r06_race_bg.txt)", RuntimeWarning)
         st = _E.side[i] = torch.cuda.Stream(device=i)
     return st
 

@@ -18,7 +18,7 @@ from mtts.optim import FusedClipAdam  # noqa: E402
 try:   # the deferred grouped weight gradients (round 5); DEFER=0 turns them off, SIDE=1 the side stream on
     from mtts import wgrad as _wg  # noqa: E402
     defer = lambda: _wg.deferred(os.environ.get("DEFER", "1") == "1")  # noqa: E731
-    _wg.SIDE_STREAM = os.environ.get("SIDE", "0") == "1"   # product default: off (unsafe, wgrad.py)
+    _wg.SIDE_STREAM = os.environ.get("SIDE", "0") == "1"   # product default: off (wgrad.py)
     if hasattr(_wg, "FUSE_BIAS"):
         _wg.FUSE_BIAS = os.environ.get("FUSE", "1") == "1"
 except ImportError:
