@@ -118,6 +118,16 @@ def probes(dev):
     def gemm():
         return [G.mm_nt(a1, w1), G.mm_tn(dyy, xx)]
     out["gemm nt/tn"] = gemm
+    gb1 = torch.randn(4096, device=dev)
+    pre1 = r(16384, 4096)
+
+    def gemm_gelu():
+        # the FFN epilogues: bias + GELU (packed-f32 polynomial beside the
+        # tile's MFMA waves) writing the pre-activation, and GELU backward
+        aux = torch.empty(16384, 4096, device=dev, dtype=bf)
+        y = G.mm_nt(a1, w1, bias=gb1, gelu_aux=aux)
+        return [y, aux, G.mm_nt(a1, w1, dgelu_aux=pre1)]
+    out["gemm gelu / dgelu epilogues"] = gemm_gelu
     # round-6 kernels: dropout forms, the codec token-table gradient, ragged
     # per-group column sums, the grouped TN weight-gradient launch
     from mtts import dropout as DO
