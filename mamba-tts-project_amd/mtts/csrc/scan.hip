@@ -1054,10 +1054,12 @@ __device__ __forceinline__ void wave_reduce_scatter32(float (&v)[32], float& o0,
 // the SIMD (another process's skinny TN GEMM or attention, or a bare MFMA
 // loop: tools/ubench/aggressor.hip) -- the carry pass's adjoint update and its
 // exp argument, the main pass's dA accumulation, all with an operand
-// broadcast from the per-wave dt / dy table.  Those few are plain ops
-// (an empty asm keeps the SLP vectorizer from re-packing them): 0 of 200
-// mismatching runs under every aggressor, 0.500 -> 0.524 ms per C2 backward.
-// Building the kernels with no packed f32 at all also fixes it, at 3.5x.
+// broadcast from a value just read from the per-wave dt / dy table.  The
+// carry pass does those as plain ops (an empty asm keeps the SLP vectorizer
+// from re-packing them); the main pass keeps its packed dA FMA but reads dt
+// through one plain v_mov_b32 copy.  0 of 200 mismatching runs under every
+// aggressor; C2 backward 0.500 -> 0.514 ms per call (0.524 with the main
+// pass's dA as plain ops too).  No packed f32 at all also fixes it, at 3.5x.
 // Backward pass 1 (only when L is split into K > 1 segments): for segments
 // k = 1..K-1, run the adjoint recurrence  dh_t = dy_t C_t + exp(dt_{t+1} A) dh_{t+1}
 // from zero carry-in at the segment end and record the carry leaving the
@@ -1556,12 +1558,10 @@ __global__ __launch_bounds__(kBlock, 2) void scan_bwd_kernel(const MttsScanBwdAr
           const f2 t1 = dh * e * hp;
           ddtA = __builtin_elementwise_fma(Anv[p], t1, ddtA);
           dus = __builtin_elementwise_fma(dh, bv, dus);
-          {   // plain ops, not re-packed (kPackedHazard)
-            float a0 = dA2[p][0], a1 = dA2[p][1];
-            a0 = fmaf(t1[0], dts, a0);
-            a1 = fmaf(t1[1], dts, a1);
-            asm volatile("" : "+v"(a0), "+v"(a1));
-            dA2[p] = f2{a0, a1};
+          {   // packed, but dt through a plain v_mov first (kPackedHazard)
+            float dtc;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(dtc) : "v"(dts));
+            dA2[p] = __builtin_elementwise_fma(t1, f2{dtc, dtc}, dA2[p]);
           }
           vB[p] = dh * dtus2;           // dB contribution (0 on lanes past `dim`)
           vC[p] = dys2 * hh[tl][p];     // dC contribution
